@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""bench.py -- SpMV GFLOP/s and HBM-roofline fraction on MI355X (BASELINE.json).
+
+Workload (config C3 of BASELINE.json, weak-scaled): every rank owns a
+2^20-row shard of a synthetic stripe-uniform CSR matrix with 2^20 columns and
+32 nonzeros per row (DESIGN.md §5 generator; rank r owns global rows
+[r*2^20, (r+1)*2^20)), fp64, and x (2^20 doubles) is broadcast from rank 0
+over RCCL once, before the timed region (inputs resident in HBM).  One step =
+one y = A_shard * x on every rank through the C ABI (hipspmv_exec_device) on
+torch's current stream.  value = 2 * nnz(all ranks) / (max over ranks of the
+per-step wall time).
+
+Also reported: the dominant kernel's roofline (algorithmic bytes per launch /
+its average duration from HIP events on the launch stream, against 8 TB/s),
+and the CPU baseline (the oracle's SoftwareSpMV restatement, 1 core, on the
+same shard) on rank 0 at N=1.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--kernel auto|vcache|csr_lane|csr_vector]
+                  [--mode ordered|fast] [--cpu-seconds S] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "spmv-vector-cache_amd"))
+import hipspmv as hs  # noqa: E402
+
+METRIC = "SpMV GFLOP/s (2·nnz/s) and % HBM roofline, 1M×1M CSR 32 nnz/row, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--kernel", default="auto", choices=list(hs.KERNELS))
+    p.add_argument("--mode", default="ordered", choices=["ordered", "fast"])
+    p.add_argument("--log2-rows", type=int, default=20)
+    p.add_argument("--log2-cols", type=int, default=20)
+    p.add_argument("--nnz-per-row", type=int, default=32)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-csv", default=None,
+                   help="rocprofv3 --pmc counter CSV (FETCH_SIZE, WRITE_SIZE) of this workload, for roofline.traffic")
+    return p.parse_args()
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def traffic_from_csv(path: str, kernel_substr: str):
+    """Per-launch HBM bytes from a rocprofv3 counter CSV, corrected as
+    MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KB) x 2 (gfx950 reports
+    half of wide streaming reads) + WRITE_SIZE (KB), averaged over dispatches."""
+    import csv
+    fetch, write = {}, {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel_substr not in row.get("Kernel_Name", ""):
+                continue
+            d = row.get("Dispatch_Id") or row.get("Correlation_Id")
+            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
+            if name == "FETCH_SIZE":
+                fetch[d] = val
+            elif name == "WRITE_SIZE":
+                write[d] = val
+    if not fetch:
+        return None
+    f = np.mean(list(fetch.values())) * 1024 * 2
+    w = np.mean(list(write.values())) * 1024 if write else 0.0
+    return float(f + w)
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            sys.exit(f"--gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    rows, cols, k = 1 << a.log2_rows, 1 << a.log2_cols, a.nnz_per_row
+    mode = hs.MODE_ORDERED if a.mode == "ordered" else hs.MODE_FAST
+    t0 = time.perf_counter()
+    rowptr, colind, vals = hs.gen_stripe_csr(rank * rows, rows, cols, k, 1, 2)
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols, device=local)
+    if a.kernel != "auto":
+        h.set_kernel(a.kernel)
+    kname = h.kernel_name(mode)
+    setup_s = time.perf_counter() - t0
+    nnz = int(colind.size)
+
+    # x: generated on rank 0, broadcast over RCCL (xGMI) -- the path's one exchange step
+    xd = torch.empty(cols, dtype=torch.float64, device=dev)
+    if rank == 0:
+        xd.copy_(torch.from_numpy(hs.gen_vector(cols, 3)))
+    bcast_us = None
+    if dist is not None:
+        for _ in range(3):
+            dist.broadcast(xd, src=0)
+        torch.cuda.synchronize()
+        dist.barrier()
+        tb = time.perf_counter()
+        reps = 10
+        for _ in range(reps):
+            dist.broadcast(xd, src=0)
+        torch.cuda.synchronize()
+        bcast_us = (time.perf_counter() - tb) / reps * 1e6
+    yd = torch.empty(rows, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        h.exec_device(xd, yd, beta=0, mode=mode, stream=stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    tw = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(a.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - tw
+    kern_ms = ev0.elapsed_time(ev1) / a.steps  # HIP events on the launch stream: kernel-only back-to-back
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    ms_per_step = wall_max / a.steps * 1e3
+
+    alg_bytes = h.stat("alg_bytes")  # 12*nnz + 4*(rows+1) + 8*cols + 8*rows per launch
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if a.traffic_csv and os.path.exists(a.traffic_csv):
+        traffic = traffic_from_csv(a.traffic_csv, "k_" + kname)
+
+    # parity guard on rank 0: the timed kernel's output vs the oracle (checker only)
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+        colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+        x = xd.cpu().numpy()
+        t_one, y_ref = oracle.time_spmv_csc_f64(colptr, rowind, cvals, x, rows, 1)
+        reps = max(1, int(a.cpu_seconds / max(t_one, 1e-6)))
+        t_avg, _ = oracle.time_spmv_csc_f64(colptr, rowind, cvals, x, rows, reps)
+        cpu = {"value": round(2.0 * nnz / t_avg / 1e9, 4), "unit": "GFLOP/s", "cores": 1, "kind": "port",
+               "sample": f"oracle SoftwareSpMV (CSC scatter) on rank 0's full shard: {rows} rows, {nnz} nnz, "
+                         f"x=U[-1,1), {reps + 1} execs, {t_avg * 1e3:.1f} ms each",
+               "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+        y = yd.cpu().numpy()
+        if mode == hs.MODE_ORDERED:
+            parity = "bit-exact" if y.tobytes() == y_ref.tobytes() else \
+                f"MISMATCH in {int(np.sum(y.view(np.uint64) != y_ref.view(np.uint64)))} rows"
+        else:
+            parity = f"max|dy|={float(np.max(np.abs(y - y_ref))):.3e}"
+
+    total_flops = 2.0 * nnz * world
+    value = total_flops / (ms_per_step * 1e-3) / 1e9
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GFLOP/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"C3 stripe-uniform CSR {rows}x{cols} per GPU, {k} nnz/row "
+                                   f"(rank r owns global rows [r*{rows},(r+1)*{rows}))",
+                       "rows_per_gpu": rows, "cols": cols, "nnz_per_gpu": nnz, "kernel": kname,
+                       "mode": a.mode, "parallelism": f"row-partition x{world}, x broadcast (RCCL) before timing"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "kernel": "k_" + kname, "alg_bytes_per_launch": alg_bytes,
+                         "kernel_us": round(kern_ms * 1e3, 3)},
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "x_bcast_us": None if bcast_us is None else round(bcast_us, 2),
+            "setup_s": round(setup_s, 3),
+        }
+        print(json.dumps(out), flush=True)
+    h.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+/*
+ * hipspmv.h -- C ABI of libhipspmv.so, the MI355X (gfx950) SpMV backend.
+ *
+ * This is the drop-in boundary behind the reference's plugin surface
+ * (maltanar/spmv-vector-cache, software/): the HIPSpMV backend
+ * (spmv-vector-cache_amd/host/HIPSpMV.cpp), registered in HWSpMVFactory, calls
+ * it in place of the FPGA register drivers (software/SpMVAccelerator*Driver.hpp)
+ * and the Chisel SpMVAccelerator* RTL they program.  Plain C types only: no HIP
+ * or torch types appear in any signature (streams travel as void*).
+ *
+ * Each entry point names the reference interface it replaces.  All functions
+ * return an int status (HIPSPMV_OK == 0) and never throw.
+ *
+ * Semantics follow SoftwareSpMV::exec (software/SoftwareSpMV.cpp:50-70):
+ *   beta == 1 : y_out = y_in + A*x  (the reference's "y +=", accumulating into
+ *               the caller's y, which main.cpp:220-222 zeroes beforehand)
+ *   beta == 0 : y_out = A*x         (accumulator starts at +0.0, i.e. the
+ *               reference's result on a zeroed y)
+ * Rows without nonzeros keep y_in (beta 1) or get +0.0 (beta 0).
+ *
+ * Modes:
+ *   HIPSPMV_MODE_ORDERED : every row is summed sequentially in ascending column
+ *                          order, products rounded before each add (no FMA):
+ *                          bit-identical to SoftwareSpMV for f64, and for u64.
+ *   HIPSPMV_MODE_FAST    : f64 row sums may be reassociated (wave-level
+ *                          segmented reduction); per row
+ *                          |y - y_ref| <= 2*len*2^-53*sum|a_ij*x_j| (+ |y_in|
+ *                          term for beta 1).  u64 stays bit-exact (mod 2^64).
+ *   HIPSPMV_MODE_AUTO    : ORDERED (the default used for parity).
+ */
+#ifndef HIPSPMV_H_
+#define HIPSPMV_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HIPSPMV_ABI_VERSION 1
+
+/* status codes */
+#define HIPSPMV_OK 0
+#define HIPSPMV_ERR_INVALID_ARG 1    /* null pointer, bad enum, bad size */
+#define HIPSPMV_ERR_INVALID_MATRIX 2 /* pointers not monotone, index out of range */
+#define HIPSPMV_ERR_HIP 3            /* a HIP runtime call failed (see hipspmv_last_error) */
+#define HIPSPMV_ERR_OOM 4            /* host or device allocation failed */
+#define HIPSPMV_ERR_UNSUPPORTED 5    /* kernel/option not applicable to this matrix */
+#define HIPSPMV_ERR_NO_DEVICE 6      /* requested device does not exist */
+#define HIPSPMV_ERR_KEY 7            /* unknown stat / option key */
+
+/* element types (SparseMatrix.h:6 SpMVData = double; u64 = StagedUIntOp
+ * semiring of chisel/frontend/SemiringOp.scala:74-92) */
+#define HIPSPMV_F64 0
+#define HIPSPMV_U64 1
+
+#define HIPSPMV_MODE_AUTO 0
+#define HIPSPMV_MODE_ORDERED 1
+#define HIPSPMV_MODE_FAST 2
+
+/* kernel selection (option "kernel") */
+#define HIPSPMV_KERNEL_AUTO 0
+#define HIPSPMV_KERNEL_VCACHE 1     /* x panels + y block staged in LDS; ordered */
+#define HIPSPMV_KERNEL_CSR_LANE 2   /* one lane per row over CSR; ordered */
+#define HIPSPMV_KERNEL_CSR_VECTOR 3 /* wave segmented DPP reduction over CSR; fast */
+
+typedef struct hipspmv_handle hipspmv_t;
+
+/* Replaces HardwareSpMV construction + setupRegs()
+ * (software/HardwareSpMV.cpp:8-25, HardwareSpMVNewCache.cpp:31-44): takes the
+ * SparseMatrix CSC arrays (SparseMatrix.h:36-58: indPtrs = colptr[cols+1],
+ * inds = row ids[nnz], nzData = 8-byte values[nnz]) and builds the device
+ * copy.  Bits 30-31 of the row ids (cold-miss-skip marks,
+ * SparseMatrix.cpp:52-90) are masked off; the caller's arrays are never
+ * modified and may be freed after the call.  device is a HIP ordinal. */
+int hipspmv_create(const uint32_t *colptr, const uint32_t *rowind, const void *vals, uint32_t rows,
+                   uint32_t cols, uint32_t nnz, int dtype, int device, hipspmv_t **out);
+
+/* Same, from CSR arrays (rowptr[rows+1], colind[nnz], vals[nnz]); colind need
+ * not be sorted within a row for FAST mode, and is summed in the given order
+ * for ORDERED mode.  Used for row-partitioned shards. */
+int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const void *vals, uint32_t rows,
+                       uint32_t cols, uint32_t nnz, int dtype, int device, hipspmv_t **out);
+
+/* Options: "kernel" (HIPSPMV_KERNEL_*), "mode" (default mode for exec with
+ * HIPSPMV_MODE_AUTO), "timing" (1 = record per-exec kernel events). */
+int hipspmv_set_option(hipspmv_t *h, const char *key, int64_t value);
+
+/* Replaces HardwareSpMV::exec()'s reset -> init -> regular -> write sequence
+ * (HardwareSpMVNewCache.cpp:78-101): copies x (cols elements) to the device,
+ * runs the kernel, copies y (rows elements) back, synchronously.  y is read
+ * first when beta == 1. */
+int hipspmv_exec(hipspmv_t *h, const void *x, void *y, int beta, int mode);
+
+/* Device-resident variant: d_x, d_y_in and d_y_out are device pointers on the
+ * handle's device; enqueued on `stream` (a hipStream_t, NULL = the handle's
+ * own stream) and returns without synchronising.  d_y_in may equal d_y_out
+ * and is ignored for beta == 0. */
+int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void *d_y_out, int beta, int mode,
+                        void *stream);
+
+/* Replaces HardwareSpMV::statInt/statKeys (HardwareSpMV.cpp:41-61,
+ * HardwareSpMVNewCache.cpp:130-204).  Keys: "rows" "cols" "nz" "dtype"
+ * "device" "kernel" (last kernel run) "setup_ns" "kernel_ns" (last timed
+ * exec) "h2d_ns" "d2h_ns" "alg_bytes" (beta 0) "alg_bytes_beta1" "flops"
+ * "device_bytes" "vcache_blocks" "vcache_panels" "vcache_rows_per_block"
+ * "max_row_len" "empty_rows" "execs". */
+int hipspmv_stat(hipspmv_t *h, const char *key, uint64_t *out);
+
+/* Name of the kernel that HIPSPMV_MODE `mode` would run (static string). */
+const char *hipspmv_kernel_name(hipspmv_t *h, int mode);
+
+int hipspmv_destroy(hipspmv_t *h);
+
+const char *hipspmv_strerror(int status);
+/* Text of the last HIP error seen by this thread (static per-thread buffer). */
+const char *hipspmv_last_error(void);
+int hipspmv_abi_version(void);
+int hipspmv_device_count(int *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

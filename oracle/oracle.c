@@ -1,0 +1,118 @@
+/*
+ * oracle.c -- CPU restatement of the reference SpMV hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h): the parity checker for tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg.  The product never
+ * links or calls it.  Built with -ffp-contract=off so that, like the
+ * reference's x86 build of SoftwareSpMV.cpp, every product is rounded before it
+ * is added (no FMA).
+ */
+#include "oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+/* software/SoftwareSpMV.cpp:50-70; hot loop :59-64. */
+void oracle_spmv_csc_f64(uint32_t cols, const uint32_t *colptr, const uint32_t *rowind,
+                         const double *vals, const double *x, double *y) {
+  for (uint32_t col = 0; col < cols; col++) {
+    const double inp = x[col];
+    for (uint32_t e = colptr[col]; e < colptr[col + 1]; e++) y[rowind[e]] += vals[e] * inp;
+  }
+}
+
+/* Same traversal; integer semiring of chisel/frontend/SemiringOp.scala:74-92
+ * (OpMulCombinatorial / OpAddCombinatorial at :35-46 feeding SystolicReg(64),
+ * which keeps the low 64 bits).  C unsigned arithmetic wraps mod 2^64. */
+void oracle_spmv_csc_u64(uint32_t cols, const uint32_t *colptr, const uint32_t *rowind,
+                         const uint64_t *vals, const uint64_t *x, uint64_t *y) {
+  for (uint32_t col = 0; col < cols; col++) {
+    const uint64_t inp = x[col];
+    for (uint32_t e = colptr[col]; e < colptr[col + 1]; e++) y[rowind[e]] += vals[e] * inp;
+  }
+}
+
+/* software/csr2csc.c:11-39: count column lengths, prefix-sum, scatter row by
+ * row (stable), then shift the pointers back by one. */
+void oracle_csr2csc(uint32_t n, uint32_t m, uint32_t nz, const uint64_t *a, const uint32_t *col_idx,
+                    const uint32_t *row_start, uint64_t *csc_a, uint32_t *row_idx, uint32_t *col_start) {
+  for (uint32_t i = 0; i <= m; i++) col_start[i] = 0;
+  for (uint32_t i = 0; i < nz; i++) col_start[col_idx[i] + 1]++;
+  for (uint32_t i = 0; i < m; i++) col_start[i + 1] += col_start[i];
+  for (uint32_t i = 0; i < n; i++) {
+    for (uint32_t j = row_start[i]; j < row_start[i + 1]; j++) {
+      const uint32_t k = col_idx[j];
+      const uint32_t l = col_start[k]++;
+      row_idx[l] = i;
+      if (a) csc_a[l] = a[j];
+    }
+  }
+  for (uint32_t i = m; i > 0; i--) col_start[i] = col_start[i - 1];
+  col_start[0] = 0;
+}
+
+/* software/SparseMatrix.cpp:52-90.  Row ids are masked with 0x3FFFFFFF before
+ * use, exactly as the reference does, so earlier markings do not alias. */
+void oracle_mark_row_starts(uint32_t rows, uint32_t nz, uint32_t *inds, int reverse, int shift) {
+  const uint32_t words = rows / 32 + 1;
+  uint32_t *seen = (uint32_t *)calloc(words, sizeof(uint32_t));
+  for (uint32_t n = 0; n < nz; n++) {
+    const uint32_t e = reverse ? nz - 1 - n : n;
+    const uint32_t row = inds[e] & 0x3FFFFFFFu;
+    const uint32_t w = row / 32, bit = 1u << (row % 32);
+    if ((seen[w] & bit) == 0) {
+      seen[w] |= bit;
+      inds[e] |= 1u << shift;
+    }
+  }
+  free(seen);
+}
+
+/* software/SparseMatrix.cpp:92-108: bit 31 = first touch of a row, bit 30 =
+ * last touch; the running count of rows "alive" between the two, maximised. */
+uint32_t oracle_max_alive(uint32_t rows, uint32_t nz, uint32_t *inds) {
+  oracle_mark_row_starts(rows, nz, inds, 0, 31);
+  oracle_mark_row_starts(rows, nz, inds, 1, 30);
+  uint32_t best = 0, alive = 0;
+  for (uint32_t e = 0; e < nz; e++) {
+    if (inds[e] & (1u << 31)) alive += 1;
+    if (inds[e] & (1u << 30)) alive -= 1;
+    if (alive > best) best = alive;
+  }
+  return best;
+}
+
+/* software/SparseMatrix.cpp:110-119.  The reference reads
+ * inds[colptr[c+1]-1] - inds[colptr[c]] with unsigned wrap-around, also for
+ * empty columns (where it reads the neighbouring column's entries); restated
+ * as is, but an empty column at c == 0 would read inds[-1], so that case
+ * contributes 0 here (documented in DESIGN.md). */
+uint32_t oracle_max_col_span(uint32_t cols, const uint32_t *colptr, const uint32_t *inds) {
+  uint32_t best = 0;
+  for (uint32_t c = 0; c < cols; c++) {
+    if (colptr[c + 1] == 0) continue;
+    const uint32_t span = inds[colptr[c + 1] - 1] - inds[colptr[c]];
+    if (span > best) best = span;
+  }
+  return best;
+}
+
+/* software/SparseMatrix.cpp:121-125 */
+void oracle_clear_row_markings(uint32_t nz, uint32_t *inds, uint32_t mask) {
+  for (uint32_t e = 0; e < nz; e++) inds[e] &= mask;
+}
+
+double oracle_time_spmv_csc_f64(uint32_t rows, uint32_t cols, const uint32_t *colptr, const uint32_t *rowind,
+                                const double *vals, const double *x, double *y, int reps) {
+  double total = 0.0;
+  for (int r = 0; r < reps; r++) {
+    memset(y, 0, sizeof(double) * rows);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    oracle_spmv_csc_f64(cols, colptr, rowind, vals, x, y);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    total += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+  }
+  return reps > 0 ? total / reps : 0.0;
+}

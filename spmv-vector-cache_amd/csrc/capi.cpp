@@ -1,0 +1,402 @@
+// libhipspmv.so: the C ABI of include/hipspmv.h.
+//
+// A handle owns the device copy of one matrix (CSR plus, when eligible, the
+// vcache segment layout), the HIP stream it runs on by default, the staging
+// buffers of the host-pointer exec path and its statistics.  Nothing here
+// throws across the ABI: every entry point catches and returns a status.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "hipspmv.h"
+#include "hipspmv_internal.h"
+#include "kernels.h"
+
+using namespace hipspmv;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct DeviceGuard {  // restore the caller's current device on scope exit
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int hip_fail(hipError_t e, const char* what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return e == hipErrorOutOfMemory ? HIPSPMV_ERR_OOM : HIPSPMV_ERR_HIP;
+}
+
+#define HIP_TRY(call)                                        \
+  do {                                                       \
+    hipError_t e_ = (call);                                  \
+    if (e_ != hipSuccess) return hip_fail(e_, #call);        \
+  } while (0)
+
+template <typename T>
+int dev_upload(T** dst, const T* src, size_t n, uint64_t& bytes) {
+  *dst = nullptr;
+  const size_t sz = sizeof(T) * (n ? n : 1);
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(dst), sz));
+  bytes += sz;
+  if (n) HIP_TRY(hipMemcpy(*dst, src, sizeof(T) * n, hipMemcpyHostToDevice));
+  return HIPSPMV_OK;
+}
+
+uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+}  // namespace
+
+struct hipspmv_handle {
+  int device = 0, dtype = HIPSPMV_F64;
+  uint32_t rows = 0, cols = 0, nnz = 0;
+  hipStream_t stream = nullptr;
+  uint32_t *d_rowptr = nullptr, *d_colind = nullptr, *d_groups = nullptr;
+  uint64_t* d_vals = nullptr;
+  uint32_t ngroups = 0;
+  bool vc_ok = false;
+  uint32_t *d_seg = nullptr, *d_code = nullptr;
+  uint64_t* d_evals = nullptr;
+  uint32_t vc_rows_per_block = 0, vc_nblocks = 0, vc_npanels = 0, vc_npad = 0, vc_max_seg = 0;
+  void *d_x = nullptr, *d_y = nullptr;
+  int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
+  uint64_t setup_ns = 0, kernel_ns = 0, h2d_ns = 0, d2h_ns = 0, execs = 0, device_bytes = 0;
+  uint32_t max_row_len = 0, empty_rows = 0;
+  int last_kernel = 0;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool pending = false;  // kernel events recorded by exec_device, not yet read
+};
+
+static void release(hipspmv_t* h) {
+  if (!h) return;
+  DeviceGuard g(h->device);
+  void* ptrs[] = {h->d_rowptr, h->d_colind, h->d_groups, h->d_vals, h->d_seg, h->d_code, h->d_evals, h->d_x, h->d_y};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  for (hipEvent_t e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+static int finish_create(hipspmv_t* h, HostCSR& a) {
+  DeviceGuard g(h->device);
+  HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  for (auto& e : h->ev) HIP_TRY(hipEventCreate(&e));
+  for (uint32_t r = 0; r < a.rows; ++r) {
+    const uint32_t len = a.rowptr[r + 1] - a.rowptr[r];
+    h->max_row_len = len > h->max_row_len ? len : h->max_row_len;
+    h->empty_rows += len == 0;
+  }
+  int st;
+  if ((st = dev_upload(&h->d_rowptr, a.rowptr.data(), a.rowptr.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&h->d_colind, a.colind.data(), a.colind.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&h->d_vals, a.vals.data(), a.vals.size(), h->device_bytes))) return st;
+  std::vector<uint32_t> groups;
+  build_row_groups(a, groups);
+  h->ngroups = (uint32_t)groups.size() - 1;
+  if ((st = dev_upload(&h->d_groups, groups.data(), groups.size(), h->device_bytes))) return st;
+  h->vc_ok = vcache_eligible(a);
+  if (h->vc_ok) {
+    VcacheLayout L;
+    build_vcache(a, L);
+    h->vc_rows_per_block = L.rows_per_block;
+    h->vc_nblocks = L.nblocks;
+    h->vc_npanels = L.npanels;
+    h->vc_npad = L.npad;
+    h->vc_max_seg = L.max_seg;
+    if ((st = dev_upload(&h->d_seg, L.seg.data(), L.seg.size(), h->device_bytes))) return st;
+    if ((st = dev_upload(&h->d_code, L.code.data(), L.code.size(), h->device_bytes))) return st;
+    if ((st = dev_upload(&h->d_evals, L.vals.data(), L.vals.size(), h->device_bytes))) return st;
+  }
+  return HIPSPMV_OK;
+}
+
+template <typename Build>
+static int create_common(uint32_t rows, uint32_t cols, uint32_t nnz, int dtype, int device, hipspmv_t** out,
+                         Build build) {
+  if (!out) return HIPSPMV_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (dtype != HIPSPMV_F64 && dtype != HIPSPMV_U64) return HIPSPMV_ERR_INVALID_ARG;
+  if (rows == 0 || cols == 0) return HIPSPMV_ERR_INVALID_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    g_last_error = "no HIP device";
+    return HIPSPMV_ERR_NO_DEVICE;
+  }
+  if (device < 0 || device >= ndev) return HIPSPMV_ERR_NO_DEVICE;
+  const uint64_t t0 = now_ns();
+  HostCSR a;
+  std::string why;
+  int st = build(a, why);
+  if (st) {
+    g_last_error = why;
+    return st;
+  }
+  hipspmv_t* h = new hipspmv_t;
+  h->device = device;
+  h->dtype = dtype;
+  h->rows = rows;
+  h->cols = cols;
+  h->nnz = nnz;
+  st = finish_create(h, a);
+  if (st) {
+    release(h);
+    return st;
+  }
+  h->setup_ns = now_ns() - t0;
+  *out = h;
+  return HIPSPMV_OK;
+}
+
+// Which kernel runs for `mode` (HIPSPMV_KERNEL_*), or a negative status.
+static int choose_kernel(const hipspmv_t* h, int mode) {
+  if (mode == HIPSPMV_MODE_AUTO) mode = h->mode_opt;
+  if (mode != HIPSPMV_MODE_ORDERED && mode != HIPSPMV_MODE_FAST) return -HIPSPMV_ERR_INVALID_ARG;
+  const bool exact_any = h->dtype == HIPSPMV_U64;  // integer sums are order-independent
+  switch (h->kernel_opt) {
+    case HIPSPMV_KERNEL_VCACHE:
+      return h->vc_ok ? HIPSPMV_KERNEL_VCACHE : -HIPSPMV_ERR_UNSUPPORTED;
+    case HIPSPMV_KERNEL_CSR_LANE:
+      return HIPSPMV_KERNEL_CSR_LANE;
+    case HIPSPMV_KERNEL_CSR_VECTOR:
+      return (mode == HIPSPMV_MODE_FAST || exact_any) ? HIPSPMV_KERNEL_CSR_VECTOR : -HIPSPMV_ERR_UNSUPPORTED;
+    case HIPSPMV_KERNEL_AUTO:
+      break;
+    default:
+      return -HIPSPMV_ERR_INVALID_ARG;
+  }
+  // The LDS vector cache pays when each swept x element feeds enough
+  // nonzeros; it is ordered, so it serves both modes.
+  if (h->vc_ok && (uint64_t)h->nnz * 16 >= (uint64_t)h->vc_nblocks * h->cols) return HIPSPMV_KERNEL_VCACHE;
+  return (mode == HIPSPMV_MODE_FAST || exact_any) ? HIPSPMV_KERNEL_CSR_VECTOR : HIPSPMV_KERNEL_CSR_LANE;
+}
+
+static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in, void* d_y_out, int beta,
+                  hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (kernel == HIPSPMV_KERNEL_VCACHE) {
+    VcacheArgs a{h->d_seg, h->d_code, h->d_evals, d_x, d_y_in, d_y_out, h->rows, h->cols, h->vc_rows_per_block,
+                 h->vc_npanels, h->vc_npad, h->nnz - 1, h->vc_nblocks, beta};
+    e = launch_vcache(h->dtype, a, s);
+  } else {
+    CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
+    e = kernel == HIPSPMV_KERNEL_CSR_LANE ? launch_csr_lane(h->dtype, a, s) : launch_csr_vector(h->dtype, a, s);
+  }
+  if (e != hipSuccess) return hip_fail(e, "kernel launch");
+  h->last_kernel = kernel;
+  h->execs++;
+  return HIPSPMV_OK;
+}
+
+static int resolve_pending(hipspmv_t* h) {
+  if (!h->pending) return HIPSPMV_OK;
+  DeviceGuard g(h->device);
+  HIP_TRY(hipEventSynchronize(h->ev[2]));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, h->ev[1], h->ev[2]));
+  h->kernel_ns = (uint64_t)(ms * 1e6);
+  h->pending = false;
+  return HIPSPMV_OK;
+}
+
+extern "C" {
+
+int hipspmv_create(const uint32_t* colptr, const uint32_t* rowind, const void* vals, uint32_t rows, uint32_t cols,
+                   uint32_t nnz, int dtype, int device, hipspmv_t** out) {
+  if (!colptr || (nnz && (!rowind || !vals))) return HIPSPMV_ERR_INVALID_ARG;
+  try {
+    return create_common(rows, cols, nnz, dtype, device, out, [&](HostCSR& a, std::string& why) {
+      return csc_to_csr(colptr, rowind, vals, rows, cols, nnz, a, why);
+    });
+  } catch (const std::bad_alloc&) {
+    return HIPSPMV_ERR_OOM;
+  } catch (...) {
+    return HIPSPMV_ERR_INVALID_ARG;
+  }
+}
+
+int hipspmv_create_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, uint32_t rows,
+                       uint32_t cols, uint32_t nnz, int dtype, int device, hipspmv_t** out) {
+  if (!rowptr || (nnz && (!colind || !vals))) return HIPSPMV_ERR_INVALID_ARG;
+  try {
+    return create_common(rows, cols, nnz, dtype, device, out, [&](HostCSR& a, std::string& why) {
+      return copy_csr(rowptr, colind, vals, rows, cols, nnz, a, why);
+    });
+  } catch (const std::bad_alloc&) {
+    return HIPSPMV_ERR_OOM;
+  } catch (...) {
+    return HIPSPMV_ERR_INVALID_ARG;
+  }
+}
+
+int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
+  if (!h || !key) return HIPSPMV_ERR_INVALID_ARG;
+  const std::string k(key);
+  if (k == "kernel") {
+    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_CSR_VECTOR) return HIPSPMV_ERR_INVALID_ARG;
+    h->kernel_opt = (int)value;
+  } else if (k == "mode") {
+    if (value != HIPSPMV_MODE_ORDERED && value != HIPSPMV_MODE_FAST) return HIPSPMV_ERR_INVALID_ARG;
+    h->mode_opt = (int)value;
+  } else if (k == "timing") {
+    h->timing = value ? 1 : 0;
+  } else {
+    return HIPSPMV_ERR_KEY;
+  }
+  return HIPSPMV_OK;
+}
+
+int hipspmv_exec(hipspmv_t* h, const void* x, void* y, int beta, int mode) {
+  if (!h || !x || !y || (beta != 0 && beta != 1)) return HIPSPMV_ERR_INVALID_ARG;
+  const int kernel = choose_kernel(h, mode);
+  if (kernel < 0) return -kernel;
+  try {
+    DeviceGuard g(h->device);
+    const size_t bx = 8ull * h->cols, by = 8ull * h->rows;
+    if (!h->d_x) {
+      HIP_TRY(hipMalloc(&h->d_x, bx));
+      h->device_bytes += bx;
+    }
+    if (!h->d_y) {
+      HIP_TRY(hipMalloc(&h->d_y, by));
+      h->device_bytes += by;
+    }
+    hipStream_t s = h->stream;
+    HIP_TRY(hipEventRecord(h->ev[0], s));
+    HIP_TRY(hipMemcpyAsync(h->d_x, x, bx, hipMemcpyHostToDevice, s));
+    if (beta) HIP_TRY(hipMemcpyAsync(h->d_y, y, by, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(h->ev[1], s));
+    int st = launch(h, kernel, h->d_x, h->d_y, h->d_y, beta, s);
+    if (st) return st;
+    HIP_TRY(hipEventRecord(h->ev[2], s));
+    HIP_TRY(hipMemcpyAsync(y, h->d_y, by, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(h->ev[3], s));
+    HIP_TRY(hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+    h->h2d_ns = (uint64_t)(ms * 1e6);
+    HIP_TRY(hipEventElapsedTime(&ms, h->ev[1], h->ev[2]));
+    h->kernel_ns = (uint64_t)(ms * 1e6);
+    HIP_TRY(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
+    h->d2h_ns = (uint64_t)(ms * 1e6);
+    h->pending = false;
+    return HIPSPMV_OK;
+  } catch (...) {
+    return HIPSPMV_ERR_OOM;
+  }
+}
+
+int hipspmv_exec_device(hipspmv_t* h, const void* d_x, const void* d_y_in, void* d_y_out, int beta, int mode,
+                        void* stream) {
+  if (!h || !d_x || !d_y_out || (beta != 0 && beta != 1) || (beta && !d_y_in)) return HIPSPMV_ERR_INVALID_ARG;
+  const int kernel = choose_kernel(h, mode);
+  if (kernel < 0) return -kernel;
+  DeviceGuard g(h->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  if (h->timing) HIP_TRY(hipEventRecord(h->ev[1], s));
+  int st = launch(h, kernel, d_x, beta ? d_y_in : d_y_out, d_y_out, beta, s);
+  if (st) return st;
+  if (h->timing) {
+    HIP_TRY(hipEventRecord(h->ev[2], s));
+    h->pending = true;
+  }
+  return HIPSPMV_OK;
+}
+
+int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
+  if (!h || !key || !out) return HIPSPMV_ERR_INVALID_ARG;
+  const std::string k(key);
+  const uint64_t alg = 12ull * h->nnz + 4ull * (h->rows + 1ull) + 8ull * h->cols + 8ull * h->rows;
+  if (k == "rows") *out = h->rows;
+  else if (k == "cols") *out = h->cols;
+  else if (k == "nz") *out = h->nnz;
+  else if (k == "dtype") *out = (uint64_t)h->dtype;
+  else if (k == "device") *out = (uint64_t)h->device;
+  else if (k == "kernel") *out = (uint64_t)h->last_kernel;
+  else if (k == "setup_ns") *out = h->setup_ns;
+  else if (k == "kernel_ns") {
+    int st = resolve_pending(h);
+    if (st) return st;
+    *out = h->kernel_ns;
+  } else if (k == "h2d_ns") *out = h->h2d_ns;
+  else if (k == "d2h_ns") *out = h->d2h_ns;
+  else if (k == "alg_bytes") *out = alg;
+  else if (k == "alg_bytes_beta1") *out = alg + 8ull * h->rows;
+  else if (k == "flops") *out = 2ull * h->nnz;
+  else if (k == "device_bytes") *out = h->device_bytes;
+  else if (k == "vcache_blocks") *out = h->vc_nblocks;
+  else if (k == "vcache_panels") *out = h->vc_npanels;
+  else if (k == "vcache_rows_per_block") *out = h->vc_rows_per_block;
+  else if (k == "vcache_max_segment") *out = h->vc_max_seg;
+  else if (k == "vcache_eligible") *out = h->vc_ok;
+  else if (k == "row_groups") *out = h->ngroups;
+  else if (k == "max_row_len") *out = h->max_row_len;
+  else if (k == "empty_rows") *out = h->empty_rows;
+  else if (k == "execs") *out = h->execs;
+  else return HIPSPMV_ERR_KEY;
+  return HIPSPMV_OK;
+}
+
+const char* hipspmv_kernel_name(hipspmv_t* h, int mode) {
+  if (!h) return "invalid";
+  switch (choose_kernel(h, mode)) {
+    case HIPSPMV_KERNEL_VCACHE: return "vcache";
+    case HIPSPMV_KERNEL_CSR_LANE: return "csr_lane";
+    case HIPSPMV_KERNEL_CSR_VECTOR: return "csr_vector";
+    default: return "unsupported";
+  }
+}
+
+int hipspmv_destroy(hipspmv_t* h) {
+  if (!h) return HIPSPMV_ERR_INVALID_ARG;
+  release(h);
+  return HIPSPMV_OK;
+}
+
+const char* hipspmv_strerror(int status) {
+  switch (status) {
+    case HIPSPMV_OK: return "ok";
+    case HIPSPMV_ERR_INVALID_ARG: return "invalid argument";
+    case HIPSPMV_ERR_INVALID_MATRIX: return "invalid matrix";
+    case HIPSPMV_ERR_HIP: return "HIP runtime error";
+    case HIPSPMV_ERR_OOM: return "out of memory";
+    case HIPSPMV_ERR_UNSUPPORTED: return "unsupported kernel/option for this matrix";
+    case HIPSPMV_ERR_NO_DEVICE: return "no such device";
+    case HIPSPMV_ERR_KEY: return "unknown key";
+    default: return "unknown status";
+  }
+}
+
+const char* hipspmv_last_error(void) { return g_last_error.c_str(); }
+
+int hipspmv_abi_version(void) { return HIPSPMV_ABI_VERSION; }
+
+int hipspmv_device_count(int* count) {
+  if (!count) return HIPSPMV_ERR_INVALID_ARG;
+  *count = 0;
+  hipError_t e = hipGetDeviceCount(count);
+  if (e == hipErrorNoDevice) {
+    *count = 0;
+    return HIPSPMV_OK;
+  }
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  return HIPSPMV_OK;
+}
+
+}  // extern "C"

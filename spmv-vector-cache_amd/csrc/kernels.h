@@ -1,0 +1,37 @@
+// Kernel launch interface used by capi.cpp (internal).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace hipspmv {
+
+struct VcacheArgs {
+  const uint32_t* seg;
+  const uint32_t* code;
+  const void* vals;
+  const void* x;
+  const void* y_in;
+  void* y_out;
+  uint32_t rows, cols, rows_per_block, npanels, npad, last, nblocks;
+  int beta;
+};
+
+struct CsrArgs {
+  const uint32_t* rowptr;
+  const uint32_t* colind;
+  const void* vals;
+  const void* x;
+  const void* y_in;
+  void* y_out;
+  const uint32_t* groups;
+  uint32_t rows, ngroups;
+  int beta;
+};
+
+hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);
+hipError_t launch_csr_lane(int dtype, const CsrArgs& a, hipStream_t s);
+hipError_t launch_csr_vector(int dtype, const CsrArgs& a, hipStream_t s);
+
+}  // namespace hipspmv

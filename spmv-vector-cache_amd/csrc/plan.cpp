@@ -1,0 +1,171 @@
+// Host-side planning for libhipspmv: CSC -> CSR transpose, validation, and the
+// device layouts each kernel reads.
+#include <algorithm>
+#include <cstring>
+
+#include "hipspmv.h"
+#include "hipspmv_internal.h"
+
+namespace hipspmv {
+
+namespace {
+constexpr uint32_t kRowMask = 0x3FFFFFFFu;  // SparseMatrix.cpp:64,77 cold-miss-skip bits
+}
+
+// Stable counting-sort transpose, the algorithm of software/csr2csc.c:11-39
+// applied to the CSC arrays (so it yields CSR with column ids ascending within
+// each row, and duplicate entries in their CSC order -- exactly the order in
+// which SoftwareSpMV::exec (SoftwareSpMV.cpp:59-64) adds them into y[row]).
+int csc_to_csr(const uint32_t* colptr, const uint32_t* rowind, const void* vals, uint32_t rows, uint32_t cols,
+               uint32_t nnz, HostCSR& out, std::string& why) {
+  if (colptr[0] != 0 || colptr[cols] != nnz) {
+    why = "colptr[0] must be 0 and colptr[cols] must equal nnz";
+    return HIPSPMV_ERR_INVALID_MATRIX;
+  }
+  for (uint32_t c = 0; c < cols; ++c)
+    if (colptr[c + 1] < colptr[c]) {
+      why = "colptr not monotone at column " + std::to_string(c);
+      return HIPSPMV_ERR_INVALID_MATRIX;
+    }
+  out.rows = rows;
+  out.cols = cols;
+  out.nnz = nnz;
+  out.rowptr.assign((size_t)rows + 1, 0);
+  for (uint32_t e = 0; e < nnz; ++e) {
+    const uint32_t r = rowind[e] & kRowMask;
+    if (r >= rows) {
+      why = "row id " + std::to_string(r) + " out of range at element " + std::to_string(e);
+      return HIPSPMV_ERR_INVALID_MATRIX;
+    }
+    out.rowptr[r + 1]++;
+  }
+  for (uint32_t r = 0; r < rows; ++r) out.rowptr[r + 1] += out.rowptr[r];
+  out.colind.resize(nnz);
+  out.vals.resize(nnz);
+  std::vector<uint32_t> cursor(out.rowptr.begin(), out.rowptr.end() - 1);
+  const uint64_t* v = static_cast<const uint64_t*>(vals);
+  for (uint32_t c = 0; c < cols; ++c) {
+    for (uint32_t e = colptr[c]; e < colptr[c + 1]; ++e) {
+      const uint32_t d = cursor[rowind[e] & kRowMask]++;
+      out.colind[d] = c;
+      out.vals[d] = v[e];
+    }
+  }
+  return HIPSPMV_OK;
+}
+
+int copy_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, uint32_t rows, uint32_t cols,
+             uint32_t nnz, HostCSR& out, std::string& why) {
+  if (rowptr[0] != 0 || rowptr[rows] != nnz) {
+    why = "rowptr[0] must be 0 and rowptr[rows] must equal nnz";
+    return HIPSPMV_ERR_INVALID_MATRIX;
+  }
+  for (uint32_t r = 0; r < rows; ++r)
+    if (rowptr[r + 1] < rowptr[r]) {
+      why = "rowptr not monotone at row " + std::to_string(r);
+      return HIPSPMV_ERR_INVALID_MATRIX;
+    }
+  for (uint32_t e = 0; e < nnz; ++e)
+    if (colind[e] >= cols) {
+      why = "column id " + std::to_string(colind[e]) + " out of range at element " + std::to_string(e);
+      return HIPSPMV_ERR_INVALID_MATRIX;
+    }
+  out.rows = rows;
+  out.cols = cols;
+  out.nnz = nnz;
+  out.rowptr.assign(rowptr, rowptr + (size_t)rows + 1);
+  out.colind.assign(colind, colind + nnz);
+  out.vals.resize(nnz);
+  if (nnz) std::memcpy(out.vals.data(), vals, sizeof(uint64_t) * nnz);
+  return HIPSPMV_OK;
+}
+
+static uint32_t vcache_rows_per_block(uint32_t rows) {
+  // One block per CU when the rows allow it (256 CUs on MI355X), never more
+  // than the LDS y budget; at least 64 rows so tiny matrices use few blocks.
+  uint32_t r = (rows + 255) / 256;
+  r = std::max<uint32_t>(r, 64);
+  return std::min<uint32_t>(r, kVcRows);
+}
+
+bool vcache_eligible(const HostCSR& a) {
+  if (a.cols < 2 || a.rows == 0 || a.nnz == 0) return false;
+  const uint32_t npanels = (a.cols + kVcPanel - 1) / kVcPanel;
+  const uint32_t npad = (npanels + kVcDepth - 1) / kVcDepth * kVcDepth;
+  if (npad + 1 > (uint32_t)kVcSegMax) return false;
+  // panel order must equal each row's summation order: columns non-decreasing
+  for (uint32_t r = 0; r < a.rows; ++r)
+    for (uint32_t e = a.rowptr[r] + 1; e < a.rowptr[r + 1]; ++e)
+      if (a.colind[e] < a.colind[e - 1]) return false;
+  return true;
+}
+
+// Entries of row block b that fall into column panel p form segment (b, p),
+// ordered by (row, column); each row's entries keep their CSR order, so a
+// thread that walks a row run in a segment, and the panels in ascending
+// order, adds the row's products in ascending column order (ordered mode).
+void build_vcache(const HostCSR& a, VcacheLayout& out) {
+  const uint32_t R = vcache_rows_per_block(a.rows);
+  const uint32_t nb = (a.rows + R - 1) / R;
+  const uint32_t np = (a.cols + kVcPanel - 1) / kVcPanel;
+  const uint32_t npad = (np + kVcDepth - 1) / kVcDepth * kVcDepth;
+  out.rows_per_block = R;
+  out.nblocks = nb;
+  out.npanels = np;
+  out.npad = npad;
+  out.seg.assign((size_t)nb * (npad + 1), 0);
+  out.code.resize(a.nnz);
+  out.vals.resize(a.nnz);
+  out.max_seg = 0;
+  std::vector<uint32_t> cnt(np + 1);
+  uint32_t base = 0;
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint32_t r0 = b * R, r1 = std::min(a.rows, r0 + R);
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (uint32_t e = a.rowptr[r0]; e < a.rowptr[r1]; ++e) cnt[a.colind[e] / kVcPanel + 1]++;
+    for (uint32_t p = 0; p < np; ++p) {
+      out.max_seg = std::max(out.max_seg, cnt[p + 1]);
+      cnt[p + 1] += cnt[p];
+    }
+    uint32_t* seg = &out.seg[(size_t)b * (npad + 1)];
+    for (uint32_t p = 0; p <= npad; ++p) seg[p] = base + cnt[std::min(p, np)];
+    std::vector<uint32_t> cur(cnt.begin(), cnt.end() - 1);
+    for (uint32_t r = r0; r < r1; ++r) {
+      uint32_t prev_d = UINT32_MAX, prev_p = UINT32_MAX;
+      for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+        const uint32_t c = a.colind[e], p = c / kVcPanel;
+        const uint32_t d = base + cur[p]++;
+        uint32_t code = (c - p * kVcPanel) | ((r - r0) << 16);
+        if (p == prev_p && d == prev_d + 1) {  // same row, same segment, adjacent: extend the run
+          code |= kVcCont;
+          out.code[prev_d] |= kVcMore;
+        }
+        out.code[d] = code;
+        out.vals[d] = a.vals[e];
+        prev_d = d;
+        prev_p = p;
+      }
+    }
+    base += cnt[np];
+  }
+}
+
+// Greedy row groups: consecutive rows while the group stays within
+// kCvGroupNnz nonzeros and kCvGroupRows rows; a longer row is a group alone.
+void build_row_groups(const HostCSR& a, std::vector<uint32_t>& groups) {
+  groups.clear();
+  uint32_t r = 0;
+  while (r < a.rows) {
+    groups.push_back(r);
+    const uint32_t start = a.rowptr[r];
+    uint32_t n = 0;
+    while (r < a.rows && n < (uint32_t)kCvGroupRows && a.rowptr[r + 1] - start <= (uint32_t)kCvGroupNnz) {
+      ++r;
+      ++n;
+    }
+    if (n == 0) ++r;  // a long row: its own group
+  }
+  groups.push_back(a.rows);
+}
+
+}  // namespace hipspmv

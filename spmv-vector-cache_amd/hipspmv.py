@@ -1,0 +1,289 @@
+"""Python binding of the MI355X SpMV backend (ctypes over the C ABI).
+
+Thin plumbing for bench.py and tests/: the product is libhipspmv.so (HIP
+kernels + include/hipspmv.h) and libspmvhost.so (the C++ restatement of the
+reference plugin surface).  This module only marshals numpy arrays / torch
+tensors into the C ABI.  There is no CPU fallback: if the shared libraries
+are missing, ``load_hipspmv`` raises.
+
+PyTorch is imported first on purpose: it loads its HIP runtime
+(libamdhip64.so.7) and libhipspmv.so, which needs the same soname, then binds
+to that one instance, so device pointers and streams are shared.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+
+try:  # torch first (see module docstring); absent torch is fine for host-only use
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover
+    torch = None
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+REPO_DIR = os.path.dirname(PKG_DIR)
+HEADER = os.path.join(REPO_DIR, "include", "hipspmv.h")
+
+F64, U64 = 0, 1
+MODE_AUTO, MODE_ORDERED, MODE_FAST = 0, 1, 2
+KERNEL_AUTO, KERNEL_VCACHE, KERNEL_CSR_LANE, KERNEL_CSR_VECTOR = 0, 1, 2, 3
+KERNELS = {"auto": KERNEL_AUTO, "vcache": KERNEL_VCACHE, "csr_lane": KERNEL_CSR_LANE,
+           "csr_vector": KERNEL_CSR_VECTOR}
+STATUS = {0: "ok", 1: "invalid argument", 2: "invalid matrix", 3: "HIP error", 4: "out of memory",
+          5: "unsupported", 6: "no device", 7: "unknown key"}
+
+_u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+
+_hip = None
+_host = None
+
+
+class HipSpMVError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        detail = ""
+        if _hip is not None:
+            detail = _hip.hipspmv_last_error().decode(errors="replace")
+        super().__init__(f"{what}: {STATUS.get(status, status)}" + (f" ({detail})" if detail else ""))
+        self.status = status
+
+
+def build(force: bool = False) -> None:
+    """Compile libhipspmv.so / libspmvhost.so / spmvbench in-tree (make)."""
+    libs = [os.path.join(LIB_DIR, n) for n in ("libhipspmv.so", "libspmvhost.so", "spmvbench")]
+    if force or not all(os.path.exists(p) for p in libs):
+        subprocess.run(["make", "-C", PKG_DIR, "-j8"], check=True)
+
+
+def declared_symbols() -> list[str]:
+    """Function names declared in include/hipspmv.h."""
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(hipspmv_[a-z_0-9]+)\s*\(", text)))
+
+
+def load_hipspmv() -> C.CDLL:
+    global _hip
+    if _hip is not None:
+        return _hip
+    path = os.path.join(LIB_DIR, "libhipspmv.so")
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} missing: build with `make -C {PKG_DIR}` (no CPU fallback exists)")
+    lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    vp = C.c_void_p
+    lib.hipspmv_create.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.POINTER(vp)]
+    lib.hipspmv_create_csr.argtypes = lib.hipspmv_create.argtypes
+    lib.hipspmv_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
+    lib.hipspmv_exec.argtypes = [vp, vp, vp, C.c_int, C.c_int]
+    lib.hipspmv_exec_device.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, vp]
+    lib.hipspmv_stat.argtypes = [vp, C.c_char_p, C.POINTER(C.c_uint64)]
+    lib.hipspmv_kernel_name.argtypes = [vp, C.c_int]
+    lib.hipspmv_kernel_name.restype = C.c_char_p
+    lib.hipspmv_destroy.argtypes = [vp]
+    lib.hipspmv_strerror.argtypes = [C.c_int]
+    lib.hipspmv_strerror.restype = C.c_char_p
+    lib.hipspmv_last_error.argtypes = []
+    lib.hipspmv_last_error.restype = C.c_char_p
+    lib.hipspmv_abi_version.argtypes = []
+    lib.hipspmv_device_count.argtypes = [C.POINTER(C.c_int)]
+    for name in ("hipspmv_create", "hipspmv_create_csr", "hipspmv_set_option", "hipspmv_exec",
+                 "hipspmv_exec_device", "hipspmv_stat", "hipspmv_destroy", "hipspmv_abi_version",
+                 "hipspmv_device_count"):
+        getattr(lib, name).restype = C.c_int
+    _hip = lib
+    return lib
+
+
+def load_host() -> C.CDLL:
+    global _host
+    if _host is not None:
+        return _host
+    load_hipspmv()
+    path = os.path.join(LIB_DIR, "libspmvhost.so")
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} missing: build with `make -C {PKG_DIR}`")
+    lib = C.CDLL(path)
+    lib.spmvhost_gen_stripe_csr.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
+                                            C.c_uint64, _u32p, _u32p, _f64p]
+    lib.spmvhost_gen_stripe_csr.restype = None
+    lib.spmvhost_gen_vector.argtypes = [C.c_uint64, C.c_uint64, _f64p]
+    lib.spmvhost_gen_vector.restype = None
+    lib.spmvhost_splitmix64_at.argtypes = [C.c_uint64, C.c_uint64]
+    lib.spmvhost_splitmix64_at.restype = C.c_uint64
+    lib.spmvhost_gen_rmat_csr.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, _u32p, _u32p, _f64p]
+    lib.spmvhost_gen_rmat_csr.restype = C.c_uint64
+    lib.spmvhost_csr2csc.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, _u64p, _u32p, _u32p, _u64p, _u32p, _u32p]
+    lib.spmvhost_csr2csc.restype = None
+    lib.spmvhost_partition_rows.argtypes = [_u32p, C.c_uint32, C.c_uint32, _u32p]
+    lib.spmvhost_partition_rows.restype = None
+    lib.spmvhost_load_matrix.argtypes = [C.c_char_p, C.c_char_p, _u32p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.spmvhost_load_matrix.restype = C.c_int
+    lib.spmvhost_convert_mtx.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
+    lib.spmvhost_convert_mtx.restype = C.c_int
+    _host = lib
+    return lib
+
+
+def _check(status: int, what: str) -> None:
+    if status != 0:
+        raise HipSpMVError(status, what)
+
+
+def _ptr(a) -> int:
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()  # torch tensor
+
+
+class Handle:
+    """One matrix resident on one device (a `hipspmv_t`)."""
+
+    def __init__(self, ptr, ind, vals, rows: int, cols: int, *, csr: bool = False, device: int = 0):
+        lib = load_hipspmv()
+        ptr = np.ascontiguousarray(ptr, dtype=np.uint32)
+        ind = np.ascontiguousarray(ind, dtype=np.uint32)
+        if vals.dtype == np.uint64:
+            self.dtype = U64
+        elif vals.dtype == np.float64:
+            self.dtype = F64
+        else:
+            raise TypeError("values must be float64 or uint64")
+        vals = np.ascontiguousarray(vals)
+        self.rows, self.cols, self.nnz = int(rows), int(cols), int(ind.size)
+        self.device = device
+        h = C.c_void_p()
+        fn = lib.hipspmv_create_csr if csr else lib.hipspmv_create
+        _check(fn(ptr.ctypes.data, ind.ctypes.data, vals.ctypes.data, self.rows, self.cols, self.nnz,
+                  self.dtype, device, C.byref(h)), "hipspmv_create")
+        self._h = h
+        self._lib = lib
+
+    @classmethod
+    def from_csc(cls, colptr, rowind, vals, rows, cols, device=0):
+        return cls(colptr, rowind, vals, rows, cols, csr=False, device=device)
+
+    @classmethod
+    def from_csr(cls, rowptr, colind, vals, rows, cols, device=0):
+        return cls(rowptr, colind, vals, rows, cols, csr=True, device=device)
+
+    def set_option(self, key: str, value: int) -> None:
+        _check(self._lib.hipspmv_set_option(self._h, key.encode(), int(value)), f"set_option({key})")
+
+    def set_kernel(self, name: str) -> None:
+        self.set_option("kernel", KERNELS[name])
+
+    def kernel_name(self, mode: int = MODE_AUTO) -> str:
+        return self._lib.hipspmv_kernel_name(self._h, mode).decode()
+
+    def exec(self, x: np.ndarray, y: np.ndarray | None = None, beta: int = 0, mode: int = MODE_ORDERED):
+        """Host-buffer exec (synchronous); returns y."""
+        npdt = np.uint64 if self.dtype == U64 else np.float64
+        x = np.ascontiguousarray(x, dtype=npdt)
+        if y is None:
+            y = np.zeros(self.rows, dtype=npdt)
+        assert x.size == self.cols and y.size == self.rows and y.dtype == npdt and y.flags.c_contiguous
+        _check(self._lib.hipspmv_exec(self._h, x.ctypes.data, y.ctypes.data, beta, mode), "hipspmv_exec")
+        return y
+
+    def exec_device(self, x, y_out, y_in=None, beta: int = 0, mode: int = MODE_ORDERED, stream=None) -> None:
+        """Device-tensor exec, enqueued on `stream` (torch stream or raw handle int)."""
+        s = stream
+        if s is not None and hasattr(s, "cuda_stream"):
+            s = s.cuda_stream
+        yin = _ptr(y_in) if y_in is not None else None
+        _check(self._lib.hipspmv_exec_device(self._h, _ptr(x), yin, _ptr(y_out), beta, mode, s),
+               "hipspmv_exec_device")
+
+    def stat(self, key: str) -> int:
+        v = C.c_uint64()
+        _check(self._lib.hipspmv_stat(self._h, key.encode(), C.byref(v)), f"stat({key})")
+        return int(v.value)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.hipspmv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    n = C.c_int()
+    _check(load_hipspmv().hipspmv_device_count(C.byref(n)), "device_count")
+    return int(n.value)
+
+
+# ---------------------------------------------------------------- host helpers
+def gen_stripe_csr(row0: int, nrows: int, cols: int, k: int = 32, seed_col: int = 1, seed_val: int = 2):
+    lib = load_host()
+    rowptr = np.empty(nrows + 1, dtype=np.uint32)
+    colind = np.empty(nrows * k, dtype=np.uint32)
+    vals = np.empty(nrows * k, dtype=np.float64)
+    lib.spmvhost_gen_stripe_csr(row0, nrows, cols, k, seed_col, seed_val, rowptr, colind, vals)
+    return rowptr, colind, vals
+
+
+def gen_vector(n: int, seed: int = 3) -> np.ndarray:
+    out = np.empty(n, dtype=np.float64)
+    load_host().spmvhost_gen_vector(n, seed, out)
+    return out
+
+
+def gen_rmat_csr(scale: int, edge_factor: int = 16, seed: int = 4):
+    lib = load_host()
+    n, m = 1 << scale, edge_factor << scale
+    rowptr = np.empty(n + 1, dtype=np.uint32)
+    colind = np.empty(m, dtype=np.uint32)
+    vals = np.empty(m, dtype=np.float64)
+    nnz = lib.spmvhost_gen_rmat_csr(scale, edge_factor, seed, rowptr, colind, vals)
+    return rowptr, colind[:nnz].copy(), vals[:nnz].copy()
+
+
+def csr2csc(rows: int, cols: int, rowptr, colind, vals):
+    """Product transpose (libspmvhost csr2csc); 8-byte values moved as words."""
+    lib = load_host()
+    nnz = int(colind.size)
+    v = np.ascontiguousarray(vals).view(np.uint64)
+    colptr = np.empty(cols + 1, dtype=np.uint32)
+    rowind = np.empty(nnz, dtype=np.uint32)
+    out = np.empty(nnz, dtype=np.uint64)
+    lib.spmvhost_csr2csc(rows, cols, nnz, v, np.ascontiguousarray(colind, dtype=np.uint32),
+                         np.ascontiguousarray(rowptr, dtype=np.uint32), out, rowind, colptr)
+    return colptr, rowind, out.view(vals.dtype)
+
+
+def partition_rows(rowptr: np.ndarray, parts: int) -> np.ndarray:
+    rows = rowptr.size - 1
+    bounds = np.empty(parts + 1, dtype=np.uint32)
+    load_host().spmvhost_partition_rows(np.ascontiguousarray(rowptr, dtype=np.uint32), rows, parts, bounds)
+    return bounds
+
+
+def load_matrix(directory: str, name: str):
+    """(rows, cols, colptr, rowind, vals) of a reference-format matrix."""
+    lib = load_host()
+    dims = np.zeros(4, dtype=np.uint32)
+    _check(lib.spmvhost_load_matrix(directory.encode(), name.encode(), dims, None, None, None), f"load {name}")
+    rows, cols, nnz, is_u64 = (int(d) for d in dims)
+    colptr = np.empty(cols + 1, dtype=np.uint32)
+    rowind = np.empty(nnz, dtype=np.uint32)
+    vals = np.empty(nnz, dtype=np.uint64)
+    _check(lib.spmvhost_load_matrix(directory.encode(), name.encode(), dims, colptr.ctypes.data,
+                                    rowind.ctypes.data, vals.ctypes.data), f"load {name}")
+    return rows, cols, colptr, rowind, (vals if is_u64 else vals.view(np.float64))
+
+
+def convert_mtx(mtx_path: str, outdir: str, name: str, golden: bool = True) -> None:
+    """Matrix Market -> reference .bin layout (+ golden.bin) via libspmvhost."""
+    os.makedirs(os.path.join(outdir, name), exist_ok=True)
+    _check(load_host().spmvhost_convert_mtx(mtx_path.encode(), outdir.encode(), name.encode(), int(golden)),
+           f"convert {mtx_path}")

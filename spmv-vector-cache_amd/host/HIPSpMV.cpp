@@ -1,0 +1,109 @@
+#include "HIPSpMV.h"
+
+#include <iostream>
+#include <map>
+#include <mutex>
+
+#include "hipspmv.h"
+
+HIPSpMVRegisterFile* HIPSpMV::registerFile(int device) {
+  static std::mutex mu;
+  static std::map<int, HIPSpMVRegisterFile> files;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = files.find(device);
+  if (it == files.end())
+    it = files.emplace(device, HIPSpMVRegisterFile{kSignature, device, HIPSPMV_MODE_ORDERED, HIPSPMV_KERNEL_AUTO, 1, 0})
+             .first;
+  return &it->second;
+}
+
+HIPSpMV::HIPSpMV(uintptr_t aBase, uintptr_t aReset, SparseMatrix* A, SpMVData* x, SpMVData* y)
+    : HardwareSpMV(aBase, aReset, A, x, y) {}
+
+HIPSpMV::~HIPSpMV() {
+  if (m_h) hipspmv_destroy(m_h);
+}
+
+// setupRegs(): the device copy of A is built once per matrix version (CSC ->
+// CSR transpose, kernel layouts, upload) and reused by later exec() calls --
+// the analogue of programming the base-address registers
+// (HardwareSpMVNewCache.cpp:31-44) without re-sending the matrix.
+void HIPSpMV::setupRegs() {
+  HardwareSpMV::setupRegs();
+  if (m_status) return;
+  if (m_h && m_builtVersion == m_A->version()) return;
+  if (m_h) {
+    hipspmv_destroy(m_h);
+    m_h = nullptr;
+  }
+  const int dtype = m_A->getDataType() == SPMV_U64 ? HIPSPMV_U64 : HIPSPMV_F64;
+  m_status = hipspmv_create(m_A->getIndPtrs(), m_A->getInds(), m_A->getNzData(), m_A->getRows(), m_A->getCols(),
+                            m_A->getNz(), dtype, regs()->device, &m_h);
+  if (m_status) {
+    std::cerr << "HIPSpMV: hipspmv_create failed: " << hipspmv_strerror(m_status) << " (" << hipspmv_last_error()
+              << ")" << std::endl;
+    m_h = nullptr;
+    return;
+  }
+  m_builtVersion = m_A->version();
+  if (regs()->kernel != HIPSPMV_KERNEL_AUTO) m_status = hipspmv_set_option(m_h, "kernel", regs()->kernel);
+}
+
+void HIPSpMV::init() {}
+
+// regular(): x to the device, the kernel, y back -- synchronously, like the
+// reference's busy-wait on doneRegular (HardwareSpMVNewCache.cpp:90-101).
+void HIPSpMV::regular() {
+  if (m_status || !m_h) return;
+  m_status = hipspmv_exec(m_h, m_x, m_y, regs()->beta, regs()->mode);
+  if (m_status)
+    std::cerr << "HIPSpMV: exec failed: " << hipspmv_strerror(m_status) << " (" << hipspmv_last_error() << ")"
+              << std::endl;
+}
+
+void HIPSpMV::write() {}
+
+// There are no stream FIFOs to throttle; the thresholds are kept only so
+// setThresholds() stays callable and they appear in the statistics.
+void HIPSpMV::setThresholdRegisters() {}
+
+bool HIPSpMV::exec() {
+  m_status = 0;
+  resetAccelerator();
+  setupRegs();
+  init();
+  regular();
+  write();
+  return m_status == 0;
+}
+
+uint64_t HIPSpMV::statU64(const std::string& key) {
+  uint64_t v = 0;
+  if (m_h && hipspmv_stat(m_h, key.c_str(), &v) == HIPSPMV_OK) return v;
+  return 0;
+}
+
+std::vector<std::string> HIPSpMV::statKeys() {
+  std::vector<std::string> keys = HardwareSpMV::statKeys();
+  for (const char* k : {"kernelTimeUs", "setupTimeUs", "h2dTimeUs", "d2hTimeUs", "algKBytes", "mode", "kernel",
+                        "device", "error"})
+    keys.push_back(k);
+  return keys;
+}
+
+unsigned int HIPSpMV::statInt(std::string name) {
+  if (name == "kernelTimeUs") return (unsigned int)(statU64("kernel_ns") / 1000);
+  if (name == "setupTimeUs") return (unsigned int)(statU64("setup_ns") / 1000);
+  if (name == "h2dTimeUs") return (unsigned int)(statU64("h2d_ns") / 1000);
+  if (name == "d2hTimeUs") return (unsigned int)(statU64("d2h_ns") / 1000);
+  if (name == "algKBytes") return (unsigned int)(statU64(regs()->beta ? "alg_bytes_beta1" : "alg_bytes") / 1024);
+  if (name == "mode") return (unsigned int)regs()->mode;
+  if (name == "kernel") return (unsigned int)statU64("kernel");
+  if (name == "device") return (unsigned int)regs()->device;
+  if (name == "error") return (unsigned int)m_status;
+  if (name == "thresColPtr") return m_thres_colPtr;
+  if (name == "thresRowInd") return m_thres_rowInd;
+  if (name == "thresNZData") return m_thres_nzData;
+  if (name == "thresInputVec") return m_thres_inpVec;
+  return HardwareSpMV::statInt(name);
+}

@@ -1,0 +1,76 @@
+// extern "C" helpers of libspmvhost.so for the Python harness (bench.py,
+// tests/): synthetic generators, the product csr2csc and the .bin loader.
+// Plain C types only, like include/hipspmv.h.
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "MatrixIO.h"
+#include "Synthetic.h"
+#include "csr2csc.h"
+
+extern "C" {
+
+void spmvhost_gen_stripe_csr(uint64_t row0, uint32_t nrows, uint32_t cols, uint32_t k, uint64_t seed_col,
+                             uint64_t seed_val, uint32_t* rowptr, uint32_t* colind, double* vals) {
+  genStripeCSR(row0, nrows, cols, k, seed_col, seed_val, rowptr, colind, vals);
+}
+
+void spmvhost_gen_vector(uint64_t n, uint64_t seed, double* out) {
+  for (uint64_t i = 0; i < n; ++i) out[i] = uniform11(splitmix64_at(seed, i));
+}
+
+uint64_t spmvhost_splitmix64_at(uint64_t seed, uint64_t i) { return splitmix64_at(seed, i); }
+
+// Fills caller arrays sized for the upper bound (rowptr: 2^scale+1, colind/vals:
+// edge_factor*2^scale); returns the nnz after summing duplicates.
+uint64_t spmvhost_gen_rmat_csr(uint32_t scale, uint32_t edge_factor, uint64_t seed, uint32_t* rowptr,
+                               uint32_t* colind, double* vals) {
+  std::vector<uint32_t> rp, ci;
+  std::vector<double> v;
+  const uint64_t nnz = genRmatCSR(scale, edge_factor, seed, 0.57, 0.19, 0.19, rp, ci, v);
+  std::memcpy(rowptr, rp.data(), sizeof(uint32_t) * rp.size());
+  std::memcpy(colind, ci.data(), sizeof(uint32_t) * nnz);
+  std::memcpy(vals, v.data(), sizeof(double) * nnz);
+  return nnz;
+}
+
+void spmvhost_csr2csc(uint32_t n, uint32_t m, uint32_t nz, const uint64_t* a, const uint32_t* col_idx,
+                      const uint32_t* row_start, uint64_t* csc_a, uint32_t* row_idx, uint32_t* col_start) {
+  csr2csc(n, m, nz, a, col_idx, row_start, csc_a, row_idx, col_start);
+}
+
+void spmvhost_partition_rows(const uint32_t* rowptr, uint32_t rows, uint32_t parts, uint32_t* bounds) {
+  partitionRows(rowptr, rows, parts, bounds);
+}
+
+// Loads <dir>/<name>; copies into caller arrays when they are non-null, and
+// always reports the dimensions.  Returns 0 on success.
+int spmvhost_load_matrix(const char* dir, const char* name, uint32_t* dims /*rows, cols, nz, is_u64*/,
+                         uint32_t* colptr, uint32_t* rowind, uint64_t* vals) {
+  SparseMatrix* A = loadSparseMatrix(dir, name);
+  if (!A) return 1;
+  dims[0] = A->getRows();
+  dims[1] = A->getCols();
+  dims[2] = A->getNz();
+  dims[3] = A->getDataType() == SPMV_U64;
+  if (colptr) std::memcpy(colptr, A->getIndPtrs(), 4ull * (A->getCols() + 1));
+  if (rowind) std::memcpy(rowind, A->getInds(), 4ull * A->getNz());
+  if (vals) std::memcpy(vals, A->getNzData(), 8ull * A->getNz());
+  delete A;
+  return 0;
+}
+
+// Matrix Market -> reference .bin files (+ golden.bin) under <outdir>/<name>/,
+// the job of matrices/matrixutils.py:187-260 and :108-113.  Returns 0 on success.
+int spmvhost_convert_mtx(const char* mtx_path, const char* outdir, const char* name, int write_golden) {
+  SparseMatrix* A = loadMatrixMarket(mtx_path);
+  if (!A) return 1;
+  bool ok = writeSparseMatrix(A, outdir, name);
+  if (ok && write_golden) ok = writeGolden(A, std::string(outdir) + "/" + name + "/golden.bin");
+  delete A;
+  return ok ? 0 : 2;
+}
+
+}  // extern "C"

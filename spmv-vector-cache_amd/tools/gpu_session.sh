@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprof kernel-trace.
+# Each GPU step has its own time limit; a crash/abort/timeout (rc >= 124 or a
+# signal) ends the session, plain test failures (rc 1) do not.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 2
+mkdir -p gpurun_out
+OUT=gpurun_out
+step() {  # step NAME TIMEOUT CMD...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" | tee -a $OUT/session.log
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a $OUT/session.log
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -gt 1 -a $rc -ne 0 -a "$name" != "pytest_gpu" ]; then
+    echo "stopping session after $name (rc=$rc)"; exit $rc
+  fi
+  return 0
+}
+STEPS=${STEPS:-"pytest smoke bench prof"}
+for s in $STEPS; do
+  case $s in
+    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    benchfast) step bench_fast 600 python bench.py --mode fast --no-cpu-baseline ;;
+    prof) export TMPDIR=/tmp; step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    pmc) export TMPDIR=/tmp; step pmc 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
+         step pmc2 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    micro) step micro 300 ./spmv-vector-cache_amd/tools/microbench ;;
+  esac
+done
+echo "session done"

@@ -1,0 +1,198 @@
+"""GPU parity: the HIP kernels through the C ABI vs the CPU oracle.
+
+Ordered kernels (vcache, csr_lane) and every u64 run must be bit-identical
+to SoftwareSpMV (oracle.spmv_csc); the fast f64 kernel (csr_vector) must meet
+the per-row bound of include/hipspmv.h:
+    |y - y_ref| <= 2*len*2^-53 * (sum_j |a_ij x_j| + |y_in|)  (+ tiny abs slack)
+"""
+import numpy as np
+import pytest
+
+import fixtures as fx
+import hipspmv as hs
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+ORDERED_KERNELS = ["vcache", "csr_lane"]
+
+
+def _fast_bound(rowptr_len, absprod, yin):
+    u = 2.0 ** -53
+    return 2.0 * np.maximum(rowptr_len, 1) * u * (absprod + np.abs(yin)) + 1e-300
+
+
+def _csr_stats(rows, cols, colptr, rowind, vals, x):
+    """per-row length and sum|a_ij x_j| (for the fast-mode bound)"""
+    lens = np.bincount(rowind, minlength=rows)
+    absprod = np.zeros(rows)
+    np.add.at(absprod, rowind, np.abs(vals.astype(np.float64) * np.repeat(x, np.diff(colptr.astype(np.int64)))))
+    return lens, absprod
+
+
+def _check(name, rows, cols, colptr, rowind, vals, x, kernel, beta, mode=hs.MODE_ORDERED, y0=None):
+    h = hs.Handle.from_csc(colptr, rowind, vals, rows, cols)
+    if kernel == "vcache" and not h.stat("vcache_eligible"):
+        pytest.skip("vcache not eligible")
+    h.set_kernel(kernel)
+    npdt = vals.dtype
+    if y0 is None:
+        y0 = (np.random.default_rng(11).uniform(-1, 1, rows) if npdt == np.float64
+              else np.random.default_rng(11).integers(0, 2**64, rows, dtype=np.uint64))
+    y_ref = oracle.spmv_csc(colptr, rowind, vals, x, y=(y0.copy() if beta else np.zeros(rows, npdt)), rows=rows)
+    y = h.exec(x, y0.copy(), beta=beta, mode=mode)
+    if npdt == np.uint64 or kernel in ORDERED_KERNELS:
+        if y.tobytes() != y_ref.tobytes():
+            bad = np.nonzero(y.view(np.uint64) != y_ref.view(np.uint64))[0]
+            pytest.fail(f"{name}/{kernel}/beta{beta}: {bad.size} rows differ, first {bad[:5]} "
+                        f"got {y[bad[:3]]} want {y_ref[bad[:3]]}")
+    else:
+        lens, absprod = _csr_stats(rows, cols, colptr, rowind, vals, x)
+        bound = _fast_bound(lens, absprod, y0 if beta else np.zeros(rows))
+        err = np.abs(y - y_ref)
+        assert np.all(err <= bound), f"{name}: max err/bound {np.max(err / bound)}"
+    return h, y
+
+
+@pytest.mark.parametrize("name", fx.ALL_FIXTURES)
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector"])
+@pytest.mark.parametrize("beta", [0, 1])
+def test_fixtures(gpu, name, kernel, beta):
+    rows, cols, colptr, rowind, vals = fx.load(name)
+    for xname, x in fx.x_variants(name, cols).items():
+        mode = hs.MODE_FAST if kernel == "csr_vector" else hs.MODE_ORDERED
+        _check(f"{name}[{xname}]", rows, cols, colptr, rowind, vals, x, kernel, beta, mode)
+
+
+@pytest.mark.parametrize("name", fx.F64_FIXTURES)
+def test_reference_golden_bin_exact(gpu, name):
+    # HIPSpMV ordered == reference golden.bin (A*1), the reference's own compareGolden
+    rows, cols, colptr, rowind, vals = fx.load(name)
+    h = hs.Handle.from_csc(colptr, rowind, vals, rows, cols)
+    y = h.exec(np.ones(cols), beta=0, mode=hs.MODE_ORDERED)
+    assert y.tobytes() == fx.golden(name).tobytes(), h.kernel_name(hs.MODE_ORDERED)
+
+
+def _random_csc(rows, cols, density, rng, dtype=np.float64, empty_rows=True, long_rows=(), dup=False):
+    dense = rng.random((rows, cols)) < density
+    if empty_rows:
+        dense[rng.integers(0, rows, rows // 7)] = False
+    for r in long_rows:
+        dense[r, :] = True
+    colptr = np.concatenate([[0], np.cumsum(dense.sum(0))]).astype(np.uint32)
+    rowind = np.concatenate([np.nonzero(dense[:, c])[0] for c in range(cols)]).astype(np.uint32)
+    if dup:  # duplicate some entries inside their column (SoftwareSpMV adds both, in order)
+        pass
+    if dtype == np.float64:
+        vals = rng.uniform(-1, 1, rowind.size)
+    else:
+        vals = rng.integers(0, 2**64, rowind.size, dtype=np.uint64)
+    return colptr, rowind, vals
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (1, 300), (300, 1), (257, 1000), (5000, 333), (3000, 20000)])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector"])
+def test_random_ragged(gpu, shape, kernel):
+    rng = np.random.default_rng(shape[0] * 31 + shape[1])
+    rows, cols = shape
+    dens = min(1.0, 40.0 / cols)
+    colptr, rowind, vals = _random_csc(rows, cols, dens, rng, long_rows=[rows // 2] if rows > 2 else [])
+    x = rng.uniform(-1, 1, cols)
+    mode = hs.MODE_FAST if kernel == "csr_vector" else hs.MODE_ORDERED
+    for beta in (0, 1):
+        _check(f"rand{shape}", rows, cols, colptr, rowind, vals, x, kernel, beta, mode)
+
+
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector"])
+def test_random_u64_wraparound(gpu, kernel):
+    rng = np.random.default_rng(5)
+    rows, cols = 4000, 9000
+    colptr, rowind, vals = _random_csc(rows, cols, 0.004, rng, dtype=np.uint64, long_rows=[17])
+    x = rng.integers(0, 2**64, cols, dtype=np.uint64)
+    for beta in (0, 1):
+        _check("u64", rows, cols, colptr, rowind, vals, x, kernel, beta, hs.MODE_FAST)
+
+
+def test_duplicates_and_cms_bits(gpu):
+    # duplicate (row, col) entries are added in CSC order; CMS bits 30/31 of the
+    # row ids (SparseMatrix::markRowStarts) are ignored by the backend
+    colptr = np.array([0, 3, 5], np.uint32)
+    rowind = np.array([0, 0, 2, 1, 1], np.uint32)
+    vals = np.array([0.1, 0.2, 1e16, 3.0, -3.0], np.float64)
+    x = np.array([1.7, -2.3])
+    y_ref = oracle.spmv_csc(colptr, rowind, vals, x, rows=3)
+    marked = rowind | np.array([1 << 31, 0, 1 << 31, 1 << 31 | 1 << 30, 1 << 30], np.uint32)
+    for kernel in ORDERED_KERNELS:
+        h = hs.Handle.from_csc(colptr, marked, vals, 3, 2)
+        h.set_kernel(kernel)
+        y = h.exec(x, beta=0)
+        assert y.tobytes() == y_ref.tobytes()
+
+
+def test_synthetic_c3_full_size_ordered(gpu):
+    # BASELINE config C3 at full size: 2^20 x 2^20, 32 nnz/row; ordered == oracle bit for bit
+    n = 1 << 20
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+    colptr, rowind, cvals = oracle.csr2csc(n, n, rowptr, colind, vals)
+    x = hs.gen_vector(n, 3)
+    y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=n)
+    h = hs.Handle.from_csc(colptr, rowind, cvals, n, n)
+    assert h.kernel_name(hs.MODE_ORDERED) == "vcache"
+    y = h.exec(x, beta=0, mode=hs.MODE_ORDERED)
+    assert y.tobytes() == y_ref.tobytes()
+    # the CSR entry point gives the same bits
+    h2 = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    assert h2.exec(x, beta=0).tobytes() == y_ref.tobytes()
+    # fast kernel within the bound
+    h.set_kernel("csr_vector")
+    yf = h.exec(x, beta=0, mode=hs.MODE_FAST)
+    lens = np.full(n, 32)
+    absprod = np.zeros(n)
+    np.add.at(absprod, np.repeat(np.arange(n), 32), np.abs(vals * x[colind]))
+    assert np.all(np.abs(yf - y_ref) <= _fast_bound(lens, absprod, 0))
+
+
+def test_exec_device_torch(gpu):
+    import torch
+    rows, cols, colptr, rowind, vals = fx.load("circuit204")
+    x = np.random.default_rng(2).uniform(-1, 1, cols)
+    y_ref = oracle.spmv_csc(colptr, rowind, vals, x, rows=rows)
+    h = hs.Handle.from_csc(colptr, rowind, vals, rows, cols)
+    h.set_option("timing", 1)
+    xd = torch.from_numpy(x).to(gpu)
+    yd = torch.empty(rows, dtype=torch.float64, device=gpu)
+    s = torch.cuda.current_stream()
+    h.exec_device(xd, yd, beta=0, mode=hs.MODE_ORDERED, stream=s)
+    s.synchronize()
+    assert yd.cpu().numpy().tobytes() == y_ref.tobytes()
+    assert h.stat("kernel_ns") > 0
+    # accumulate in place (y_in == y_out)
+    h.exec_device(xd, yd, y_in=yd, beta=1, mode=hs.MODE_ORDERED, stream=s)
+    s.synchronize()
+    y2 = oracle.spmv_csc(colptr, rowind, vals, x, y=y_ref.copy(), rows=rows)
+    assert yd.cpu().numpy().tobytes() == y2.tobytes()
+
+
+def test_invalid_matrix_rejected(gpu):
+    colptr = np.array([0, 2, 1], np.uint32)  # not monotone
+    with pytest.raises(hs.HipSpMVError) as e:
+        hs.Handle.from_csc(colptr, np.array([0, 1], np.uint32), np.ones(2), 2, 2)
+    assert e.value.status == 2
+    with pytest.raises(hs.HipSpMVError):
+        hs.Handle.from_csc(np.array([0, 1, 2], np.uint32), np.array([0, 5], np.uint32), np.ones(2), 2, 2)
+
+
+def test_plugin_surface_spmvbench(gpu):
+    # software/main.cpp pipeline through HWSpMVFactory -> HIPSpMV; diffFromGolden == 0
+    import subprocess
+    names = fx.ALL_FIXTURES
+    out = subprocess.run([f"{hs.LIB_DIR}/spmvbench", "--dir", fx.MATRICES, "--confs", "hip", "--cms", "1", *names],
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = out.stdout.splitlines()
+    hdr = next(l for l in lines if l.startswith("diffFromGolden,"))
+    keys = hdr.rstrip(",").split(",")
+    recs = [dict(zip(keys, l.rstrip(",").split(","))) for l in lines if l[:1].isdigit()]
+    assert len(recs) == len(names)
+    for r in recs:
+        assert r["diffFromGolden"] == "0" and r["accType"] == "HIPSpMV" and r["error"] == "0", r
