@@ -64,6 +64,8 @@ extern "C" {
 #define HIPSPMV_KERNEL_VCACHE 1     /* x panels + y block staged in LDS; ordered */
 #define HIPSPMV_KERNEL_CSR_LANE 2   /* one lane per row over CSR; ordered */
 #define HIPSPMV_KERNEL_CSR_VECTOR 3 /* wave segmented DPP reduction over CSR; fast */
+#define HIPSPMV_KERNEL_VCACHE_SPLIT 4 /* vcache over two column halves, fixed-order
+                                         combine p0 + p1; fast, deterministic */
 
 typedef struct hipspmv_handle hipspmv_t;
 
@@ -94,9 +96,9 @@ int hipspmv_set_option(hipspmv_t *h, const char *key, int64_t value);
 int hipspmv_exec(hipspmv_t *h, const void *x, void *y, int beta, int mode);
 
 /* Device-resident variant: d_x, d_y_in and d_y_out are device pointers on the
- * handle's device; enqueued on `stream` (a hipStream_t, NULL = the handle's
- * own stream) and returns without synchronising.  d_y_in may equal d_y_out
- * and is ignored for beta == 0. */
+ * handle's device; enqueued on `stream` (a hipStream_t; NULL is HIP's default
+ * stream, as in every HIP API) and returns without synchronising.  d_y_in may
+ * equal d_y_out and is ignored for beta == 0. */
 int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void *d_y_out, int beta, int mode,
                         void *stream);
 

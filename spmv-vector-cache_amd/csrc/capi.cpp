@@ -69,10 +69,13 @@ struct hipspmv_handle {
   uint32_t *d_rowptr = nullptr, *d_colind = nullptr, *d_groups = nullptr;
   uint64_t* d_vals = nullptr;
   uint32_t ngroups = 0;
-  bool vc_ok = false;
-  uint32_t *d_seg = nullptr, *d_code = nullptr;
-  uint64_t* d_evals = nullptr;
-  uint32_t vc_rows_per_block = 0, vc_nblocks = 0, vc_npanels = 0, vc_npad = 0, vc_max_seg = 0;
+  struct Vc {  // one vcache layout on the device (ordered or split geometry)
+    bool ok = false;
+    uint32_t *d_seg = nullptr, *d_code = nullptr, *d_tickets = nullptr;
+    uint64_t *d_vals = nullptr, *d_partial = nullptr;
+    uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, part_panels = 0, npad = 0, max_seg = 0;
+    int split = 1;
+  } vc[2];  // [0] ordered (kVcOrdered), [1] split (kVcSplit)
   void *d_x = nullptr, *d_y = nullptr;
   int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
   uint64_t setup_ns = 0, kernel_ns = 0, h2d_ns = 0, d2h_ns = 0, execs = 0, device_bytes = 0;
@@ -85,9 +88,14 @@ struct hipspmv_handle {
 static void release(hipspmv_t* h) {
   if (!h) return;
   DeviceGuard g(h->device);
-  void* ptrs[] = {h->d_rowptr, h->d_colind, h->d_groups, h->d_vals, h->d_seg, h->d_code, h->d_evals, h->d_x, h->d_y};
+  void* ptrs[] = {h->d_rowptr, h->d_colind, h->d_groups, h->d_vals, h->d_x, h->d_y};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (auto& v : h->vc) {
+    void* vp[] = {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial};
+    for (void* p : vp)
+      if (p) (void)hipFree(p);
+  }
   for (hipEvent_t e : h->ev)
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -111,18 +119,29 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   build_row_groups(a, groups);
   h->ngroups = (uint32_t)groups.size() - 1;
   if ((st = dev_upload(&h->d_groups, groups.data(), groups.size(), h->device_bytes))) return st;
-  h->vc_ok = vcache_eligible(a);
-  if (h->vc_ok) {
+  const VcGeom geoms[2] = {kVcOrdered, kVcSplit};
+  for (int k = 0; k < 2; ++k) {
+    auto& v = h->vc[k];
+    v.ok = vcache_eligible(a, geoms[k]);
+    if (!v.ok) continue;
     VcacheLayout L;
-    build_vcache(a, L);
-    h->vc_rows_per_block = L.rows_per_block;
-    h->vc_nblocks = L.nblocks;
-    h->vc_npanels = L.npanels;
-    h->vc_npad = L.npad;
-    h->vc_max_seg = L.max_seg;
-    if ((st = dev_upload(&h->d_seg, L.seg.data(), L.seg.size(), h->device_bytes))) return st;
-    if ((st = dev_upload(&h->d_code, L.code.data(), L.code.size(), h->device_bytes))) return st;
-    if ((st = dev_upload(&h->d_evals, L.vals.data(), L.vals.size(), h->device_bytes))) return st;
+    build_vcache(a, geoms[k], L);
+    v.split = geoms[k].split;
+    v.rows_per_block = L.rows_per_block;
+    v.nblocks = L.nblocks;
+    v.npanels = L.npanels;
+    v.part_panels = L.part_panels;
+    v.npad = L.npad;
+    v.max_seg = L.max_seg;
+    if ((st = dev_upload(&v.d_seg, L.seg.data(), L.seg.size(), h->device_bytes))) return st;
+    if ((st = dev_upload(&v.d_code, L.code.data(), L.code.size(), h->device_bytes))) return st;
+    if ((st = dev_upload(&v.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return st;
+    if (v.split > 1) {
+      std::vector<uint32_t> zeros(v.nblocks, 0u);
+      if ((st = dev_upload(&v.d_tickets, zeros.data(), zeros.size(), h->device_bytes))) return st;
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&v.d_partial), 8ull * v.split * a.rows));
+      h->device_bytes += 8ull * v.split * a.rows;
+    }
   }
   return HIPSPMV_OK;
 }
@@ -169,30 +188,40 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
   if (mode == HIPSPMV_MODE_AUTO) mode = h->mode_opt;
   if (mode != HIPSPMV_MODE_ORDERED && mode != HIPSPMV_MODE_FAST) return -HIPSPMV_ERR_INVALID_ARG;
   const bool exact_any = h->dtype == HIPSPMV_U64;  // integer sums are order-independent
+  const bool fast_ok = mode == HIPSPMV_MODE_FAST || exact_any;
   switch (h->kernel_opt) {
     case HIPSPMV_KERNEL_VCACHE:
-      return h->vc_ok ? HIPSPMV_KERNEL_VCACHE : -HIPSPMV_ERR_UNSUPPORTED;
+      return h->vc[0].ok ? HIPSPMV_KERNEL_VCACHE : -HIPSPMV_ERR_UNSUPPORTED;
+    case HIPSPMV_KERNEL_VCACHE_SPLIT:
+      if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
+      return h->vc[1].ok ? HIPSPMV_KERNEL_VCACHE_SPLIT : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_LANE:
       return HIPSPMV_KERNEL_CSR_LANE;
     case HIPSPMV_KERNEL_CSR_VECTOR:
-      return (mode == HIPSPMV_MODE_FAST || exact_any) ? HIPSPMV_KERNEL_CSR_VECTOR : -HIPSPMV_ERR_UNSUPPORTED;
+      return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_AUTO:
       break;
     default:
       return -HIPSPMV_ERR_INVALID_ARG;
   }
-  // The LDS vector cache pays when each swept x element feeds enough
-  // nonzeros; it is ordered, so it serves both modes.
-  if (h->vc_ok && (uint64_t)h->nnz * 16 >= (uint64_t)h->vc_nblocks * h->cols) return HIPSPMV_KERNEL_VCACHE;
-  return (mode == HIPSPMV_MODE_FAST || exact_any) ? HIPSPMV_KERNEL_CSR_VECTOR : HIPSPMV_KERNEL_CSR_LANE;
+  // The LDS vector cache pays when each x element a work unit streams feeds
+  // enough nonzeros.
+  auto worth = [&](const hipspmv_handle::Vc& v) {
+    return v.ok && (uint64_t)h->nnz * 16 * v.split >= (uint64_t)v.nblocks * v.split * h->cols;
+  };
+  if (fast_ok && worth(h->vc[1])) return HIPSPMV_KERNEL_VCACHE_SPLIT;
+  if (worth(h->vc[0])) return HIPSPMV_KERNEL_VCACHE;
+  return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : HIPSPMV_KERNEL_CSR_LANE;
 }
 
 static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in, void* d_y_out, int beta,
                   hipStream_t s) {
   hipError_t e = hipSuccess;
-  if (kernel == HIPSPMV_KERNEL_VCACHE) {
-    VcacheArgs a{h->d_seg, h->d_code, h->d_evals, d_x, d_y_in, d_y_out, h->rows, h->cols, h->vc_rows_per_block,
-                 h->vc_npanels, h->vc_npad, h->nnz - 1, h->vc_nblocks, beta};
+  if (kernel == HIPSPMV_KERNEL_VCACHE || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT) {
+    const auto& v = h->vc[kernel == HIPSPMV_KERNEL_VCACHE ? 0 : 1];
+    VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    v.d_partial,
+                 v.d_tickets, h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
+                 v.npad,      h->nnz - 1, v.split,   beta};
     e = launch_vcache(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
@@ -249,7 +278,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   if (!h || !key) return HIPSPMV_ERR_INVALID_ARG;
   const std::string k(key);
   if (k == "kernel") {
-    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_CSR_VECTOR) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_VCACHE_SPLIT) return HIPSPMV_ERR_INVALID_ARG;
     h->kernel_opt = (int)value;
   } else if (k == "mode") {
     if (value != HIPSPMV_MODE_ORDERED && value != HIPSPMV_MODE_FAST) return HIPSPMV_ERR_INVALID_ARG;
@@ -308,7 +337,7 @@ int hipspmv_exec_device(hipspmv_t* h, const void* d_x, const void* d_y_in, void*
   const int kernel = choose_kernel(h, mode);
   if (kernel < 0) return -kernel;
   DeviceGuard g(h->device);
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+  hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the default stream
   if (h->timing) HIP_TRY(hipEventRecord(h->ev[1], s));
   int st = launch(h, kernel, d_x, beta ? d_y_in : d_y_out, d_y_out, beta, s);
   if (st) return st;
@@ -340,11 +369,14 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "alg_bytes_beta1") *out = alg + 8ull * h->rows;
   else if (k == "flops") *out = 2ull * h->nnz;
   else if (k == "device_bytes") *out = h->device_bytes;
-  else if (k == "vcache_blocks") *out = h->vc_nblocks;
-  else if (k == "vcache_panels") *out = h->vc_npanels;
-  else if (k == "vcache_rows_per_block") *out = h->vc_rows_per_block;
-  else if (k == "vcache_max_segment") *out = h->vc_max_seg;
-  else if (k == "vcache_eligible") *out = h->vc_ok;
+  else if (k == "vcache_blocks") *out = h->vc[0].nblocks;
+  else if (k == "vcache_panels") *out = h->vc[0].npanels;
+  else if (k == "vcache_rows_per_block") *out = h->vc[0].rows_per_block;
+  else if (k == "vcache_max_segment") *out = h->vc[0].max_seg;
+  else if (k == "vcache_eligible") *out = h->vc[0].ok;
+  else if (k == "vcache_split_eligible") *out = h->vc[1].ok;
+  else if (k == "vcache_split_units") *out = (uint64_t)h->vc[1].nblocks * h->vc[1].split;
+  else if (k == "vcache_split_rows_per_block") *out = h->vc[1].rows_per_block;
   else if (k == "row_groups") *out = h->ngroups;
   else if (k == "max_row_len") *out = h->max_row_len;
   else if (k == "empty_rows") *out = h->empty_rows;
@@ -357,6 +389,7 @@ const char* hipspmv_kernel_name(hipspmv_t* h, int mode) {
   if (!h) return "invalid";
   switch (choose_kernel(h, mode)) {
     case HIPSPMV_KERNEL_VCACHE: return "vcache";
+    case HIPSPMV_KERNEL_VCACHE_SPLIT: return "vcache_split";
     case HIPSPMV_KERNEL_CSR_LANE: return "csr_lane";
     case HIPSPMV_KERNEL_CSR_VECTOR: return "csr_vector";
     default: return "unsupported";

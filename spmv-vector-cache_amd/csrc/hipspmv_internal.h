@@ -9,13 +9,21 @@
 namespace hipspmv {
 
 // ---- vcache kernel geometry ---------------------------
-// One 1024-thread workgroup per row block; LDS holds the block's y accumulators
-// (<= kVcRows doubles), two x panels of kVcPanel doubles and the block's
-// segment table (<= kVcSegMax offsets): 32768 + 130048 + 1024 = 163840 B.
+// One 1024-thread workgroup per work unit = (row block, column part); LDS
+// holds the block's y accumulators (<= rows doubles), two x panels of `panel`
+// doubles and the unit's segment table (<= kVcSegMax offsets), 163840 B total:
+//   ordered: 4096 rows, 1 part  : 32768 + 2*8128*8 + 1024
+//   split  : 8192 rows, 2 parts : 65536 + 2*6080*8 + 1024
+// The split geometry halves the x bytes each CU streams (the measured limit,
+// DESIGN.md §3.1) and combines the two column-half partials in fixed order
+// (p0 + p1), so it is deterministic but not bit-identical: FAST mode.
+struct VcGeom {
+  int rows, panel, split;
+};
+constexpr VcGeom kVcOrdered{4096, 8128, 1};
+constexpr VcGeom kVcSplit{8192, 6080, 2};
 constexpr int kVcThreads = 1024;
-constexpr int kVcRows = 4096;
-constexpr int kVcPanel = 8128;
-constexpr int kVcSegMax = 256;        // npad + 1 <= kVcSegMax
+constexpr int kVcSegMax = 256;        // npad + 1 <= kVcSegMax per unit
 constexpr int kVcEpt = 2;             // entries per thread held in registers per panel
 constexpr int kVcDepth = 2;           // panels of prefetch in flight (entries + x)
 constexpr uint32_t kVcCont = 1u << 30;  // entry continues the previous entry's row run
@@ -32,8 +40,11 @@ struct HostCSR {
 };
 
 struct VcacheLayout {
-  uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, npad = 0;
-  std::vector<uint32_t> seg;    // nblocks * (npad + 1) global entry offsets
+  VcGeom geom{};
+  uint32_t rows_per_block = 0, nblocks = 0, npanels = 0;
+  uint32_t part_panels = 0;  // panels per column part (the last part may have fewer)
+  uint32_t npad = 0;         // part_panels rounded up to kVcDepth
+  std::vector<uint32_t> seg;    // (nblocks * split) units * (npad + 1) global entry offsets
   std::vector<uint32_t> code;   // per entry: col_local | row_local << 16 | CONT | MORE
   std::vector<uint64_t> vals;   // per entry
   uint32_t max_seg = 0;
@@ -46,8 +57,8 @@ int csc_to_csr(const uint32_t* colptr, const uint32_t* rowind, const void* vals,
 int copy_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, uint32_t rows, uint32_t cols,
              uint32_t nnz, HostCSR& out, std::string& why);
 
-bool vcache_eligible(const HostCSR& a);
-void build_vcache(const HostCSR& a, VcacheLayout& out);
+bool vcache_eligible(const HostCSR& a, const VcGeom& g);
+void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out);
 // Row groups for csr_vector: group g covers rows [groups[g], groups[g+1]).
 void build_row_groups(const HostCSR& a, std::vector<uint32_t>& groups);
 

@@ -14,8 +14,10 @@ struct VcacheArgs {
   const void* x;
   const void* y_in;
   void* y_out;
-  uint32_t rows, cols, rows_per_block, npanels, npad, last, nblocks;
-  int beta;
+  void* partial;       // split == 2: [2][rows] scratch for the column-part partials
+  uint32_t* tickets;   // split == 2: [nblocks] arrival counters, zero between launches
+  uint32_t rows, cols, rows_per_block, nblocks, npanels, part_panels, npad, last;
+  int split, beta;
 };
 
 struct CsrArgs {

@@ -80,18 +80,20 @@ int copy_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, u
   return HIPSPMV_OK;
 }
 
-static uint32_t vcache_rows_per_block(uint32_t rows) {
-  // One block per CU when the rows allow it (256 CUs on MI355X), never more
-  // than the LDS y budget; at least 64 rows so tiny matrices use few blocks.
-  uint32_t r = (rows + 255) / 256;
+static uint32_t vcache_rows_per_block(uint32_t rows, const VcGeom& g) {
+  // About one work unit per CU (256 CUs on MI355X), never more rows than the
+  // LDS y budget; at least 64 rows so tiny matrices use few units.
+  uint32_t r = (uint32_t)(((uint64_t)rows * g.split + 255) / 256);
   r = std::max<uint32_t>(r, 64);
-  return std::min<uint32_t>(r, kVcRows);
+  return std::min<uint32_t>(r, (uint32_t)g.rows);
 }
 
-bool vcache_eligible(const HostCSR& a) {
+bool vcache_eligible(const HostCSR& a, const VcGeom& g) {
   if (a.cols < 2 || a.rows == 0 || a.nnz == 0) return false;
-  const uint32_t npanels = (a.cols + kVcPanel - 1) / kVcPanel;
-  const uint32_t npad = (npanels + kVcDepth - 1) / kVcDepth * kVcDepth;
+  const uint32_t np = (a.cols + g.panel - 1) / g.panel;
+  if (np < (uint32_t)g.split) return false;  // every column part needs >= 1 panel
+  const uint32_t part = (np + g.split - 1) / g.split;
+  const uint32_t npad = (part + kVcDepth - 1) / kVcDepth * kVcDepth;
   if (npad + 1 > (uint32_t)kVcSegMax) return false;
   // panel order must equal each row's summation order: columns non-decreasing
   for (uint32_t r = 0; r < a.rows; ++r)
@@ -103,17 +105,23 @@ bool vcache_eligible(const HostCSR& a) {
 // Entries of row block b that fall into column panel p form segment (b, p),
 // ordered by (row, column); each row's entries keep their CSR order, so a
 // thread that walks a row run in a segment, and the panels in ascending
-// order, adds the row's products in ascending column order (ordered mode).
-void build_vcache(const HostCSR& a, VcacheLayout& out) {
-  const uint32_t R = vcache_rows_per_block(a.rows);
+// order, adds the row's products in ascending column order.  A work unit
+// (b, h) covers panels [h*part, (h+1)*part); its seg row lists npad+1 offsets
+// (empty segments past its last panel).
+void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
+  const uint32_t P = (uint32_t)g.panel, S = (uint32_t)g.split;
+  const uint32_t R = vcache_rows_per_block(a.rows, g);
   const uint32_t nb = (a.rows + R - 1) / R;
-  const uint32_t np = (a.cols + kVcPanel - 1) / kVcPanel;
-  const uint32_t npad = (np + kVcDepth - 1) / kVcDepth * kVcDepth;
+  const uint32_t np = (a.cols + P - 1) / P;
+  const uint32_t part = (np + S - 1) / S;
+  const uint32_t npad = (part + kVcDepth - 1) / kVcDepth * kVcDepth;
+  out.geom = g;
   out.rows_per_block = R;
   out.nblocks = nb;
   out.npanels = np;
+  out.part_panels = part;
   out.npad = npad;
-  out.seg.assign((size_t)nb * (npad + 1), 0);
+  out.seg.assign((size_t)nb * S * (npad + 1), 0);
   out.code.resize(a.nnz);
   out.vals.resize(a.nnz);
   out.max_seg = 0;
@@ -122,20 +130,23 @@ void build_vcache(const HostCSR& a, VcacheLayout& out) {
   for (uint32_t b = 0; b < nb; ++b) {
     const uint32_t r0 = b * R, r1 = std::min(a.rows, r0 + R);
     std::fill(cnt.begin(), cnt.end(), 0);
-    for (uint32_t e = a.rowptr[r0]; e < a.rowptr[r1]; ++e) cnt[a.colind[e] / kVcPanel + 1]++;
+    for (uint32_t e = a.rowptr[r0]; e < a.rowptr[r1]; ++e) cnt[a.colind[e] / P + 1]++;
     for (uint32_t p = 0; p < np; ++p) {
       out.max_seg = std::max(out.max_seg, cnt[p + 1]);
       cnt[p + 1] += cnt[p];
     }
-    uint32_t* seg = &out.seg[(size_t)b * (npad + 1)];
-    for (uint32_t p = 0; p <= npad; ++p) seg[p] = base + cnt[std::min(p, np)];
+    for (uint32_t h = 0; h < S; ++h) {
+      uint32_t* seg = &out.seg[((size_t)b * S + h) * (npad + 1)];
+      const uint32_t plast = std::min((h + 1) * part, np);
+      for (uint32_t i = 0; i <= npad; ++i) seg[i] = base + cnt[std::min(h * part + i, plast)];
+    }
     std::vector<uint32_t> cur(cnt.begin(), cnt.end() - 1);
     for (uint32_t r = r0; r < r1; ++r) {
       uint32_t prev_d = UINT32_MAX, prev_p = UINT32_MAX;
       for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
-        const uint32_t c = a.colind[e], p = c / kVcPanel;
+        const uint32_t c = a.colind[e], p = c / P;
         const uint32_t d = base + cur[p]++;
-        uint32_t code = (c - p * kVcPanel) | ((r - r0) << 16);
+        uint32_t code = (c - p * P) | ((r - r0) << 16);
         if (p == prev_p && d == prev_d + 1) {  // same row, same segment, adjacent: extend the run
           code |= kVcCont;
           out.code[prev_d] |= kVcMore;

@@ -32,7 +32,8 @@ def _csr_stats(rows, cols, colptr, rowind, vals, x):
 
 def _check(name, rows, cols, colptr, rowind, vals, x, kernel, beta, mode=hs.MODE_ORDERED, y0=None):
     h = hs.Handle.from_csc(colptr, rowind, vals, rows, cols)
-    if kernel == "vcache" and not h.stat("vcache_eligible"):
+    if (kernel == "vcache" and not h.stat("vcache_eligible")) or \
+            (kernel == "vcache_split" and not h.stat("vcache_split_eligible")):
         pytest.skip("vcache not eligible")
     h.set_kernel(kernel)
     npdt = vals.dtype
@@ -55,12 +56,12 @@ def _check(name, rows, cols, colptr, rowind, vals, x, kernel, beta, mode=hs.MODE
 
 
 @pytest.mark.parametrize("name", fx.ALL_FIXTURES)
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split"])
 @pytest.mark.parametrize("beta", [0, 1])
 def test_fixtures(gpu, name, kernel, beta):
     rows, cols, colptr, rowind, vals = fx.load(name)
     for xname, x in fx.x_variants(name, cols).items():
-        mode = hs.MODE_FAST if kernel == "csr_vector" else hs.MODE_ORDERED
+        mode = hs.MODE_ORDERED if kernel in ORDERED_KERNELS else hs.MODE_FAST
         _check(f"{name}[{xname}]", rows, cols, colptr, rowind, vals, x, kernel, beta, mode)
 
 
@@ -91,19 +92,19 @@ def _random_csc(rows, cols, density, rng, dtype=np.float64, empty_rows=True, lon
 
 
 @pytest.mark.parametrize("shape", [(1, 1), (1, 300), (300, 1), (257, 1000), (5000, 333), (3000, 20000)])
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split"])
 def test_random_ragged(gpu, shape, kernel):
     rng = np.random.default_rng(shape[0] * 31 + shape[1])
     rows, cols = shape
     dens = min(1.0, 40.0 / cols)
     colptr, rowind, vals = _random_csc(rows, cols, dens, rng, long_rows=[rows // 2] if rows > 2 else [])
     x = rng.uniform(-1, 1, cols)
-    mode = hs.MODE_FAST if kernel == "csr_vector" else hs.MODE_ORDERED
+    mode = hs.MODE_ORDERED if kernel in ORDERED_KERNELS else hs.MODE_FAST
     for beta in (0, 1):
         _check(f"rand{shape}", rows, cols, colptr, rowind, vals, x, kernel, beta, mode)
 
 
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split"])
 def test_random_u64_wraparound(gpu, kernel):
     rng = np.random.default_rng(5)
     rows, cols = 4000, 9000
@@ -196,3 +197,25 @@ def test_plugin_surface_spmvbench(gpu):
     assert len(recs) == len(names)
     for r in recs:
         assert r["diffFromGolden"] == "0" and r["accType"] == "HIPSpMV" and r["error"] == "0", r
+
+
+def test_c3_split_deterministic_and_within_bound(gpu):
+    # vcache_split: two column-half partials combined in fixed order -> identical
+    # bits on every run, and within the FAST-mode bound of the oracle
+    n = 1 << 20
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+    x = hs.gen_vector(n, 3)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    assert h.stat("vcache_split_eligible") == 1
+    assert h.kernel_name(hs.MODE_FAST) == "vcache_split"
+    ys = [h.exec(x, beta=0, mode=hs.MODE_FAST) for _ in range(3)]
+    assert ys[0].tobytes() == ys[1].tobytes() == ys[2].tobytes()
+    colptr, rowind, cvals = oracle.csr2csc(n, n, rowptr, colind, vals)
+    y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=n)
+    absprod = np.zeros(n)
+    np.add.at(absprod, np.repeat(np.arange(n), 32), np.abs(vals * x[colind]))
+    assert np.all(np.abs(ys[0] - y_ref) <= _fast_bound(np.full(n, 32), absprod, 0))
+    # beta = 1 accumulates y_in into part 0 only
+    y0 = np.random.default_rng(4).uniform(-1, 1, n)
+    y1 = h.exec(x, y0.copy(), beta=1, mode=hs.MODE_FAST)
+    assert np.all(np.abs(y1 - (y_ref + y0)) <= _fast_bound(np.full(n, 33), absprod + np.abs(y0), 0) * 2)
