@@ -25,7 +25,7 @@ constexpr VcGeom kVcSplit{8192, 6080, 2};
 constexpr int kVcThreads = 1024;
 constexpr int kVcSegMax = 256;        // npad + 1 <= kVcSegMax per unit
 constexpr int kVcEpt = 2;             // entries per thread held in registers per panel
-constexpr int kVcDepth = 2;           // panels of prefetch in flight (entries + x)
+constexpr int kVcDepth = 4;           // panels of prefetch in flight (entries + x)
 constexpr uint32_t kVcCont = 1u << 30;  // entry continues the previous entry's row run
 constexpr uint32_t kVcMore = 1u << 31;  // next entry continues this entry's row run
 
@@ -43,7 +43,7 @@ struct VcacheLayout {
   VcGeom geom{};
   uint32_t rows_per_block = 0, nblocks = 0, npanels = 0;
   uint32_t part_panels = 0;  // panels per column part (the last part may have fewer)
-  uint32_t npad = 0;         // part_panels rounded up to kVcDepth
+  uint32_t npad = 0;         // seg entries per unit - 1 (= part_panels)
   std::vector<uint32_t> seg;    // (nblocks * split) units * (npad + 1) global entry offsets
   std::vector<uint32_t> code;   // per entry: col_local | row_local << 16 | CONT | MORE
   std::vector<uint64_t> vals;   // per entry

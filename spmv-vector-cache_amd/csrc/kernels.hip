@@ -1,189 +1,22 @@
-// HIPSpMV device kernels for gfx950 (MI355X, CDNA4, wave64).
+// HIPSpMV CSR kernels for gfx950 (MI355X, CDNA4, wave64).
 //
-// Each kernel computes y_out = (beta ? y_in : 0) + A*x for its layout; the
-// reference arithmetic is SoftwareSpMV::exec (software/SoftwareSpMV.cpp:59-64):
-// per row, products rounded then added in ascending column order.  The file is
-// compiled with -ffp-contract=off and every kernel body repeats
-// `#pragma clang fp contract(off)`, so no a*b+c is fused (tests/ check the
-// ordered kernels bit-for-bit against the oracle).
+// Each kernel computes y_out = (beta ? y_in : 0) + A*x over the CSR copy of A;
+// the reference arithmetic is SoftwareSpMV::exec (software/SoftwareSpMV.cpp:
+// 59-64): per row, products rounded then added in ascending column order.
+// Compiled with -ffp-contract=off, and every body repeats
+// `#pragma clang fp contract(off)`, so no a*b+c is fused.
 //
-//   k_vcache     ordered; x panels and the row block's y accumulators staged in
-//                LDS (the GPU analogue of the reference's vector cache,
-//                chisel/cache-new/NoWMVectorCache.scala); one 1024-thread
-//                workgroup per row block.                        DESIGN.md §3.1
 //   k_csr_lane   ordered; one lane per CSR row, any matrix.      DESIGN.md §3.2
 //   k_csr_vector fast; row groups, one wave each, wave-level segmented scan
 //                with DPP row_shr / row_bcast.                   DESIGN.md §3.3
+// The LDS vector-cache kernel is in vcache.hip.
 #include <hip/hip_runtime.h>
 
+#include "device_common.h"
 #include "hipspmv_internal.h"
 #include "kernels.h"
 
 namespace hipspmv {
-
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-
-template <typename T>
-__device__ __forceinline__ T madd(T acc, T a, T b) {
-#pragma clang fp contract(off)
-  const T p = a * b;  // rounded (f64) / truncated mod 2^64 (u64) before the add
-  return acc + p;
-}
-
-// ---------------------------------------------------------------------------
-// k_vcache
-// ---------------------------------------------------------------------------
-// One workgroup per work unit (row block b, column part h).  Per panel of VP
-// columns: x[panel] -> LDS (register-staged, kVcDepth panels ahead), the
-// unit's entries of that panel (same prefetch distance, so the in-order
-// vmcnt never makes a young load wait behind an old one) each add
-// val * x_lds[col] into y_lds[row]; one barrier per panel.  SPLIT == 2: the
-// two column parts of a block run in workgroups i and i+8 (one XCD under
-// round-robin dispatch, speed only), each publishes its partial and the
-// second to arrive writes y = p0 + p1 (agent-scope release/acquire ticket,
-// MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility").
-template <typename T, int VR, int VP, int SPLIT>
-__global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restrict__ seg,
-                                                        const uint32_t* __restrict__ ecode,
-                                                        const T* __restrict__ evals, const T* __restrict__ x,
-                                                        const T* __restrict__ y_in, T* __restrict__ y_out,
-                                                        T* __restrict__ partial, uint32_t* __restrict__ tickets,
-                                                        uint32_t rows, uint32_t cols, uint32_t rows_per_block,
-                                                        uint32_t nblocks, uint32_t npanels, uint32_t part_panels,
-                                                        uint32_t npad, uint32_t last, int beta) {
-#pragma clang fp contract(off)
-  constexpr int VT = kVcThreads, D = kVcDepth, EPT = kVcEpt;
-  constexpr uint32_t PAIRS = VP / 2;  // 16-byte pairs per panel
-  constexpr int NJ = (PAIRS + VT - 1) / VT;
-  static_assert(VR * 8 + 2 * VP * 8 + kVcSegMax * 4 <= 163840, "LDS budget");
-  __shared__ T ylds[VR];
-  __shared__ T xb[2][VP];
-  __shared__ uint32_t segl[kVcSegMax];
-
-  const int t = threadIdx.x;
-  uint32_t b = blockIdx.x, h = 0;
-  if (SPLIT == 2) {  // unit i -> (b, h): parts of one block are 8 dispatch slots apart
-    const uint32_t g = blockIdx.x / 16, rem = blockIdx.x % 16;
-    const uint32_t nbg = min(8u, nblocks - g * 8);
-    h = rem / nbg;
-    b = g * 8 + rem % nbg;
-  }
-  const uint32_t r0 = b * rows_per_block;
-  const uint32_t nr = min(rows_per_block, rows - r0);
-  const uint32_t p0 = h * part_panels;                   // first global panel of this unit
-  const uint32_t npu = min(part_panels, npanels - p0);   // >= 1 (vcache_eligible)
-  const uint32_t* sp = seg + ((size_t)b * SPLIT + h) * (npad + 1);
-  if ((uint32_t)t <= npad) segl[t] = sp[t];
-  for (uint32_t i = t; i < nr; i += VT) ylds[i] = (beta && h == 0) ? y_in[r0 + i] : T(0);
-
-  // x panel staging: branch-free 16-byte loads clamped to the last in-bounds
-  // pair (so no divergent path rewrites an in-flight load register); for odd
-  // cols the final element is patched from a scalar load by the thread owning
-  // its LDS slot.
-  const uint32_t cmax = (cols - 2) & ~1u;
-  const T xlast = x[cols - 1];
-  auto load_x = [&](uint32_t s, u64x2* r) {
-    const uint32_t base = (p0 + min(s, npu - 1)) * VP;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      r[j] = *reinterpret_cast<const u64x2*>(x + min(base + 2 * (t + j * VT), cmax));
-  };
-  auto store_x = [&](uint32_t s, const u64x2* r) {
-    T* dst = xb[s & 1];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      if ((j + 1) * VT <= (int)PAIRS || (uint32_t)(t + j * VT) < PAIRS)
-        *reinterpret_cast<u64x2*>(&dst[2 * (t + j * VT)]) = r[j];
-    if ((cols & 1) && p0 + s == npanels - 1) {
-      const uint32_t slot = cols - 1 - (p0 + s) * VP;
-      if ((uint32_t)t == (slot >> 1) % VT) dst[slot] = xlast;
-    }
-  };
-  // entries: branch-free loads at clamped indices, validity checked at use
-  auto load_e = [&](uint32_t s, uint32_t* c, T* v) {
-    const uint32_t beg = segl[min(s, npad)];
-#pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-      const uint32_t i = min(beg + t + j * VT, last);
-      c[j] = __builtin_nontemporal_load(ecode + i);
-      v[j] = __builtin_nontemporal_load(evals + i);
-    }
-  };
-  // a row run: its first entry is held by this thread; continuation entries
-  // (MORE) are read back from memory (rare: >1 entry of a row in one panel)
-  auto run = [&](uint32_t i, uint32_t code, T v, const T* xs) {
-    const uint32_t row = (code >> 16) & 0x3FFF;
-    T acc = madd(ylds[row], v, xs[code & 0xFFFF]);
-    while (code & kVcMore) {
-      ++i;
-      code = ecode[i];
-      acc = madd(acc, evals[i], xs[code & 0xFFFF]);
-    }
-    ylds[row] = acc;
-  };
-
-  u64x2 X[D][NJ];
-  uint32_t EC[D][EPT];
-  T EV[D][EPT];
-  __syncthreads();  // segl visible
-  load_x(0, X[0]);
-  store_x(0, X[0]);
-#pragma unroll
-  for (int i = 0; i < D; ++i) {
-    load_e(i, EC[i], EV[i]);
-    load_x(i + 1, X[(i + 1) % D]);
-  }
-  __syncthreads();
-  for (uint32_t base = 0; base < npad; base += D) {
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-      const uint32_t s = base + i;
-      const T* xs = xb[s & 1];
-      const uint32_t beg = segl[s], end = segl[s + 1];
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        const uint32_t q = beg + t + j * VT;
-        if (q < end && !(EC[i][j] & kVcCont)) run(q, EC[i][j], EV[i][j], xs);
-      }
-      for (uint32_t q = beg + EPT * VT + t; q < end; q += VT) {  // overflow beyond the register window
-        const uint32_t code = ecode[q];
-        if (!(code & kVcCont)) run(q, code, evals[q], xs);
-      }
-      load_e(s + D, EC[i], EV[i]);
-      if (s + 1 < npu) store_x(s + 1, X[(i + 1) % D]);
-      load_x(s + 1 + D, X[(i + 1) % D]);
-      __syncthreads();
-    }
-  }
-  if (SPLIT == 1) {
-    for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
-    return;
-  }
-  // ---- combine the two column parts (fixed order p0 + p1) ----
-  T* mine = partial + (size_t)h * rows;
-  for (uint32_t i = t; i < nr; i += VT) mine[r0 + i] = ylds[i];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t old = __hip_atomic_fetch_add(tickets + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-    }
-    segl[0] = old;
-  }
-  __syncthreads();
-  if (segl[0] == 1) {
-    const T* other = partial + (size_t)(1 - h) * rows;
-    for (uint32_t i = t; i < nr; i += VT) {
-      const T o = other[r0 + i], m = ylds[i];
-      y_out[r0 + i] = h == 0 ? m + o : o + m;
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------
 // k_csr_lane: ordered, one lane per row
@@ -308,21 +141,6 @@ __global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__
 // launchers
 // ---------------------------------------------------------------------------
 template <typename T>
-hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
-  const uint32_t units = a.nblocks * a.split;
-  if (a.split == 1)
-    hipLaunchKernelGGL((k_vcache<T, kVcOrdered.rows, kVcOrdered.panel, 1>), dim3(units), dim3(kVcThreads), 0, s,
-                       a.seg, a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out,
-                       (T*)a.partial, a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels,
-                       a.part_panels, a.npad, a.last, a.beta);
-  else
-    hipLaunchKernelGGL((k_vcache<T, kVcSplit.rows, kVcSplit.panel, 2>), dim3(units), dim3(kVcThreads), 0, s,
-                       a.seg, a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out,
-                       (T*)a.partial, a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels,
-                       a.part_panels, a.npad, a.last, a.beta);
-  return hipGetLastError();
-}
-template <typename T>
 hipError_t launch_csr_lane(const CsrArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_csr_lane<T>, dim3((a.rows + 255) / 256), dim3(256), 0, s, a.rowptr, a.colind,
                      (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.beta);
@@ -335,9 +153,6 @@ hipError_t launch_csr_vector(const CsrArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s) {
-  return dtype ? launch_vcache<uint64_t>(a, s) : launch_vcache<double>(a, s);
-}
 hipError_t launch_csr_lane(int dtype, const CsrArgs& a, hipStream_t s) {
   return dtype ? launch_csr_lane<uint64_t>(a, s) : launch_csr_lane<double>(a, s);
 }

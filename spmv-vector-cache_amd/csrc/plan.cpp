@@ -93,7 +93,7 @@ bool vcache_eligible(const HostCSR& a, const VcGeom& g) {
   const uint32_t np = (a.cols + g.panel - 1) / g.panel;
   if (np < (uint32_t)g.split) return false;  // every column part needs >= 1 panel
   const uint32_t part = (np + g.split - 1) / g.split;
-  const uint32_t npad = (part + kVcDepth - 1) / kVcDepth * kVcDepth;
+  const uint32_t npad = part;  // the kernel clamps prefetches past its last panel
   if (npad + 1 > (uint32_t)kVcSegMax) return false;
   // panel order must equal each row's summation order: columns non-decreasing
   for (uint32_t r = 0; r < a.rows; ++r)
@@ -114,7 +114,7 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
   const uint32_t nb = (a.rows + R - 1) / R;
   const uint32_t np = (a.cols + P - 1) / P;
   const uint32_t part = (np + S - 1) / S;
-  const uint32_t npad = (part + kVcDepth - 1) / kVcDepth * kVcDepth;
+  const uint32_t npad = part;  // the kernel clamps prefetches past its last panel
   out.geom = g;
   out.rows_per_block = R;
   out.nblocks = nb;

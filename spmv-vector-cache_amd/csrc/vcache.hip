@@ -1,0 +1,259 @@
+// k_vcache: the LDS "vector cache" SpMV kernel for gfx950.
+//
+// The reference's accelerators stream A in column order and keep the output
+// vector y in an on-chip vector cache (chisel/cache-new/NoWMVectorCache.scala,
+// chisel/frontend/SpMVFrontendNewCache.scala:102-151).  Here one 1024-thread
+// workgroup owns a block of rows: their y accumulators live in LDS for the
+// whole launch, and x is streamed through LDS in panels of VP columns, so every
+// x gather and every y update is an LDS access; HBM sees each nonzero once.
+//
+// Work unit = (row block b, column part h).  SPLIT == 1 (ordered geometry):
+// one part, every row's products are added in ascending column order, starting
+// from y_in or +0.0 -- bit-identical to SoftwareSpMV.  SPLIT == 2: two column
+// halves per block (halving the x bytes each CU streams, the measured limit),
+// combined in fixed order y = p0 + p1 by whichever workgroup finishes second:
+// deterministic, FAST-mode tolerance.
+//
+// Waves are specialised (producer/consumer): waves [0, WL) stream x panels
+// into LDS (register-staged, two panels ahead); waves [WL, 16) stream the
+// unit's entries (DE panels ahead) and apply them.  Each role waits only on
+// its own vmcnt, so the L2-served x stream and the HBM-served entry stream
+// overlap; one workgroup barrier per panel hands the next x panel over.
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "hipspmv_internal.h"
+#include "kernels.h"
+
+namespace hipspmv {
+
+// Per-geometry configuration.  LDS: VR*8 + 2*VP*8 + kVcSegMax*4 = 163840 B.
+template <int SPLIT>
+struct VcCfg;
+template <>
+struct VcCfg<1> {  // 4096 rows; x panel 63.5 KiB; 8 loader waves (8 pairs/lane), 8 compute waves
+  static constexpr int VR = kVcOrdered.rows, VP = kVcOrdered.panel, WL = 8, DE = 4, EPT = 3;
+};
+template <>
+struct VcCfg<2> {  // 8192 rows; x panel 47.5 KiB; 6 loader waves (8 pairs/lane), 10 compute waves
+  static constexpr int VR = kVcSplit.rows, VP = kVcSplit.panel, WL = 6, DE = 4, EPT = 3;
+};
+
+// AB: ablation mask for the diagnostic build (tools/vc_ablate.hip); the
+// product instantiates AB = 0 and every hook folds away.  Bits: 1 no x loads,
+// 2 no x LDS stores, 4 no entry loads, 8 no compute, 16 x always from panel 0,
+// 32 no per-panel barrier (wrong results, timing only).
+template <typename T, int SPLIT, int WL = VcCfg<SPLIT>::WL, int DE = VcCfg<SPLIT>::DE, int EPT = VcCfg<SPLIT>::EPT,
+          int AB = 0, int MAP = 0, bool NT = false>
+__global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restrict__ seg,
+                                                        const uint32_t* __restrict__ ecode,
+                                                        const T* __restrict__ evals, const T* __restrict__ x,
+                                                        const T* __restrict__ y_in, T* __restrict__ y_out,
+                                                        T* __restrict__ partial, uint32_t* __restrict__ tickets,
+                                                        uint32_t rows, uint32_t cols, uint32_t rows_per_block,
+                                                        uint32_t nblocks, uint32_t npanels, uint32_t part_panels,
+                                                        uint32_t npad, uint32_t last, int beta) {
+#pragma clang fp contract(off)
+  constexpr int VR = VcCfg<SPLIT>::VR, VP = VcCfg<SPLIT>::VP;
+  constexpr int VT = kVcThreads, NW = VT / 64, WC = NW - WL;
+  constexpr int LT = WL * 64, CT = WC * 64;  // loader / compute lanes
+  constexpr uint32_t PAIRS = VP / 2;         // 16-byte pairs per panel
+  constexpr int NJ = (PAIRS + LT - 1) / LT;  // pairs per loader lane per panel
+  static_assert(VR * 8 + 2 * VP * 8 + kVcSegMax * 4 <= 163840, "LDS budget");
+  static_assert(WL > 0 && WC > 0, "both roles need waves");
+  __shared__ T ylds[VR];
+  __shared__ T xb[2][VP];
+  __shared__ uint32_t segl[kVcSegMax];
+
+  const int t = threadIdx.x;
+  const bool loader = __builtin_amdgcn_readfirstlane(t >> 6) < WL;  // wave-uniform role
+  uint32_t b = blockIdx.x, h = 0;
+  if (SPLIT == 2 && MAP == 1 && nblocks % 4 == 0) {
+    // dispatch slot i -> XCD group i % 8: groups 0-3 take column half 0,
+    // groups 4-7 half 1, so one XCD's L2 serves one half of x (speed only)
+    const uint32_t grp = blockIdx.x % 8;
+    h = grp / 4;
+    b = (blockIdx.x / 8) * 4 + grp % 4;
+  } else if (SPLIT == 2) {  // unit i -> (b, h): the parts of a block are 8 dispatch slots apart
+    const uint32_t g = blockIdx.x / 16, rem = blockIdx.x % 16;
+    const uint32_t nbg = min(8u, nblocks - g * 8);
+    h = rem / nbg;
+    b = g * 8 + rem % nbg;
+  }
+  const uint32_t r0 = b * rows_per_block;
+  const uint32_t nr = min(rows_per_block, rows - r0);
+  const uint32_t p0 = h * part_panels;                  // first global panel of this unit
+  const uint32_t npu = min(part_panels, npanels - p0);  // >= 1 (vcache_eligible)
+  const uint32_t* sp = seg + ((size_t)b * SPLIT + h) * (npad + 1);
+  if ((uint32_t)t <= npad) segl[t] = sp[t];
+  for (uint32_t i = t; i < nr; i += VT) ylds[i] = (beta && h == 0) ? y_in[r0 + i] : T(0);
+
+  // ---- loader role: x panels, branch-free 16-byte loads clamped to the last
+  // in-bounds pair; for odd cols the final element is patched from a scalar
+  // load by the lane owning its LDS slot.
+  const uint32_t cmax = (cols - 2) & ~1u;
+  const T xlast = x[cols - 1];
+  auto load_x = [&](uint32_t s, u64x2* r) {
+    if (AB & 1) return;
+    const uint32_t base = (AB & 16) ? 0 : (p0 + min(s, npu - 1)) * VP;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      r[j] = *reinterpret_cast<const u64x2*>(x + min(base + 2 * (t + j * LT), cmax));
+  };
+  auto store_x = [&](uint32_t s, const u64x2* r) {
+    if (AB & 2) return;
+    T* dst = xb[s & 1];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      if ((j + 1) * LT <= (int)PAIRS || (uint32_t)(t + j * LT) < PAIRS)
+        *reinterpret_cast<u64x2*>(&dst[2 * (t + j * LT)]) = r[j];
+    if ((cols & 1) && p0 + s == npanels - 1) {
+      const uint32_t slot = cols - 1 - (p0 + s) * VP;
+      if ((uint32_t)t == (slot >> 1) % LT) dst[slot] = xlast;
+    }
+  };
+
+  // ---- compute role: entries at clamped indices (branch-free), validity
+  // checked at use.  A row run's first entry is held by one lane; its
+  // continuation entries (MORE) are read back from memory (rare: several
+  // entries of one row inside one panel).
+  const int ct = t - LT;
+  auto load_e = [&](uint32_t s, uint32_t* c, T* v) {
+    if (AB & 4) {
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) c[j] = kVcCont;
+      return;
+    }
+    const uint32_t beg = segl[min(s, npad)];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const uint32_t i = min(beg + ct + j * CT, last);
+      if (NT) {  // streamed once: non-temporal, so the entries do not evict x from L2
+        c[j] = __builtin_nontemporal_load(ecode + i);
+        v[j] = __builtin_nontemporal_load(evals + i);
+      } else {
+        c[j] = ecode[i];
+        v[j] = evals[i];
+      }
+    }
+  };
+  auto run = [&](uint32_t i, uint32_t code, T v, const T* xs) {
+    const uint32_t row = (code >> 16) & 0x3FFF;
+    T acc = madd(ylds[row], v, xs[code & 0xFFFF]);
+    while (code & kVcMore) {
+      ++i;
+      code = ecode[i];
+      acc = madd(acc, evals[i], xs[code & 0xFFFF]);
+    }
+    ylds[row] = acc;
+  };
+  auto apply = [&](uint32_t s, const uint32_t* c, const T* v) {
+    if (AB & 8) return;
+    const T* xs = xb[s & 1];
+    const uint32_t beg = segl[s], end = segl[s + 1];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const uint32_t q = beg + ct + j * CT;
+      if (q < end && !(c[j] & kVcCont)) run(q, c[j], v[j], xs);
+    }
+    for (uint32_t q = beg + EPT * CT + ct; q < end; q += CT) {  // beyond the register window (slow path)
+      const uint32_t code = ecode[q];
+      if (!(code & kVcCont)) run(q, code, evals[q], xs);
+    }
+  };
+
+  // Each role runs its own loop with exactly one workgroup barrier per panel
+  // (npu + 1 barriers in all, the same count in both), so the two register
+  // rings are never live together and the allocator overlays them.
+  auto barrier = [&]() {
+    if (AB & 32) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  __syncthreads();  // segl visible
+  if (loader) {
+    u64x2 R[2][NJ];  // R[(s+1)&1] holds x(s+1) during step s
+    load_x(0, R[0]);
+    store_x(0, R[0]);
+    load_x(1, R[1]);
+    load_x(2, R[0]);
+    barrier();
+    for (uint32_t base = 0; base < npu; base += 2) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t s = base + i;  // parity of s == parity of i
+        if (s >= npu) break;
+        if (s + 1 < npu) store_x(s + 1, R[(i + 1) & 1]);
+        load_x(s + 3, R[(i + 1) & 1]);
+        barrier();
+      }
+    }
+  } else {
+    uint32_t EC[DE][EPT];
+    T EV[DE][EPT];
+#pragma unroll
+    for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i]);
+    barrier();
+    for (uint32_t base = 0; base < npu; base += DE) {
+#pragma unroll
+      for (int i = 0; i < DE; ++i) {
+        const uint32_t s = base + i;
+        if (s >= npu) break;
+        apply(s, EC[i], EV[i]);
+        load_e(s + DE, EC[i], EV[i]);
+        barrier();
+      }
+    }
+  }
+  if (SPLIT == 1) {
+    for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
+    return;
+  }
+  // ---- combine the two column parts, fixed order p0 + p1.  Hand-off per
+  // MI355X_MICROARCH.md (Valid forms, table row 1): every partial byte stored
+  // write-through (sc1: agent-scope relaxed atomic store), each storing wave
+  // drains vmcnt, one lane adds to the block's counter after the barrier; the
+  // workgroup whose add returned 1 reads the other partial with sc1 loads.
+  uint64_t* mine = reinterpret_cast<uint64_t*>(partial) + (size_t)h * rows;
+  for (uint32_t i = t; i < nr; i += VT)
+    __hip_atomic_store(mine + r0 + i, __builtin_bit_cast(uint64_t, ylds[i]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(tickets + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == 1) __hip_atomic_store(tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    segl[0] = old;
+  }
+  __syncthreads();
+  if (segl[0] == 1) {
+    const uint64_t* other = reinterpret_cast<const uint64_t*>(partial) + (size_t)(1 - h) * rows;
+    for (uint32_t i = t; i < nr; i += VT) {
+      const T o = __builtin_bit_cast(
+          T, __hip_atomic_load(other + r0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const T m = ylds[i];
+      y_out[r0 + i] = h == 0 ? m + o : o + m;
+    }
+  }
+}
+
+template <typename T>
+hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
+  const uint32_t units = a.nblocks * a.split;
+  if (a.split == 1)
+    hipLaunchKernelGGL((k_vcache<T, 1>), dim3(units), dim3(kVcThreads), 0, s, a.seg, a.code, (const T*)a.vals,
+                       (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets, a.rows, a.cols,
+                       a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta);
+  else
+    hipLaunchKernelGGL((k_vcache<T, 2>), dim3(units), dim3(kVcThreads), 0, s, a.seg, a.code, (const T*)a.vals,
+                       (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets, a.rows, a.cols,
+                       a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta);
+  return hipGetLastError();
+}
+
+hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s) {
+  return dtype ? launch_vcache<uint64_t>(a, s) : launch_vcache<double>(a, s);
+}
+
+}  // namespace hipspmv
