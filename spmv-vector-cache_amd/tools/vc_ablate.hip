@@ -114,7 +114,6 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 2, 6, 4, 3, 0, 1, true>, "WL6 MAP1 NT", 0);
       variant(k_vcache<double, 2, 6, 4, 3, 16, 1, true>, "WL6 MAP1 NT x-L2hot", 16);
       variant(k_vcache<double, 2, 6, 4, 3, 12, 1, true>, "WL6 MAP1 NT no entries", 12);
-      variant(k_vcache<double, 1, 8, 4, 3, 0, 0, true>, "ordered NT", 0);
       variant(k_vcache<double, 2, 4, 4, 3, 1>, "no x loads", 1);
       variant(k_vcache<double, 2, 4, 4, 3, 3>, "no x", 3);
       variant(k_vcache<double, 2, 4, 4, 3, 4>, "no entry loads", 4);

@@ -1,0 +1,310 @@
+// vc_sim: CPU transliteration of k_vcache's addressing (csrc/vcache.hip) for
+// checking the kernel's index math on the host.
+//
+// For one matrix it builds the product layout (csrc/plan.cpp build_vcache),
+// then replays every work unit the way the kernel's two wave roles do --
+// loader lanes' clamped x-pair loads and LDS stores (with the odd-cols patch),
+// compute lanes' clamped quad loads, the DE-deep entry ring, the EPT register
+// window and the overflow loop, the run continuation, the split combine -- with
+// a bounds check on every global and LDS access and a check that no two lanes
+// write the same LDS y row within one panel step (the kernel's no-race
+// premise).  The result is compared bit-for-bit (ordered geometry) or within
+// the FAST bound (split) with a sequential CSR reference.
+//
+// Test infrastructure (tests/test_vcache_sim.py); not part of the product.
+//   g++ -O2 -std=c++17 -Icsrc -I../include tools/vc_sim.cpp csrc/plan.cpp host/Synthetic.cpp -o lib/vc_sim
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../host/Synthetic.h"
+#include "hipspmv_internal.h"
+
+using namespace hipspmv;
+
+static int g_errors = 0;
+#define CHECK(cond, ...)                                   \
+  do {                                                     \
+    if (!(cond)) {                                         \
+      if (g_errors++ < 20) {                               \
+        std::fprintf(stderr, "VIOLATION %s:%d: ", __FILE__, __LINE__); \
+        std::fprintf(stderr, __VA_ARGS__);                 \
+        std::fprintf(stderr, "\n");                        \
+      }                                                    \
+    }                                                      \
+  } while (0)
+
+template <typename T>
+struct Buf {  // bounds-checked global array
+  const char* name;
+  std::vector<T> v;
+  T get(size_t i) const {
+    CHECK(i < v.size(), "%s[%zu] read, size %zu", name, i, v.size());
+    return i < v.size() ? v[i] : T();
+  }
+  void put(size_t i, T x) {
+    CHECK(i < v.size(), "%s[%zu] write, size %zu", name, i, v.size());
+    if (i < v.size()) v[i] = x;
+  }
+};
+
+// kernel configuration mirrored from vcache.hip VcCfg<SPLIT>
+struct Cfg {
+  int VR, VP, WL, DE, EPT, SPLIT;
+};
+
+static double madd(double acc, double a, double b) {
+  volatile double p = a * b;  // rounded product, then the add (no contraction)
+  return acc + p;
+}
+
+// Replays k_vcache for every unit; returns y.
+static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, const Cfg& c, const std::vector<double>& x,
+                                    const std::vector<double>& yin, int beta) {
+  const int VT = 1024, NW = VT / 64, WC = NW - c.WL, LT = c.WL * 64, CT = WC * 64;
+  const uint32_t PAIRS = c.VP / 2;
+  const int NJ = (PAIRS + LT - 1) / LT;
+  const uint32_t rows = A.rows, cols = A.cols, nblocks = L.nblocks, npanels = L.npanels, part = L.part_panels,
+                 npad = L.npad, rpb = L.rows_per_block, last = (uint32_t)L.code.size() - 1;
+  Buf<uint32_t> seg{"seg", L.seg}, code{"ecode", L.code};
+  Buf<double> vals{"evals", {}}, X{"x", x}, Yin{"y_in", yin}, Y{"y_out", std::vector<double>(rows, NAN)};
+  vals.v.resize(L.vals.size());
+  std::memcpy(vals.v.data(), L.vals.data(), 8 * L.vals.size());
+  Buf<double> partial{"partial", std::vector<double>((size_t)rows * c.SPLIT, NAN)};
+  std::vector<uint32_t> tickets(nblocks, 0);
+  const uint32_t units = nblocks * c.SPLIT;
+  std::vector<std::vector<double>> ylds_of(units);
+  std::vector<uint32_t> b_of(units), h_of(units);
+  for (uint32_t bid = 0; bid < units; ++bid) {
+    uint32_t b = bid, h = 0;
+    if (c.SPLIT == 2) {
+      const uint32_t g = bid / 16, rem = bid % 16;
+      const uint32_t nbg = std::min(8u, nblocks - g * 8);
+      h = rem / nbg;
+      b = g * 8 + rem % nbg;
+    }
+    CHECK(b < nblocks && h < (uint32_t)c.SPLIT, "unit %u maps to (%u,%u)", bid, b, h);
+    b_of[bid] = b;
+    h_of[bid] = h;
+    const uint32_t r0 = b * rpb;
+    CHECK(r0 < rows, "unit %u r0 %u >= rows", bid, r0);
+    const uint32_t nr = std::min(rpb, rows - r0);
+    CHECK(nr <= (uint32_t)c.VR, "nr %u > VR", nr);
+    const uint32_t p0 = h * part;
+    CHECK(p0 < npanels, "p0 %u >= npanels %u", p0, npanels);
+    const uint32_t npu = std::min(part, npanels - p0);
+    CHECK(npu >= 1 && npad + 1 <= (uint32_t)kVcSegMax, "npu %u npad %u", npu, npad);
+    std::vector<uint32_t> segl(kVcSegMax, 0xDEADBEEF);
+    for (uint32_t t = 0; t <= npad; ++t) segl[t] = seg.get(((size_t)b * c.SPLIT + h) * (npad + 1) + t);
+    std::vector<double> ylds(c.VR, NAN);
+    for (uint32_t i = 0; i < nr; ++i) ylds[i] = (beta && h == 0) ? Yin.get(r0 + i) : 0.0;
+    const uint32_t cmax = (cols - 2) & ~1u;
+    const double xlast = X.get(cols - 1);
+    // loader: the LDS image of x panel s (load_x + store_x)
+    auto panel = [&](uint32_t s) {
+      std::vector<double> xb(c.VP, NAN);
+      const uint32_t base = (p0 + std::min(s, npu - 1)) * c.VP;
+      for (int t = 0; t < LT; ++t)
+        for (int j = 0; j < NJ; ++j) {
+          const uint32_t a = std::min(base + 2 * (t + j * LT), cmax);
+          const double v0 = X.get(a), v1 = X.get(a + 1);
+          if ((j + 1) * LT <= (int)PAIRS || (uint32_t)(t + j * LT) < PAIRS) {
+            const uint32_t slot = 2 * (t + j * LT);
+            CHECK(slot + 1 < (uint32_t)c.VP, "x LDS slot %u", slot);
+            xb[slot] = v0;
+            xb[slot + 1] = v1;
+          }
+        }
+      if ((cols & 1) && p0 + s == npanels - 1) {
+        const uint32_t slot = cols - 1 - (p0 + s) * c.VP;
+        CHECK(slot < (uint32_t)c.VP, "odd patch slot %u", slot);
+        xb[slot] = xlast;
+      }
+      return xb;
+    };
+    for (uint32_t s = 0; s < npu; ++s) {
+      const std::vector<double> xs = panel(s);
+      const uint32_t beg = segl[s], end = segl[s + 1];
+      CHECK(beg <= end, "segment %u [%u,%u)", s, beg, end);
+      std::set<uint32_t> written;  // y rows written this step (race check)
+      const uint32_t lbeg = segl[std::min(s, npad)];  // load_e(s), issued DE steps earlier
+      for (int ct = 0; ct < CT; ++ct) {
+        std::vector<uint32_t> cc(c.EPT);
+        std::vector<double> vv(c.EPT);
+        for (int j = 0; j < c.EPT; ++j) {  // branch-free clamped loads
+          const uint32_t i = std::min(lbeg + ct + j * CT, last);
+          cc[j] = code.get(i);
+          vv[j] = vals.get(i);
+        }
+        for (int j = 0; j < c.EPT; ++j) {
+          const uint32_t ei = beg + ct + j * CT;
+          const bool act = ei < end && !(cc[j] & kVcCont);
+          if (!act) continue;
+          const uint32_t row = (cc[j] >> 16) & 0x3FFF, col = cc[j] & 0xFFFF;
+          CHECK(row < nr, "row_local %u >= nr %u (unit %u step %u)", row, nr, bid, s);
+          CHECK(col < (uint32_t)c.VP, "col_local %u", col);
+          CHECK(!written.count(row), "race: row %u written twice in step %u of unit %u", row, s, bid);
+          written.insert(row);
+          double acc = madd(ylds[row], vv[j], xs[col]);
+          if (cc[j] & kVcMore) {
+            uint32_t i = ei, cd = cc[j];
+            do {
+              ++i;
+              cd = code.get(i);
+              acc = madd(acc, vals.get(i), xs[cd & 0xFFFF]);
+            } while (cd & kVcMore);
+          }
+          ylds[row] = acc;
+        }
+        for (uint32_t q = beg + c.EPT * CT + ct; q < end; q += CT) {  // overflow
+          uint32_t cd = code.get(q);
+          if (cd & kVcCont) continue;
+          const uint32_t row = (cd >> 16) & 0x3FFF;
+          CHECK(row < nr && !written.count(row), "overflow row %u", row);
+          written.insert(row);
+          double acc = madd(ylds[row], vals.get(q), xs[cd & 0xFFFF]);
+          uint32_t i = q;
+          while (cd & kVcMore) {
+            ++i;
+            cd = code.get(i);
+            acc = madd(acc, vals.get(i), xs[cd & 0xFFFF]);
+          }
+          ylds[row] = acc;
+        }
+      }
+    }
+    if (c.SPLIT == 1) {
+      for (uint32_t i = 0; i < nr; ++i) Y.put(r0 + i, ylds[i]);
+    } else {
+      for (uint32_t i = 0; i < nr; ++i) partial.put((size_t)h * rows + r0 + i, ylds[i]);
+      ylds_of[bid] = ylds;
+    }
+  }
+  if (c.SPLIT == 2) {  // every block: the second arriver (either order) writes p0 + p1
+    for (uint32_t bid = 0; bid < units; ++bid) {
+      const uint32_t b = b_of[bid], h = h_of[bid];
+      if (++tickets[b] != 2) continue;  // arrival order = unit order here; the sum is order-independent
+      const uint32_t r0 = b * rpb, nr = std::min(rpb, rows - r0);
+      for (uint32_t i = 0; i < nr; ++i) {
+        const double o = partial.get((size_t)(1 - h) * rows + r0 + i), m = ylds_of[bid][i];
+        Y.put(r0 + i, h == 0 ? m + o : o + m);
+      }
+    }
+    for (uint32_t b = 0; b < nblocks; ++b) CHECK(tickets[b] == 2, "block %u tickets %u", b, tickets[b]);
+  }
+  return Y.v;
+}
+
+static std::vector<double> reference(const HostCSR& A, const std::vector<double>& x, const std::vector<double>& yin,
+                                     int beta) {
+  std::vector<double> y(A.rows);
+  for (uint32_t r = 0; r < A.rows; ++r) {
+    double acc = beta ? yin[r] : 0.0;
+    for (uint32_t e = A.rowptr[r]; e < A.rowptr[r + 1]; ++e) {
+      double v;
+      std::memcpy(&v, &A.vals[e], 8);
+      acc = madd(acc, v, x[A.colind[e]]);
+    }
+    y[r] = acc;
+  }
+  return y;
+}
+
+static HostCSR random_csr(uint32_t rows, uint32_t cols, double density, uint64_t seed, bool long_row) {
+  HostCSR A;
+  A.rows = rows;
+  A.cols = cols;
+  A.rowptr.assign(rows + 1, 0);
+  uint64_t k = 0;
+  for (uint32_t r = 0; r < rows; ++r) {
+    const bool empty = (splitmix64_at(seed, 1000000 + r) % 7) == 0;
+    for (uint32_t c0 = 0; c0 < cols; ++c0) {
+      const double u = (double)(splitmix64_at(seed, (uint64_t)r * cols + c0) >> 11) * 0x1.0p-53;
+      if ((!empty && u < density) || (long_row && r == rows / 2)) {
+        A.colind.push_back(c0);
+        const double v = uniform11(splitmix64_at(seed + 1, k++));
+        uint64_t bits;
+        std::memcpy(&bits, &v, 8);
+        A.vals.push_back(bits);
+      }
+    }
+    A.rowptr[r + 1] = (uint32_t)A.colind.size();
+  }
+  A.nnz = (uint32_t)A.colind.size();
+  return A;
+}
+
+int main(int argc, char** argv) {
+  // cases: stripe C3-like (scaled), random ragged, odd cols, a long row
+  struct Case {
+    std::string name;
+    HostCSR A;
+  };
+  std::vector<Case> cases;
+  const int big = argc > 1 ? std::atoi(argv[1]) : 16;
+  {
+    const uint32_t n = 1u << big, k = 32;
+    HostCSR A;
+    A.rows = A.cols = n;
+    A.nnz = n * k;
+    A.rowptr.resize(n + 1);
+    A.colind.resize(A.nnz);
+    std::vector<double> v(A.nnz);
+    genStripeCSR(0, n, n, k, 1, 2, A.rowptr.data(), A.colind.data(), v.data());
+    A.vals.resize(A.nnz);
+    std::memcpy(A.vals.data(), v.data(), 8ull * A.nnz);
+    cases.push_back({"stripe 2^" + std::to_string(big), std::move(A)});
+  }
+  cases.push_back({"random 3000x20001", random_csr(3000, 20001, 0.002, 7, true)});
+  cases.push_back({"random 5000x333", random_csr(5000, 333, 0.12, 9, false)});
+  cases.push_back({"random 257x12161 dense rows", random_csr(257, 12161, 0.3, 11, true)});
+  cases.push_back({"random 70000x13001", random_csr(70000, 13001, 0.0008, 13, false)});
+  // must match VcCfg<1>/VcCfg<2> in csrc/vcache.hip (WL, DE, EPT)
+  const Cfg cfgs[] = {{kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1}, {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2}};
+  int failures = 0;
+  for (auto& cs : cases) {
+    std::vector<double> x(cs.A.cols), yin(cs.A.rows);
+    for (uint32_t i = 0; i < cs.A.cols; ++i) x[i] = uniform11(splitmix64_at(3, i));
+    for (uint32_t i = 0; i < cs.A.rows; ++i) yin[i] = uniform11(splitmix64_at(5, i));
+    for (const Cfg& c : cfgs) {
+      const VcGeom g{c.VR, c.VP, c.SPLIT};
+      if (!vcache_eligible(cs.A, g)) {
+        std::printf("%-28s split=%d: not eligible\n", cs.name.c_str(), c.SPLIT);
+        continue;
+      }
+      VcacheLayout L;
+      build_vcache(cs.A, g, L);
+      for (int beta = 0; beta < 2; ++beta) {
+        g_errors = 0;
+        const auto y = simulate(cs.A, L, c, x, yin, beta);
+        const auto r = reference(cs.A, x, yin, beta);
+        size_t bad = 0;
+        for (uint32_t i = 0; i < cs.A.rows; ++i) {
+          if (c.SPLIT == 1) {
+            bad += std::memcmp(&y[i], &r[i], 8) != 0;
+          } else {
+            double absp = std::fabs(beta ? yin[i] : 0.0);
+            uint32_t len = cs.A.rowptr[i + 1] - cs.A.rowptr[i];
+            for (uint32_t e = cs.A.rowptr[i]; e < cs.A.rowptr[i + 1]; ++e) {
+              double v;
+              std::memcpy(&v, &cs.A.vals[e], 8);
+              absp += std::fabs(v * x[cs.A.colind[e]]);
+            }
+            bad += !(std::fabs(y[i] - r[i]) <= 2.0 * (len + 1) * 0x1.0p-53 * absp + 1e-300);
+          }
+        }
+        const bool ok = bad == 0 && g_errors == 0;
+        failures += !ok;
+        std::printf("%-28s split=%d beta=%d units=%u panels=%u: %s (%zu rows off, %d violations)\n",
+                    cs.name.c_str(), c.SPLIT, beta, L.nblocks * c.SPLIT, L.npanels, ok ? "ok" : "FAIL", bad,
+                    g_errors);
+      }
+    }
+  }
+  return failures ? 1 : 0;
+}

@@ -1,0 +1,18 @@
+"""CPU replay of the vcache kernel's addressing (spmv-vector-cache_amd/tools/
+vc_sim.cpp): every global/LDS index in bounds, no two lanes updating one LDS y
+row in the same panel step, ordered geometry bit-exact and split geometry within
+the FAST bound -- on the product layout (csrc/plan.cpp) for stripe, ragged,
+odd-column and long-row matrices.  Runs without a GPU."""
+import os
+import subprocess
+
+import hipspmv as hs
+
+
+def test_vcache_addressing_replay():
+    subprocess.run(["make", "-C", hs.PKG_DIR, "lib/vc_sim"], check=True, stdout=subprocess.DEVNULL)
+    out = subprocess.run([os.path.join(hs.LIB_DIR, "vc_sim"), "15"], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = [l for l in out.stdout.splitlines() if "split=" in l]
+    assert sum(": ok" in l for l in lines) >= 16, out.stdout
+    assert "VIOLATION" not in out.stderr
