@@ -1,0 +1,157 @@
+"""bench.py's host logic on CPU: the HIP handle and the torch.cuda surface are
+replaced by stand-ins (the handle computes y with the oracle), so the contract
+JSON, the timing/parity/roofline/cpu_baseline legs and the N>1 code path
+(gloo, world size 2) are exercised without a GPU.  The real kernels are
+covered by the -m gpu tests; this only guards the script itself."""
+import io
+import json
+import os
+import socket
+import sys
+import time
+from contextlib import redirect_stdout
+
+import numpy as np
+import pytest
+import torch
+
+import hipspmv as hs
+import oracle
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class FakeHandle:
+    def __init__(self, rowptr, colind, vals, rows, cols, device=0):
+        self.rows, self.cols = rows, cols
+        self.colptr, self.rowind, self.cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+        self.nnz = colind.size
+        self.kernel = "auto"
+
+    @classmethod
+    def from_csr(cls, rowptr, colind, vals, rows, cols, device=0):
+        return cls(rowptr, colind, vals, rows, cols, device)
+
+    def set_kernel(self, k):
+        self.kernel = k
+
+    def kernel_name(self, mode):
+        return "vcache_split" if mode == hs.MODE_FAST else "vcache"
+
+    def exec_device(self, x, y_out, y_in=None, beta=0, mode=hs.MODE_ORDERED, stream=None):
+        y = oracle.spmv_csc(self.colptr, self.rowind, self.cvals, x.numpy(), rows=self.rows)
+        y_out.copy_(torch.from_numpy(y))
+
+    def stat(self, key):
+        assert key == "alg_bytes"
+        return 12 * self.nnz + 4 * (self.rows + 1) + 8 * self.cols + 8 * self.rows
+
+    def close(self):
+        pass
+
+
+class FakeEvent:
+    def __init__(self, enable_timing=True):
+        self.t = None
+
+    def record(self, stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
+
+
+class FakeStream:
+    cuda_stream = 0
+
+
+def _patch(monkeypatch):
+    import bench
+    monkeypatch.setattr(bench.hs.Handle, "from_csr", FakeHandle.from_csr)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: None)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: None)
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda *a: FakeStream())
+    monkeypatch.setattr(torch.cuda, "Event", FakeEvent)
+    real_device = torch.device
+    monkeypatch.setattr(bench.torch, "device", lambda *a, **k: real_device("cpu"))
+    return bench
+
+
+def _run(bench, argv):
+    old = sys.argv
+    sys.argv = ["bench.py"] + argv
+    buf = io.StringIO()
+    try:
+        with redirect_stdout(buf):
+            bench.main()
+    finally:
+        sys.argv = old
+    lines = [l for l in buf.getvalue().splitlines() if l.startswith("{")]
+    return json.loads(lines[-1]) if lines else None
+
+
+def test_bench_json_contract_single(monkeypatch):
+    sys.path.insert(0, REPO)
+    bench = _patch(monkeypatch)
+    out = _run(bench, ["--steps", "2", "--warmup", "1", "--log2-rows", "12", "--log2-cols", "12",
+                       "--cpu-seconds", "0.05"])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert key in out, key
+    assert out["n_gpus"] == 1 and out["steps"] == 2 and out["scaling"] == "weak" and out["dtype"] == "f64"
+    assert out["config"]["workload"].startswith("C3") and out["config"]["mode"] == "fast"
+    rf = out["roofline"]
+    assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and abs(rf["frac"] - rf["achieved"] / 8000.0) < 1e-3
+    cb = out["cpu_baseline"]
+    assert cb["cores"] == 1 and cb["kind"] == "port" and cb["value"] > 0
+    # the stand-in computes the ordered result, so both legs must pass their parity checks
+    assert out["parity"].startswith("within FAST bound")
+    assert out["secondary"]["mode"] == "ordered" and out["secondary"]["parity"] == "bit-exact vs oracle"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, q):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "spmv-vector-cache_amd"))
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import torch.distributed as dist
+
+    class MP:  # minimal monkeypatch
+        def setattr(self, obj, name, val):
+            setattr(obj, name, val)
+
+    bench = _patch(MP())
+    real_init = dist.init_process_group
+    dist.init_process_group = lambda backend, device_id=None: real_init("gloo", rank=rank, world_size=world)
+    out = _run(bench, ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--log2-rows", "10",
+                       "--log2-cols", "10", "--no-cpu-baseline"])
+    q.put((rank, out))
+
+
+def test_bench_multi_rank_gloo():
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None  # only rank 0 prints the line
+    out = res[0]
+    assert out["n_gpus"] == 2 and out["x_bcast_us"] is not None
+    assert out["config"]["parallelism"].startswith("row-partition x2")
+    # value is the whole-job rate: both ranks' flops over the max step time
+    assert abs(out["value"] - 2 * 2 * out["config"]["nnz_per_gpu"] / (out["ms_per_step"] * 1e-3) / 1e9) < 0.02 * out["value"]
