@@ -260,6 +260,35 @@ int main(int argc, char** argv) {
     std::memcpy(A.vals.data(), v.data(), 8ull * A.nnz);
     cases.push_back({"stripe 2^" + std::to_string(big), std::move(A)});
   }
+  // row shards of the 2^20-column stripe matrix, as the row-partition and
+  // golden-vector GPU tests create them (tests/test_golden_vectors.py)
+  for (const uint32_t shard : {43691u, 65536u}) {
+    const uint32_t n = shard, cols = 1u << 20, k = 32;
+    HostCSR A;
+    A.rows = n;
+    A.cols = cols;
+    A.nnz = n * k;
+    A.rowptr.resize(n + 1);
+    A.colind.resize(A.nnz);
+    std::vector<double> v(A.nnz);
+    genStripeCSR(43690, n, cols, k, 1, 2, A.rowptr.data(), A.colind.data(), v.data());
+    A.vals.resize(A.nnz);
+    std::memcpy(A.vals.data(), v.data(), 8ull * A.nnz);
+    cases.push_back({"stripe shard " + std::to_string(n) + "x2^20", std::move(A)});
+  }
+  {
+    std::vector<uint32_t> rp, ci;
+    std::vector<double> v;
+    genRmatCSR(14, 16, 4, 0.57, 0.19, 0.19, rp, ci, v);
+    HostCSR A;
+    A.rows = A.cols = 1u << 14;
+    A.nnz = (uint32_t)ci.size();
+    A.rowptr = rp;
+    A.colind = ci;
+    A.vals.resize(A.nnz);
+    std::memcpy(A.vals.data(), v.data(), 8ull * A.nnz);
+    cases.push_back({"rmat s14", std::move(A)});
+  }
   cases.push_back({"random 3000x20001", random_csr(3000, 20001, 0.002, 7, true)});
   cases.push_back({"random 5000x333", random_csr(5000, 333, 0.12, 9, false)});
   cases.push_back({"random 257x12161 dense rows", random_csr(257, 12161, 0.3, 11, true)});
