@@ -115,6 +115,35 @@ const char *hipspmv_kernel_name(hipspmv_t *h, int mode);
 
 int hipspmv_destroy(hipspmv_t *h);
 
+/* Matrix preprocessing statistics on the GPU.  Replaces
+ * SoftwareSpMV::measurePreprocessingTimes (software/SoftwareSpMV.cpp:72-95)
+ * and the SparseMatrix scans it times: maxColSpan (SparseMatrix.cpp:110-119),
+ * maxAlive (SparseMatrix.cpp:92-108) and markRowStarts(false, 31)
+ * (SparseMatrix.cpp:52-90, timed only).  Row ids are read with bits 30-31
+ * masked, so the values are the reference's on an unmarked matrix (as
+ * measurePreprocessingTimes runs them) even if A carries CMS marks.  Input is
+ * the SparseMatrix CSC (colptr[cols+1], rowind[nnz]); times are GPU kernel
+ * time in ns with the data resident (h2d_ns is the upload). */
+typedef struct {
+  uint32_t max_alive;
+  uint32_t max_col_span;
+  uint64_t max_alive_ns;
+  uint64_t max_col_span_ns;
+  uint64_t cms_ns;
+  uint64_t h2d_ns;
+} hipspmv_prep_stats_t;
+
+int hipspmv_prep_stats(const uint32_t *colptr, const uint32_t *rowind, uint32_t rows, uint32_t cols, uint32_t nnz,
+                       int device, hipspmv_prep_stats_t *out);
+
+/* SparseMatrix::markRowStarts(reverse, shift) (SparseMatrix.cpp:52-90) on the
+ * GPU: rowind_out[e] = rowind[e] | 1 << shift for the first (reverse: last)
+ * entry of every row in storage order, other entries copied.  Rows are
+ * compared with bits 30-31 masked; rowind_out may equal rowind.  kernel_ns
+ * (may be NULL) receives the GPU time without the transfers. */
+int hipspmv_mark_row_starts(const uint32_t *rowind, uint32_t *rowind_out, uint32_t rows, uint32_t nnz, int reverse,
+                            int shift, int device, uint64_t *kernel_ns);
+
 const char *hipspmv_strerror(int status);
 /* Text of the last HIP error seen by this thread (static per-thread buffer). */
 const char *hipspmv_last_error(void);

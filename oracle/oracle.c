@@ -85,13 +85,15 @@ uint32_t oracle_max_alive(uint32_t rows, uint32_t nz, uint32_t *inds) {
 
 /* software/SparseMatrix.cpp:110-119.  The reference reads
  * inds[colptr[c+1]-1] - inds[colptr[c]] with unsigned wrap-around, also for
- * empty columns (where it reads the neighbouring column's entries); restated
- * as is, but an empty column at c == 0 would read inds[-1], so that case
- * contributes 0 here (documented in DESIGN.md). */
+ * empty columns (where it reads the neighbouring columns' entries); restated
+ * as is, except that an empty column whose reads would leave [0, nnz) -- a
+ * leading one reads inds[-1], a trailing one inds[nnz] -- contributes 0
+ * (undefined in the reference). */
 uint32_t oracle_max_col_span(uint32_t cols, const uint32_t *colptr, const uint32_t *inds) {
   uint32_t best = 0;
+  const uint32_t nz = colptr[cols];
   for (uint32_t c = 0; c < cols; c++) {
-    if (colptr[c + 1] == 0) continue;
+    if (colptr[c + 1] == 0 || colptr[c] >= nz || colptr[c + 1] > nz) continue;
     const uint32_t span = inds[colptr[c + 1] - 1] - inds[colptr[c]];
     if (span > best) best = span;
   }

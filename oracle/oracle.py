@@ -76,3 +76,22 @@ def csr2csc(n_rows, n_cols, rowptr, colind, vals):
 def time_spmv_csc_f64(colptr, rowind, vals, x, rows, reps):
     y = np.zeros(rows, dtype=np.float64)
     return lib().oracle_time_spmv_csc_f64(rows, colptr.size - 1, colptr, rowind, vals, x, y, reps), y
+
+
+def mark_row_starts(inds, rows, reverse=False, shift=31):
+    """SparseMatrix::markRowStarts restated; returns a marked copy."""
+    out = np.array(inds, dtype=np.uint32, copy=True)
+    lib().oracle_mark_row_starts(rows, out.size, out, int(reverse), shift)
+    return out
+
+
+def max_alive(inds, rows):
+    """SparseMatrix::maxAlive restated (on a copy: the reference marks A in place)."""
+    out = np.array(inds, dtype=np.uint32, copy=True)
+    return int(lib().oracle_max_alive(rows, out.size, out))
+
+
+def max_col_span(colptr, inds):
+    """SparseMatrix::maxColSpan restated."""
+    colptr = np.ascontiguousarray(colptr, dtype=np.uint32)
+    return int(lib().oracle_max_col_span(colptr.size - 1, colptr, np.ascontiguousarray(inds, dtype=np.uint32)))

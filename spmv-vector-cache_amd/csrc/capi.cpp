@@ -62,6 +62,8 @@ uint64_t now_ns() {
 
 }  // namespace
 
+void hipspmv::set_last_error(const std::string& what) { g_last_error = what; }
+
 struct hipspmv_handle {
   int device = 0, dtype = HIPSPMV_F64;
   uint32_t rows = 0, cols = 0, nnz = 0;
@@ -400,6 +402,24 @@ int hipspmv_destroy(hipspmv_t* h) {
   if (!h) return HIPSPMV_ERR_INVALID_ARG;
   release(h);
   return HIPSPMV_OK;
+}
+
+int hipspmv_prep_stats(const uint32_t* colptr, const uint32_t* rowind, uint32_t rows, uint32_t cols, uint32_t nnz,
+                       int device, hipspmv_prep_stats_t* out) {
+  try {
+    return prep_stats(colptr, rowind, rows, cols, nnz, device, out);
+  } catch (...) {
+    return HIPSPMV_ERR_OOM;
+  }
+}
+
+int hipspmv_mark_row_starts(const uint32_t* rowind, uint32_t* rowind_out, uint32_t rows, uint32_t nnz, int reverse,
+                            int shift, int device, uint64_t* kernel_ns) {
+  try {
+    return mark_row_starts(rowind, rowind_out, rows, nnz, reverse, shift, device, kernel_ns);
+  } catch (...) {
+    return HIPSPMV_ERR_OOM;
+  }
 }
 
 const char* hipspmv_strerror(int status) {

@@ -6,6 +6,8 @@
 #include <string>
 #include <vector>
 
+#include "hipspmv.h"
+
 namespace hipspmv {
 
 // ---- vcache kernel geometry ---------------------------
@@ -61,5 +63,14 @@ bool vcache_eligible(const HostCSR& a, const VcGeom& g);
 void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out);
 // Row groups for csr_vector: group g covers rows [groups[g], groups[g+1]).
 void build_row_groups(const HostCSR& a, std::vector<uint32_t>& groups);
+
+// hipspmv_last_error() text for this thread (capi.cpp).
+void set_last_error(const std::string& what);
+
+// csrc/prep.hip: the bodies of hipspmv_prep_stats / hipspmv_mark_row_starts.
+int prep_stats(const uint32_t* colptr, const uint32_t* rowind, uint32_t rows, uint32_t cols, uint32_t nnz,
+               int device, hipspmv_prep_stats_t* out);
+int mark_row_starts(const uint32_t* rowind, uint32_t* rowind_out, uint32_t rows, uint32_t nnz, int reverse,
+                    int shift, int device, uint64_t* kernel_ns);
 
 }  // namespace hipspmv

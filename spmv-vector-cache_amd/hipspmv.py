@@ -61,6 +61,12 @@ def build(force: bool = False) -> None:
         subprocess.run(["make", "-C", PKG_DIR, "-j8"], check=True)
 
 
+class PrepStats(C.Structure):
+    """hipspmv_prep_stats_t (include/hipspmv.h)"""
+    _fields_ = [("max_alive", C.c_uint32), ("max_col_span", C.c_uint32), ("max_alive_ns", C.c_uint64),
+                ("max_col_span_ns", C.c_uint64), ("cms_ns", C.c_uint64), ("h2d_ns", C.c_uint64)]
+
+
 def declared_symbols() -> list[str]:
     """Function names declared in include/hipspmv.h."""
     text = open(HEADER).read()
@@ -91,9 +97,13 @@ def load_hipspmv() -> C.CDLL:
     lib.hipspmv_last_error.restype = C.c_char_p
     lib.hipspmv_abi_version.argtypes = []
     lib.hipspmv_device_count.argtypes = [C.POINTER(C.c_int)]
+    lib.hipspmv_prep_stats.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                       C.POINTER(PrepStats)]
+    lib.hipspmv_mark_row_starts.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int,
+                                            C.POINTER(C.c_uint64)]
     for name in ("hipspmv_create", "hipspmv_create_csr", "hipspmv_set_option", "hipspmv_exec",
                  "hipspmv_exec_device", "hipspmv_stat", "hipspmv_destroy", "hipspmv_abi_version",
-                 "hipspmv_device_count"):
+                 "hipspmv_device_count", "hipspmv_prep_stats", "hipspmv_mark_row_starts"):
         getattr(lib, name).restype = C.c_int
     _hip = lib
     return lib
@@ -214,6 +224,27 @@ class Handle:
             self.close()
         except Exception:
             pass
+
+
+def prep_stats(colptr: np.ndarray, rowind: np.ndarray, rows: int, device: int = 0) -> dict:
+    """SoftwareSpMV::measurePreprocessingTimes on the GPU (hipspmv_prep_stats):
+    maxAlive, maxColSpan and the GPU times of the three scans, for a CSC matrix."""
+    colptr = np.ascontiguousarray(colptr, dtype=np.uint32)
+    rowind = np.ascontiguousarray(rowind, dtype=np.uint32)
+    out = PrepStats()
+    _check(load_hipspmv().hipspmv_prep_stats(_ptr(colptr), _ptr(rowind), rows, colptr.size - 1, rowind.size,
+                                             device, C.byref(out)), "prep_stats")
+    return {f: getattr(out, f) for f, _ in PrepStats._fields_}
+
+
+def mark_row_starts(rowind: np.ndarray, rows: int, reverse: bool = False, shift: int = 31, device: int = 0):
+    """SparseMatrix::markRowStarts on the GPU; returns (marked copy, kernel ns)."""
+    rowind = np.ascontiguousarray(rowind, dtype=np.uint32)
+    out = np.empty_like(rowind)
+    ns = C.c_uint64()
+    _check(load_hipspmv().hipspmv_mark_row_starts(_ptr(rowind), _ptr(out), rows, rowind.size, int(reverse), shift,
+                                                  device, C.byref(ns)), "mark_row_starts")
+    return out, int(ns.value)
 
 
 def device_count() -> int:

@@ -86,9 +86,24 @@ uint64_t HIPSpMV::statU64(const std::string& key) {
 std::vector<std::string> HIPSpMV::statKeys() {
   std::vector<std::string> keys = HardwareSpMV::statKeys();
   for (const char* k : {"kernelTimeUs", "setupTimeUs", "h2dTimeUs", "d2hTimeUs", "algKBytes", "mode", "kernel",
-                        "device", "error"})
+                        "device", "error", "maxAlive", "maxColSpan", "cmstime", "maxAliveTime", "maxColSpanTime"})
     keys.push_back(k);
   return keys;
+}
+
+// The SoftwareSpMV preprocessing statistics (SoftwareSpMV.cpp:72-95), computed
+// on the GPU once per matrix version (hipspmv_prep_stats); times in us.
+const hipspmv_prep_stats_t& HIPSpMV::prepStats() {
+  if (m_prepVersion != m_A->version()) {
+    m_prep = hipspmv_prep_stats_t{};
+    int st = hipspmv_prep_stats(m_A->getIndPtrs(), m_A->getInds(), m_A->getRows(), m_A->getCols(), m_A->getNz(),
+                                regs()->device, &m_prep);
+    if (st)
+      std::cerr << "HIPSpMV: prep_stats failed: " << hipspmv_strerror(st) << " (" << hipspmv_last_error() << ")"
+                << std::endl;
+    m_prepVersion = m_A->version();
+  }
+  return m_prep;
 }
 
 unsigned int HIPSpMV::statInt(std::string name) {
@@ -101,6 +116,11 @@ unsigned int HIPSpMV::statInt(std::string name) {
   if (name == "kernel") return (unsigned int)statU64("kernel");
   if (name == "device") return (unsigned int)regs()->device;
   if (name == "error") return (unsigned int)m_status;
+  if (name == "maxAlive") return prepStats().max_alive;
+  if (name == "maxColSpan") return prepStats().max_col_span;
+  if (name == "cmstime") return (unsigned int)(prepStats().cms_ns / 1000);
+  if (name == "maxAliveTime") return (unsigned int)(prepStats().max_alive_ns / 1000);
+  if (name == "maxColSpanTime") return (unsigned int)(prepStats().max_col_span_ns / 1000);
   if (name == "thresColPtr") return m_thres_colPtr;
   if (name == "thresRowInd") return m_thres_rowInd;
   if (name == "thresNZData") return m_thres_nzData;

@@ -11,6 +11,7 @@
 #include <cstdint>
 
 #include "HardwareSpMV.h"
+#include "hipspmv.h"
 
 struct hipspmv_handle;
 
@@ -55,7 +56,11 @@ class HIPSpMV : public HardwareSpMV {
   virtual void write();
   virtual void setThresholdRegisters();
 
+  const hipspmv_prep_stats_t& prepStats();
+
   hipspmv_handle* m_h = nullptr;
+  hipspmv_prep_stats_t m_prep{};
+  uint64_t m_prepVersion = ~0ull;
   uint64_t m_builtVersion = ~0ull;
   int m_status = 0;
 };

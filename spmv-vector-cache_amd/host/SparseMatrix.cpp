@@ -89,8 +89,11 @@ unsigned int SparseMatrix::maxAlive() {
 // of reading before the index array.
 unsigned int SparseMatrix::maxColSpan() {
   unsigned int best = 0;
+  // SparseMatrix.cpp:110-119, also for empty columns (they read the
+  // neighbouring columns' entries); reads that would leave [0, nz) -- the
+  // reference's undefined cases -- contribute nothing.
   for (SpMVIndex c = 0; c < m_cols; ++c) {
-    if (m_indPtrs[c + 1] == 0) continue;
+    if (m_indPtrs[c + 1] == 0 || m_indPtrs[c] >= m_nz || m_indPtrs[c + 1] > m_nz) continue;
     const unsigned int span = m_inds[m_indPtrs[c + 1] - 1] - m_inds[m_indPtrs[c]];
     if (span > best) best = span;
   }
