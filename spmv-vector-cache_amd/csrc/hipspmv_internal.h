@@ -10,14 +10,14 @@
 
 namespace hipspmv {
 
-// ---- vcache kernel geometry (see DESIGN.md §3.1) ---------------------------
+// ---- vcache kernel geometry (see DESIGN.md §6.1) ---------------------------
 // One 1024-thread workgroup per work unit = (row block, column part); LDS
 // holds the block's y accumulators (<= rows doubles), two x panels of `panel`
 // doubles and the unit's segment table (<= kVcSegMax offsets), 163840 B total:
 //   ordered: 4096 rows, 1 part  : 32768 + 2*8128*8 + 1024
 //   split  : 8192 rows, 2 parts : 65536 + 2*6080*8 + 1024
 // The split geometry halves the x bytes each CU streams (the measured limit,
-// DESIGN.md §3.1) and combines the two column-half partials in fixed order
+// DESIGN.md §6.0) and combines the two column-half partials in fixed order
 // (p0 + p1), so it is deterministic but not bit-identical: FAST mode.
 struct VcGeom {
   int rows, panel, split;

@@ -6,9 +6,9 @@
 // Compiled with -ffp-contract=off, and every body repeats
 // `#pragma clang fp contract(off)`, so no a*b+c is fused.
 //
-//   k_csr_lane   ordered; one lane per CSR row, any matrix.      DESIGN.md §3.2
+//   k_csr_lane   ordered; one lane per CSR row, any matrix.      DESIGN.md §6.2
 //   k_csr_vector fast; row groups, one wave each, wave-level segmented scan
-//                with DPP row_shr / row_bcast.                   DESIGN.md §3.3
+//                with DPP row_shr / row_bcast.                   DESIGN.md §6.3
 // The LDS vector-cache kernel is in vcache.hip.
 #include <hip/hip_runtime.h>
 
@@ -62,7 +62,7 @@ __device__ __forceinline__ void seg_step(T& v, uint32_t& f) {
 // Inclusive segmented sum across the 64 lanes (segment heads have f = 1):
 // row_shr:1,2,4,8 scan each 16-lane DPP row, then row_bcast:15 carries the
 // row tails into rows 1 and 3 and row_bcast:31 carries lane 31 into rows 2
-// and 3 (gfx9 DPP; DESIGN.md §3.3).
+// and 3 (gfx9 DPP; DESIGN.md §6.3).
 template <typename T>
 __device__ __forceinline__ T wave_segscan(T v, uint32_t f) {
   seg_step<0x111, 0xF>(v, f);  // row_shr:1

@@ -1,5 +1,5 @@
 // Host-side planning for libhipspmv: CSC -> CSR transpose, validation, and the
-// device layouts each kernel reads (DESIGN.md §3).
+// device layouts each kernel reads (DESIGN.md §4).
 #include <algorithm>
 #include <cstring>
 

@@ -1,4 +1,4 @@
-// k_vcache: the LDS "vector cache" SpMV kernel for gfx950 (DESIGN.md §3.1).
+// k_vcache: the LDS "vector cache" SpMV kernel for gfx950 (DESIGN.md §6.1).
 //
 // The reference's accelerators stream A in column order and keep the output
 // vector y in an on-chip vector cache (chisel/cache-new/NoWMVectorCache.scala,

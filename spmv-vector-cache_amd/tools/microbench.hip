@@ -2,7 +2,7 @@
 //
 // Not product code: a standalone probe, run once per design question, that
 // times candidate inner loops of the SpMV row gather on the C3 workload
-// (2^20 x 2^20, 32 nnz/row, one column per 2^15-wide stripe; DESIGN.md §2)
+// (2^20 x 2^20, 32 nnz/row, one column per 2^15-wide stripe; DESIGN.md §5)
 // generated on the device, so that kernel structure is chosen from
 // measurements rather than guesses.
 //
