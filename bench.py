@@ -1,14 +1,19 @@
 #!/usr/bin/env python3
 """bench.py -- SpMV GFLOP/s and HBM-roofline fraction on MI355X (BASELINE.json).
 
-Workload (config C3 of BASELINE.json, weak-scaled): every rank owns a
-2^20-row shard of a synthetic stripe-uniform CSR matrix with 2^20 columns and
-32 nonzeros per row (DESIGN.md §5 generator; rank r owns global rows
-[r*2^20, (r+1)*2^20)), fp64, and x (2^20 doubles) is broadcast from rank 0
-over RCCL once, before the timed region (inputs resident in HBM).  One step =
-one y = A_shard * x on every rank through the C ABI (hipspmv_exec_device) on
-torch's current stream.  value = 2 * nnz(all ranks) / (max over ranks of the
-per-step wall time).
+Workload (--workload, BASELINE.json configs; generators in DESIGN.md §5):
+  c3 (default, the headline): weak-scaled -- every rank owns a 2^20-row shard
+     of a synthetic stripe-uniform CSR matrix with 2^20 columns and 32
+     nonzeros per row (rank r owns global rows [r*2^20, (r+1)*2^20)).
+  c4: strong-scaled -- the 2^s x 2^s stripe matrix (s = --scale, 24: C4),
+     32 nnz/row, rows split into N equal contiguous blocks.
+  c5: strong-scaled -- R-MAT scale s (24: C5), edge factor 16, rows split
+     nnz-balanced from the per-row edge counts; the per-rank step times are
+     reported (load balance).
+fp64; x is generated on rank 0 and broadcast over RCCL once, before the timed
+region (inputs resident in HBM).  One step = one y = A_shard * x on every
+rank through the C ABI (hipspmv_exec_device) on torch's current stream.
+value = 2 * nnz(all ranks) / (max over ranks of the per-step wall time).
 
 Modes (include/hipspmv.h): the headline runs FAST mode -- the north-star
 contract for f64 is "within a stated tolerance", checked here per row against
@@ -19,7 +24,7 @@ its average duration from HIP events on the launch stream, against 8 TB/s),
 and the CPU baseline (the oracle's SoftwareSpMV restatement, 1 core, on the
 same shard) on rank 0 at N=1.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode fast|ordered]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode fast|ordered] [--workload c3|c4|c5]
                   [--kernel auto|vcache|vcache_split|csr_lane|csr_vector]
                   [--cpu-seconds S] [--no-cpu-baseline] [--no-secondary]
 """
@@ -51,9 +56,13 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--kernel", default="auto", choices=list(hs.KERNELS))
     p.add_argument("--mode", default="fast", choices=list(MODES))
-    p.add_argument("--log2-rows", type=int, default=20)
-    p.add_argument("--log2-cols", type=int, default=20)
+    p.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"])
+    p.add_argument("--scale", type=int, default=24, help="log2 of the matrix dimension for c4/c5")
+    p.add_argument("--log2-rows", type=int, default=20, help="c3: rows per GPU")
+    p.add_argument("--log2-cols", type=int, default=20, help="c3: columns")
     p.add_argument("--nnz-per-row", type=int, default=32)
+    p.add_argument("--cpu-sample-nnz", type=int, default=1 << 25,
+                   help="bound on the nonzeros (leading rows of rank 0's shard) the CPU baseline and parity use")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true", help="skip timing the other mode")
@@ -109,9 +118,30 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    rows, cols, k = 1 << a.log2_rows, 1 << a.log2_cols, a.nnz_per_row
+    k = a.nnz_per_row
     t0 = time.perf_counter()
-    rowptr, colind, vals = hs.gen_stripe_csr(rank * rows, rows, cols, k, 1, 2)
+    if a.workload == "c3":
+        rows, cols = 1 << a.log2_rows, 1 << a.log2_cols
+        row0 = rank * rows
+        rowptr, colind, vals = hs.gen_stripe_csr(row0, rows, cols, k, 1, 2)
+        workload = (f"C3 stripe-uniform CSR {rows}x{cols} per GPU, {k} nnz/row "
+                    f"(rank r owns global rows [r*{rows},(r+1)*{rows}))")
+        scaling = "weak"
+    elif a.workload == "c4":
+        n = 1 << a.scale
+        row0, row1 = n * rank // world, n * (rank + 1) // world
+        rows, cols = row1 - row0, n
+        rowptr, colind, vals = hs.gen_stripe_csr(row0, rows, cols, k, 1, 2)
+        workload = f"C4 stripe-uniform CSR {n}x{n}, {k} nnz/row, {world} equal row blocks"
+        scaling = "strong"
+    else:
+        n = 1 << a.scale
+        bounds = hs.partition_row_counts(hs.gen_rmat_row_counts(a.scale, 16, 4), world)
+        row0, row1 = int(bounds[rank]), int(bounds[rank + 1])
+        rows, cols = row1 - row0, n
+        rowptr, colind, vals = hs.gen_rmat_rows(a.scale, row0, row1, 16, 4)
+        workload = f"C5 R-MAT scale {a.scale} (a,b,c=0.57,0.19,0.19), edge factor 16, {world} nnz-balanced row blocks"
+        scaling = "strong"
     h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols, device=local)
     if a.kernel != "auto":
         h.set_kernel(a.kernel)
@@ -156,19 +186,26 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         wall = time.perf_counter() - tw
+        kern = ev0.elapsed_time(ev1) / a.steps
+        if dist is None:
+            return wall, kern, [kern]
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        if dist is not None:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item()), ev0.elapsed_time(ev1) / a.steps
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        per = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(per, torch.tensor([kern], dtype=torch.float64, device=dev))
+        return float(t.item()), kern, [float(v.item()) for v in per]
 
     mode = MODES[a.mode]
     kname = h.kernel_name(mode)
-    wall_max, kern_ms = timed(mode)
+    wall_max, kern_ms, rank_kern_ms = timed(mode)
     y_main = yd.cpu().numpy().copy() if rank == 0 else None
     ms_per_step = wall_max / a.steps * 1e3
     alg_bytes = h.stat("alg_bytes")  # 12*nnz + 4*(rows+1) + 8*cols + 8*rows per launch
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    total_flops = 2.0 * nnz * world
+    nnz_t = torch.tensor([nnz], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(nnz_t)
+    total_flops = 2.0 * float(nnz_t.item())
     value = total_flops / (ms_per_step * 1e-3) / 1e9
 
     secondary = None
@@ -176,7 +213,7 @@ def main():
     if not a.no_secondary:
         try:
             k2 = h.kernel_name(MODES[other])
-            w2, km2 = timed(MODES[other])
+            w2, km2, _ = timed(MODES[other])
             secondary = {"mode": other, "kernel": "k_" + k2,
                          "value": round(total_flops / (w2 / a.steps) / 1e9, 2),
                          "ms_per_step": round(w2 / a.steps * 1e3, 5), "kernel_us": round(km2 * 1e3, 3),
@@ -196,27 +233,35 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle
-        colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+        # bounded sample: the leading rows of the shard holding <= cpu_sample_nnz nonzeros
+        srows = int(np.searchsorted(rowptr, a.cpu_sample_nnz, side="right")) - 1
+        srows = max(1, min(rows, srows))
+        snnz = int(rowptr[srows])
+        s_rowptr, s_colind, s_vals = rowptr[:srows + 1], colind[:snnz], vals[:snnz]
+        colptr, rowind, cvals = oracle.csr2csc(srows, cols, s_rowptr, s_colind, s_vals)
         x = xd.cpu().numpy()
-        t_one, y_ref = oracle.time_spmv_csc_f64(colptr, rowind, cvals, x, rows, 1)
+        t_one, y_ref = oracle.time_spmv_csc_f64(colptr, rowind, cvals, x, srows, 1)
         reps = max(1, int(a.cpu_seconds / max(t_one, 1e-6)))
-        t_avg, _ = oracle.time_spmv_csc_f64(colptr, rowind, cvals, x, rows, reps)
-        cpu = {"value": round(2.0 * nnz / t_avg / 1e9, 4), "unit": "GFLOP/s", "cores": 1, "kind": "port",
-               "sample": f"oracle SoftwareSpMV (CSC scatter) on rank 0's full shard: {rows} rows, {nnz} nnz, "
+        t_avg, _ = oracle.time_spmv_csc_f64(colptr, rowind, cvals, x, srows, reps)
+        what = "rank 0's full shard" if srows == rows else f"the first {srows} of {rows} rows of rank 0's shard"
+        cpu = {"value": round(2.0 * snnz / t_avg / 1e9, 4), "unit": "GFLOP/s", "cores": 1, "kind": "port",
+               "sample": f"oracle SoftwareSpMV (CSC scatter) on {what}: {srows} rows, {snnz} nnz, "
                          f"x=U[-1,1), {reps + 1} execs, {t_avg * 1e3:.1f} ms each",
                "cpu_model": cpu_model(), "nproc": os.cpu_count()}
         # FAST bound per row (include/hipspmv.h): |y - y_ref| <= 2*len*2^-53*sum_j|a_ij x_j|
-        row_of = np.repeat(np.arange(rows), np.diff(rowptr.astype(np.int64)))
-        absprod = np.bincount(row_of, weights=np.abs(vals * x[colind]), minlength=rows)
-        bound = 2.0 * np.maximum(np.diff(rowptr.astype(np.int64)), 1) * 2.0 ** -53 * absprod + 1e-300
+        lens = np.diff(s_rowptr.astype(np.int64))
+        row_of = np.repeat(np.arange(srows), lens)
+        absprod = np.bincount(row_of, weights=np.abs(s_vals * x[s_colind]), minlength=srows)
+        bound = 2.0 * np.maximum(lens, 1) * 2.0 ** -53 * absprod + 1e-300
 
         def check(y, m):
+            y = y[:srows]
             if m == hs.MODE_ORDERED:
                 bad = int(np.sum(y.view(np.uint64) != y_ref.view(np.uint64)))
                 return "bit-exact vs oracle" if bad == 0 else f"MISMATCH in {bad} rows"
             r = np.abs(y - y_ref) / bound
             exact = int(np.sum(y.view(np.uint64) == y_ref.view(np.uint64)))
-            return (f"within FAST bound (max err/bound {float(r.max()):.3f}; {exact}/{rows} rows bit-exact)"
+            return (f"within FAST bound (max err/bound {float(r.max()):.3f}; {exact}/{srows} rows bit-exact)"
                     if np.all(r <= 1.0) else f"BOUND VIOLATED in {int(np.sum(r > 1.0))} rows")
 
         parity = check(y_main, mode)
@@ -227,11 +272,11 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GFLOP/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 5),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"C3 stripe-uniform CSR {rows}x{cols} per GPU, {k} nnz/row "
-                                   f"(rank r owns global rows [r*{rows},(r+1)*{rows}))",
-                       "rows_per_gpu": rows, "cols": cols, "nnz_per_gpu": nnz, "kernel": kname,
+            "config": {"workload": workload,
+                       "rows_per_gpu": rows, "cols": cols, "nnz_per_gpu": nnz,
+                       "nnz_total": int(nnz_t.item()), "kernel": kname,
                        "mode": a.mode, "parallelism": f"row-partition x{world}, x broadcast (RCCL) before timing"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -242,6 +287,7 @@ def main():
             "parity": parity,
             "secondary": secondary,
             "x_bcast_us": None if bcast_us is None else round(bcast_us, 2),
+            "rank_kernel_us": [round(v * 1e3, 3) for v in rank_kern_ms],
             "setup_s": round(setup_s, 3),
         }
         print(json.dumps(out), flush=True)

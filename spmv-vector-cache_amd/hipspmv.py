@@ -127,6 +127,13 @@ def load_host() -> C.CDLL:
     lib.spmvhost_splitmix64_at.restype = C.c_uint64
     lib.spmvhost_gen_rmat_csr.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, _u32p, _u32p, _f64p]
     lib.spmvhost_gen_rmat_csr.restype = C.c_uint64
+    lib.spmvhost_gen_rmat_rows.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, _u32p, _u32p,
+                                           _f64p, C.c_uint64]
+    lib.spmvhost_gen_rmat_rows.restype = C.c_uint64
+    lib.spmvhost_gen_rmat_row_counts.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, _u32p]
+    lib.spmvhost_gen_rmat_row_counts.restype = None
+    lib.spmvhost_partition_row_counts.argtypes = [_u32p, C.c_uint32, C.c_uint32, _u32p]
+    lib.spmvhost_partition_row_counts.restype = None
     lib.spmvhost_csr2csc.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, _u64p, _u32p, _u32p, _u64p, _u32p, _u32p]
     lib.spmvhost_csr2csc.restype = None
     lib.spmvhost_partition_rows.argtypes = [_u32p, C.c_uint32, C.c_uint32, _u32p]
@@ -276,6 +283,33 @@ def gen_rmat_csr(scale: int, edge_factor: int = 16, seed: int = 4):
     colind = np.empty(m, dtype=np.uint32)
     vals = np.empty(m, dtype=np.float64)
     nnz = lib.spmvhost_gen_rmat_csr(scale, edge_factor, seed, rowptr, colind, vals)
+    return rowptr, colind[:nnz].copy(), vals[:nnz].copy()
+
+
+def gen_rmat_row_counts(scale: int, edge_factor: int = 16, seed: int = 4) -> np.ndarray:
+    counts = np.empty(1 << scale, dtype=np.uint32)
+    load_host().spmvhost_gen_rmat_row_counts(scale, edge_factor, seed, counts)
+    return counts
+
+
+def partition_row_counts(counts: np.ndarray, parts: int) -> np.ndarray:
+    bounds = np.empty(parts + 1, dtype=np.uint32)
+    load_host().spmvhost_partition_row_counts(np.ascontiguousarray(counts, dtype=np.uint32), counts.size, parts, bounds)
+    return bounds
+
+
+def gen_rmat_rows(scale: int, row0: int, row1: int, edge_factor: int = 16, seed: int = 4, cap: int | None = None):
+    """Rows [row0, row1) of gen_rmat_csr(scale, ...), rowptr rebased to 0."""
+    lib = load_host()
+    nr = row1 - row0
+    if cap is None:
+        cap = edge_factor << scale if nr == (1 << scale) else int(gen_rmat_row_counts(scale, edge_factor, seed)[row0:row1].sum(dtype=np.uint64))
+    rowptr = np.empty(nr + 1, dtype=np.uint32)
+    colind = np.empty(max(cap, 1), dtype=np.uint32)
+    vals = np.empty(max(cap, 1), dtype=np.float64)
+    nnz = lib.spmvhost_gen_rmat_rows(scale, edge_factor, seed, row0, row1, rowptr, colind, vals, cap)
+    if nnz > cap:
+        raise RuntimeError(f"gen_rmat_rows: {nnz} nonzeros exceed the capacity {cap}")
     return rowptr, colind[:nnz].copy(), vals[:nnz].copy()
 
 

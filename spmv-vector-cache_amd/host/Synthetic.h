@@ -28,8 +28,28 @@ void genStripeCSR(uint64_t row0, uint32_t nrows, uint32_t cols, uint32_t k, uint
 uint64_t genRmatCSR(uint32_t scale, uint32_t edgeFactor, uint64_t seed, double a, double b, double c,
                     std::vector<uint32_t>& rowptr, std::vector<uint32_t>& colind, std::vector<double>& vals);
 
+// The same matrix restricted to rows [row0, row1) (rowptr rebased to 0,
+// columns global): what a rank of a row-partitioned run generates.  Every
+// edge is still drawn (the row of an edge is only known once drawn), in
+// parallel; equal to the corresponding rows of genRmatCSR.
+uint64_t genRmatCSRRows(uint32_t scale, uint32_t edgeFactor, uint64_t seed, double a, double b, double c,
+                        uint32_t row0, uint32_t row1, std::vector<uint32_t>& rowptr, std::vector<uint32_t>& colind,
+                        std::vector<double>& vals);
+
+// Edges per row before duplicates are summed (counts[2^scale]): the input of
+// an nnz-balanced partition that no rank has to materialise the matrix for.
+void genRmatRowCounts(uint32_t scale, uint32_t edgeFactor, uint64_t seed, double a, double b, double c,
+                      uint32_t* counts);
+
 // nnz-balanced contiguous row partition: bounds[0..parts], bounds[0] = 0,
 // bounds[parts] = rows, each part holding about nnz/parts nonzeros.
 void partitionRows(const uint32_t* rowptr, uint32_t rows, uint32_t parts, uint32_t* bounds);
+// Same from per-row counts: bounds[p] = first row whose prefix count reaches
+// total*p/parts.
+void partitionRowCounts(const uint32_t* counts, uint32_t rows, uint32_t parts, uint32_t* bounds);
+
+// Worker threads of the host generators: $SPMV_THREADS, else
+// $OMP_NUM_THREADS, else min(16, hardware threads).
+unsigned hostThreads();
 
 #endif

@@ -4,6 +4,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "MatrixIO.h"
@@ -18,7 +19,13 @@ void spmvhost_gen_stripe_csr(uint64_t row0, uint32_t nrows, uint32_t cols, uint3
 }
 
 void spmvhost_gen_vector(uint64_t n, uint64_t seed, double* out) {
-  for (uint64_t i = 0; i < n; ++i) out[i] = uniform11(splitmix64_at(seed, i));
+  const unsigned nt = n > (1u << 20) ? hostThreads() : 1;
+  std::vector<std::thread> pool;
+  for (unsigned t = 0; t < nt; ++t)
+    pool.emplace_back([=] {
+      for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) out[i] = uniform11(splitmix64_at(seed, i));
+    });
+  for (auto& th : pool) th.join();
 }
 
 uint64_t spmvhost_splitmix64_at(uint64_t seed, uint64_t i) { return splitmix64_at(seed, i); }
@@ -34,6 +41,29 @@ uint64_t spmvhost_gen_rmat_csr(uint32_t scale, uint32_t edge_factor, uint64_t se
   std::memcpy(colind, ci.data(), sizeof(uint32_t) * nnz);
   std::memcpy(vals, v.data(), sizeof(double) * nnz);
   return nnz;
+}
+
+// Rows [row0, row1) of the R-MAT matrix.  Copies into the caller's arrays
+// (rowptr: row1-row0+1, colind/vals: cap) when nnz <= cap; always returns nnz.
+uint64_t spmvhost_gen_rmat_rows(uint32_t scale, uint32_t edge_factor, uint64_t seed, uint32_t row0, uint32_t row1,
+                                uint32_t* rowptr, uint32_t* colind, double* vals, uint64_t cap) {
+  std::vector<uint32_t> rp, ci;
+  std::vector<double> v;
+  const uint64_t nnz = genRmatCSRRows(scale, edge_factor, seed, 0.57, 0.19, 0.19, row0, row1, rp, ci, v);
+  if (nnz <= cap) {
+    std::memcpy(rowptr, rp.data(), sizeof(uint32_t) * rp.size());
+    std::memcpy(colind, ci.data(), sizeof(uint32_t) * nnz);
+    std::memcpy(vals, v.data(), sizeof(double) * nnz);
+  }
+  return nnz;
+}
+
+void spmvhost_gen_rmat_row_counts(uint32_t scale, uint32_t edge_factor, uint64_t seed, uint32_t* counts) {
+  genRmatRowCounts(scale, edge_factor, seed, 0.57, 0.19, 0.19, counts);
+}
+
+void spmvhost_partition_row_counts(const uint32_t* counts, uint32_t rows, uint32_t parts, uint32_t* bounds) {
+  partitionRowCounts(counts, rows, parts, bounds);
 }
 
 void spmvhost_csr2csc(uint32_t n, uint32_t m, uint32_t nz, const uint64_t* a, const uint32_t* col_idx,

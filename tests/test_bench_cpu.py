@@ -117,7 +117,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, extra=()):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     sys.path.insert(0, REPO)
@@ -133,8 +133,49 @@ def _rank_main(rank, world, port, q):
     real_init = dist.init_process_group
     dist.init_process_group = lambda backend, device_id=None: real_init("gloo", rank=rank, world_size=world)
     out = _run(bench, ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--log2-rows", "10",
-                       "--log2-cols", "10", "--no-cpu-baseline"])
+                       "--log2-cols", "10", "--no-cpu-baseline", *extra])
     q.put((rank, out))
+
+
+def _multi_rank(extra, world=2):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, tuple(extra))) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("workload,scale", [("c4", 11), ("c5", 10)])
+def test_bench_strong_workloads_single(monkeypatch, workload, scale):
+    sys.path.insert(0, REPO)
+    bench = _patch(monkeypatch)
+    out = _run(bench, ["--steps", "2", "--warmup", "1", "--workload", workload, "--scale", str(scale),
+                       "--cpu-seconds", "0.05", "--cpu-sample-nnz", "5000"])
+    assert out["scaling"] == "strong" and out["config"]["workload"].startswith(workload.upper())
+    assert out["config"]["rows_per_gpu"] == 1 << scale
+    assert out["config"]["nnz_total"] == out["config"]["nnz_per_gpu"]
+    assert out["parity"].startswith("within FAST bound") and "first" in out["cpu_baseline"]["sample"]
+
+
+@pytest.mark.parametrize("workload,scale", [("c4", 11), ("c5", 10)])
+def test_bench_strong_workloads_gloo(workload, scale):
+    res = _multi_rank(["--workload", workload, "--scale", str(scale)])
+    out = res[0]
+    assert res[1] is None and out["n_gpus"] == 2 and out["scaling"] == "strong"
+    assert len(out["rank_kernel_us"]) == 2
+    # the two shards together are the whole matrix
+    if workload == "c4":
+        assert out["config"]["nnz_total"] == 32 << scale and out["config"]["rows_per_gpu"] == 1 << (scale - 1)
+    else:
+        import hipspmv as hs_
+        assert out["config"]["nnz_total"] == hs_.gen_rmat_csr(scale)[1].size
 
 
 def test_bench_multi_rank_gloo():

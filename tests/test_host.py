@@ -2,6 +2,7 @@
 plugin surface, loaders, generators, csr2csc and row partitioning."""
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -113,3 +114,36 @@ def test_product_csr2csc_equals_oracle():
     b = oracle.csr2csc(n, n, rowptr, colind, vals)
     for u, v in zip(a, b):
         assert u.tobytes() == v.tobytes()
+
+
+def test_rmat_row_ranges_concatenate_to_the_whole_matrix():
+    scale = 13
+    rowptr, colind, vals = hs.gen_rmat_csr(scale, 16, 4)
+    counts = hs.gen_rmat_row_counts(scale, 16, 4)
+    assert int(counts.sum(dtype=np.uint64)) == 16 << scale
+    assert np.all(np.diff(rowptr.astype(np.int64)) <= counts)  # duplicates only shrink rows
+    for parts in (1, 3, 8):
+        b = hs.partition_row_counts(counts, parts)
+        assert b[0] == 0 and b[-1] == 1 << scale and np.all(np.diff(b.astype(np.int64)) >= 0)
+        for p in range(parts):
+            r0, r1 = int(b[p]), int(b[p + 1])
+            rp, ci, v = hs.gen_rmat_rows(scale, r0, r1, 16, 4)
+            e0, e1 = int(rowptr[r0]), int(rowptr[r1])
+            assert np.array_equal(rp, rowptr[r0:r1 + 1] - rowptr[r0])
+            assert np.array_equal(ci, colind[e0:e1]) and v.tobytes() == vals[e0:e1].tobytes()
+        if parts == 8:  # nnz balance of the count-based split
+            share = np.diff(rowptr[b.astype(np.int64)].astype(np.int64)) / rowptr[-1]
+            assert share.max() < 1.5 / parts
+
+
+def test_generators_independent_of_thread_count(monkeypatch):
+    import subprocess
+    code = ("import sys; sys.path.insert(0, %r); import hipspmv as hs, hashlib; "
+            "a = hs.gen_rmat_csr(12); b = hs.gen_stripe_csr(5, 3000, 1 << 20); "
+            "print(hashlib.sha256(b''.join(x.tobytes() for x in a + b)).hexdigest())") % hs.PKG_DIR
+    outs = set()
+    for t in ("1", "3", "8"):
+        env = dict(os.environ, SPMV_THREADS=t)
+        outs.add(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                                check=True).stdout)
+    assert len(outs) == 1
