@@ -144,6 +144,28 @@ int hipspmv_prep_stats(const uint32_t *colptr, const uint32_t *rowind, uint32_t 
 int hipspmv_mark_row_starts(const uint32_t *rowind, uint32_t *rowind_out, uint32_t rows, uint32_t nnz, int reverse,
                             int shift, int device, uint64_t *kernel_ns);
 
+/* ---- several devices of one process ---------------------------------------
+ * One matrix row-partitioned over ndev devices (rows cut into contiguous,
+ * nnz-balanced blocks; block i on devices[i]): the single-host-thread
+ * multi-GPU form of SURVEY.md §8(b)/(e), for HIPSpMV (register num_devices)
+ * and C callers.  exec copies x to devices[0], broadcasts it device to device
+ * (RCCL ncclBroadcast over xGMI when the ids are distinct, peer copies when an
+ * id repeats), runs every block on its device and copies each block's y into
+ * its rows of y.  No cross-device reduction: every row equals the
+ * single-device result for the same mode and kernel.  Stat keys:
+ * "num_devices" "rccl" "rows" "cols" "nz" "setup_ns" "h2d_ns" "bcast_ns"
+ * "kernel_ns" (slowest block) "d2h_ns" "execs" "kernel" (block 0's last) "alg_bytes" (x counted once per
+ * device) and "shard<i>_{rows,row0,nz,device,kernel_ns}". */
+typedef struct hipspmv_multi hipspmv_multi_t;
+
+int hipspmv_multi_create(const uint32_t *colptr, const uint32_t *rowind, const void *vals, uint32_t rows,
+                         uint32_t cols, uint32_t nnz, int dtype, const int *devices, int ndev,
+                         hipspmv_multi_t **out);
+int hipspmv_multi_set_option(hipspmv_multi_t *m, const char *key, int64_t value);
+int hipspmv_multi_exec(hipspmv_multi_t *m, const void *x, void *y, int beta, int mode);
+int hipspmv_multi_stat(hipspmv_multi_t *m, const char *key, uint64_t *out);
+int hipspmv_multi_destroy(hipspmv_multi_t *m);
+
 const char *hipspmv_strerror(int status);
 /* Text of the last HIP error seen by this thread (static per-thread buffer). */
 const char *hipspmv_last_error(void);

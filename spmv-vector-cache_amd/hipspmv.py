@@ -101,6 +101,16 @@ def load_hipspmv() -> C.CDLL:
                                        C.POINTER(PrepStats)]
     lib.hipspmv_mark_row_starts.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int,
                                             C.POINTER(C.c_uint64)]
+    ip = C.POINTER(C.c_int)
+    lib.hipspmv_multi_create.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, ip, C.c_int,
+                                         C.POINTER(vp)]
+    lib.hipspmv_multi_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
+    lib.hipspmv_multi_exec.argtypes = [vp, vp, vp, C.c_int, C.c_int]
+    lib.hipspmv_multi_stat.argtypes = [vp, C.c_char_p, C.POINTER(C.c_uint64)]
+    lib.hipspmv_multi_destroy.argtypes = [vp]
+    for name in ("hipspmv_multi_create", "hipspmv_multi_set_option", "hipspmv_multi_exec", "hipspmv_multi_stat",
+                 "hipspmv_multi_destroy"):
+        getattr(lib, name).restype = C.c_int
     for name in ("hipspmv_create", "hipspmv_create_csr", "hipspmv_set_option", "hipspmv_exec",
                  "hipspmv_exec_device", "hipspmv_stat", "hipspmv_destroy", "hipspmv_abi_version",
                  "hipspmv_device_count", "hipspmv_prep_stats", "hipspmv_mark_row_starts"):
@@ -252,6 +262,52 @@ def mark_row_starts(rowind: np.ndarray, rows: int, reverse: bool = False, shift:
     _check(load_hipspmv().hipspmv_mark_row_starts(_ptr(rowind), _ptr(out), rows, rowind.size, int(reverse), shift,
                                                   device, C.byref(ns)), "mark_row_starts")
     return out, int(ns.value)
+
+
+class MultiHandle:
+    """One CSC matrix row-partitioned over several devices of this process
+    (`hipspmv_multi_t`): x broadcast device to device, one block per device."""
+
+    def __init__(self, colptr, rowind, vals, rows: int, cols: int, devices):
+        lib = load_hipspmv()
+        self._keep = [np.ascontiguousarray(colptr, dtype=np.uint32), np.ascontiguousarray(rowind, dtype=np.uint32),
+                      np.ascontiguousarray(vals)]
+        self.dtype = self._keep[2].dtype
+        self.rows, self.cols = rows, cols
+        devs = (C.c_int * len(devices))(*devices)
+        self._h = C.c_void_p()
+        _check(lib.hipspmv_multi_create(_ptr(self._keep[0]), _ptr(self._keep[1]), _ptr(self._keep[2]), rows, cols,
+                                        self._keep[1].size, U64 if self.dtype == np.uint64 else F64, devs,
+                                        len(devices), C.byref(self._h)), "multi_create")
+        self._keep = None
+
+    def set_option(self, key: str, value: int) -> None:
+        _check(load_hipspmv().hipspmv_multi_set_option(self._h, key.encode(), value), f"multi_set_option({key})")
+
+    def set_kernel(self, name: str) -> None:
+        self.set_option("kernel", KERNELS[name])
+
+    def exec(self, x: np.ndarray, y: np.ndarray | None = None, beta: int = 0, mode: int = MODE_ORDERED):
+        x = np.ascontiguousarray(x, dtype=self.dtype)
+        y = np.zeros(self.rows, dtype=self.dtype) if y is None else np.ascontiguousarray(y, dtype=self.dtype)
+        _check(load_hipspmv().hipspmv_multi_exec(self._h, _ptr(x), _ptr(y), beta, mode), "multi_exec")
+        return y
+
+    def stat(self, key: str) -> int:
+        v = C.c_uint64()
+        _check(load_hipspmv().hipspmv_multi_stat(self._h, key.encode(), C.byref(v)), f"multi_stat({key})")
+        return int(v.value)
+
+    def close(self) -> None:
+        if self._h:
+            load_hipspmv().hipspmv_multi_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def device_count() -> int:

@@ -12,7 +12,8 @@ HIPSpMVRegisterFile* HIPSpMV::registerFile(int device) {
   std::lock_guard<std::mutex> lock(mu);
   auto it = files.find(device);
   if (it == files.end())
-    it = files.emplace(device, HIPSpMVRegisterFile{kSignature, device, HIPSPMV_MODE_ORDERED, HIPSPMV_KERNEL_AUTO, 1, 0})
+    it = files.emplace(device, HIPSpMVRegisterFile{kSignature, device, HIPSPMV_MODE_ORDERED, HIPSPMV_KERNEL_AUTO, 1, 0,
+                                                   1, {device}})
              .first;
   return &it->second;
 }
@@ -22,6 +23,7 @@ HIPSpMV::HIPSpMV(uintptr_t aBase, uintptr_t aReset, SparseMatrix* A, SpMVData* x
 
 HIPSpMV::~HIPSpMV() {
   if (m_h) hipspmv_destroy(m_h);
+  if (m_multi) hipspmv_multi_destroy(m_multi);
 }
 
 // setupRegs(): the device copy of A is built once per matrix version (CSC ->
@@ -31,22 +33,36 @@ HIPSpMV::~HIPSpMV() {
 void HIPSpMV::setupRegs() {
   HardwareSpMV::setupRegs();
   if (m_status) return;
-  if (m_h && m_builtVersion == m_A->version()) return;
+  const bool built = multi() ? m_multi != nullptr : m_h != nullptr;
+  if (built && m_builtVersion == m_A->version()) return;
   if (m_h) {
     hipspmv_destroy(m_h);
     m_h = nullptr;
   }
+  if (m_multi) {
+    hipspmv_multi_destroy(m_multi);
+    m_multi = nullptr;
+  }
   const int dtype = m_A->getDataType() == SPMV_U64 ? HIPSPMV_U64 : HIPSPMV_F64;
-  m_status = hipspmv_create(m_A->getIndPtrs(), m_A->getInds(), m_A->getNzData(), m_A->getRows(), m_A->getCols(),
-                            m_A->getNz(), dtype, regs()->device, &m_h);
+  if (multi()) {
+    const int n = regs()->num_devices < 16 ? regs()->num_devices : 16;
+    m_status = hipspmv_multi_create(m_A->getIndPtrs(), m_A->getInds(), m_A->getNzData(), m_A->getRows(),
+                                    m_A->getCols(), m_A->getNz(), dtype, regs()->devices, n, &m_multi);
+  } else {
+    m_status = hipspmv_create(m_A->getIndPtrs(), m_A->getInds(), m_A->getNzData(), m_A->getRows(), m_A->getCols(),
+                              m_A->getNz(), dtype, regs()->device, &m_h);
+  }
   if (m_status) {
-    std::cerr << "HIPSpMV: hipspmv_create failed: " << hipspmv_strerror(m_status) << " (" << hipspmv_last_error()
-              << ")" << std::endl;
+    std::cerr << "HIPSpMV: create failed: " << hipspmv_strerror(m_status) << " (" << hipspmv_last_error() << ")"
+              << std::endl;
     m_h = nullptr;
+    m_multi = nullptr;
     return;
   }
   m_builtVersion = m_A->version();
-  if (regs()->kernel != HIPSPMV_KERNEL_AUTO) m_status = hipspmv_set_option(m_h, "kernel", regs()->kernel);
+  if (regs()->kernel != HIPSPMV_KERNEL_AUTO)
+    m_status = multi() ? hipspmv_multi_set_option(m_multi, "kernel", regs()->kernel)
+                       : hipspmv_set_option(m_h, "kernel", regs()->kernel);
 }
 
 void HIPSpMV::init() {}
@@ -54,8 +70,9 @@ void HIPSpMV::init() {}
 // regular(): x to the device, the kernel, y back -- synchronously, like the
 // reference's busy-wait on doneRegular (HardwareSpMVNewCache.cpp:90-101).
 void HIPSpMV::regular() {
-  if (m_status || !m_h) return;
-  m_status = hipspmv_exec(m_h, m_x, m_y, regs()->beta, regs()->mode);
+  if (m_status || !(m_h || m_multi)) return;
+  m_status = m_multi ? hipspmv_multi_exec(m_multi, m_x, m_y, regs()->beta, regs()->mode)
+                     : hipspmv_exec(m_h, m_x, m_y, regs()->beta, regs()->mode);
   if (m_status)
     std::cerr << "HIPSpMV: exec failed: " << hipspmv_strerror(m_status) << " (" << hipspmv_last_error() << ")"
               << std::endl;
@@ -79,14 +96,23 @@ bool HIPSpMV::exec() {
 
 uint64_t HIPSpMV::statU64(const std::string& key) {
   uint64_t v = 0;
+  if (m_multi) {
+    if (key == "alg_bytes_beta1") {  // y read as well
+      if (hipspmv_multi_stat(m_multi, "alg_bytes", &v) == HIPSPMV_OK) return v + 8ull * m_A->getRows();
+      return 0;
+    }
+    return hipspmv_multi_stat(m_multi, key.c_str(), &v) == HIPSPMV_OK ? v : 0;
+  }
   if (m_h && hipspmv_stat(m_h, key.c_str(), &v) == HIPSPMV_OK) return v;
+  if (key == "num_devices") return 1;
   return 0;
 }
 
 std::vector<std::string> HIPSpMV::statKeys() {
   std::vector<std::string> keys = HardwareSpMV::statKeys();
   for (const char* k : {"kernelTimeUs", "setupTimeUs", "h2dTimeUs", "d2hTimeUs", "algKBytes", "mode", "kernel",
-                        "device", "error", "maxAlive", "maxColSpan", "cmstime", "maxAliveTime", "maxColSpanTime"})
+                        "device", "error", "numDevices", "bcastTimeUs", "maxAlive", "maxColSpan", "cmstime",
+                        "maxAliveTime", "maxColSpanTime"})
     keys.push_back(k);
   return keys;
 }
@@ -116,6 +142,8 @@ unsigned int HIPSpMV::statInt(std::string name) {
   if (name == "kernel") return (unsigned int)statU64("kernel");
   if (name == "device") return (unsigned int)regs()->device;
   if (name == "error") return (unsigned int)m_status;
+  if (name == "numDevices") return (unsigned int)statU64("num_devices");
+  if (name == "bcastTimeUs") return (unsigned int)(statU64("bcast_ns") / 1000);
   if (name == "maxAlive") return prepStats().max_alive;
   if (name == "maxColSpan") return prepStats().max_col_span;
   if (name == "cmstime") return (unsigned int)(prepStats().cms_ns / 1000);

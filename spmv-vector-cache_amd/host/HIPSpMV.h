@@ -14,6 +14,7 @@
 #include "hipspmv.h"
 
 struct hipspmv_handle;
+struct hipspmv_multi;
 
 // The in-memory register block that stands in for the accelerator's AXI-Lite
 // register map: word 0 is the signature HWSpMVFactory dispatches on
@@ -25,6 +26,10 @@ struct HIPSpMVRegisterFile {
   int32_t kernel;  // HIPSPMV_KERNEL_* (AUTO picks by matrix shape)
   int32_t beta;    // 1: y += A*x (reference semantics), 0: y = A*x
   uint32_t reset;  // the reset word resetAccelerator() pulses
+  // > 1: rows partitioned over devices[0..num_devices) of this process
+  // (hipspmv_multi_*; x broadcast device to device).  0 or 1: `device` alone.
+  int32_t num_devices;
+  int32_t devices[16];
 };
 
 class HIPSpMV : public HardwareSpMV {
@@ -58,7 +63,10 @@ class HIPSpMV : public HardwareSpMV {
 
   const hipspmv_prep_stats_t& prepStats();
 
+  bool multi() const { return regs()->num_devices > 1; }
+
   hipspmv_handle* m_h = nullptr;
+  hipspmv_multi* m_multi = nullptr;
   hipspmv_prep_stats_t m_prep{};
   uint64_t m_prepVersion = ~0ull;
   uint64_t m_builtVersion = ~0ull;

@@ -6,8 +6,10 @@
 // (main.cpp:26-37), x = 1 and y = 0 (:210-222), SoftwareSpMV golden
 // (:225-226), optional CMS marking (:228-229), HWSpMVFactory::make, exec,
 // compareGolden, one CSV row of statKeys() + accType + matrix (:49-66).
-// Configurations: "hip" (HIPSpMV on the device of --device) and "sw"
-// (benchmarkSW, :102-144).  Times are microseconds.
+// Configurations: "hip" (HIPSpMV on the device of --device), "hip<N>"
+// (HIPSpMV row-partitioned over N devices of this process, ids wrapping
+// around the visible devices) and "sw" (benchmarkSW, :102-144).  Times are
+// microseconds.
 //
 //   spmvbench [--dir D] [--device N] [--mode ordered|fast] [--kernel K] [--reps N]
 //             [--cms 0|1] [--confs hip,sw] matrix...
@@ -99,6 +101,7 @@ int main(int argc, char** argv) {
     else if (a == "--kernel") {
       const std::string k = next();
       kernel = k == "vcache" ? HIPSPMV_KERNEL_VCACHE
+               : k == "vcache_split" ? HIPSPMV_KERNEL_VCACHE_SPLIT
                : k == "csr_lane" ? HIPSPMV_KERNEL_CSR_LANE
                : k == "csr_vector" ? HIPSPMV_KERNEL_CSR_VECTOR : HIPSPMV_KERNEL_AUTO;
     } else if (a == "--reps") reps = std::atoi(next().c_str());
@@ -138,10 +141,15 @@ int main(int argc, char** argv) {
       benchmarkSW(dir, ms);
       break;
     }
-    if (cf != "hip") {
+    int ndev = 1;
+    if (cf.rfind("hip", 0) != 0 || (cf.size() > 3 && (ndev = std::atoi(cf.c_str() + 3)) < 1) || ndev > 16) {
       std::cout << "unknown configuration " << cf << std::endl;
       continue;
     }
+    int visible = 1;
+    if (hipspmv_device_count(&visible) != HIPSPMV_OK || visible < 1) visible = 1;
+    regs->num_devices = ndev;
+    for (int d = 0; d < ndev; ++d) regs->devices[d] = (device + d) % visible;
     for (const auto& m : ms) {
       SparseMatrix* A = loadSparseMatrix(dir, m);
       if (!A) {

@@ -1,0 +1,73 @@
+"""hipspmv_multi_* (one matrix row-partitioned over several devices of one
+process) vs the oracle and vs the single-device handle.  The GPU box has one
+device, so the blocks share it ([0, 0, 0] takes the peer-copy broadcast
+path); on a multi-GPU host distinct ids take the RCCL path.  No cross-device
+reduction exists, so ORDERED stays bit-exact and any fixed kernel gives
+bit-identical rows to the single-device run."""
+import numpy as np
+import pytest
+
+import fixtures as fx
+import hipspmv as hs
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _devices(n):
+    return [i % hs.device_count() for i in range(n)]
+
+
+@pytest.mark.parametrize("name", ["circuit204", "row64k", "i1k", "circuit204-uint64", "rowvec64-uint64"])
+@pytest.mark.parametrize("ndev", [1, 2, 3])
+@pytest.mark.parametrize("beta", [0, 1])
+def test_multi_ordered_matches_oracle(gpu, name, ndev, beta):
+    rows, cols, colptr, rowind, vals = fx.load(name)
+    u64 = vals.dtype == np.uint64
+    m = hs.MultiHandle(colptr, rowind, vals, rows, cols, _devices(ndev))
+    assert m.stat("num_devices") == ndev
+    assert sum(m.stat(f"shard{i}_rows") for i in range(ndev)) == rows
+    assert sum(m.stat(f"shard{i}_nz") for i in range(ndev)) == rowind.size
+    for xname, x in fx.x_variants(name, cols).items():
+        y0 = (np.random.default_rng(3).integers(0, 2**64, rows, dtype=np.uint64) if u64
+              else np.random.default_rng(3).uniform(-1, 1, rows))
+        want = oracle.spmv_csc(colptr, rowind, vals, x, y=(y0.copy() if beta else None), rows=rows)
+        got = m.exec(x, y0.copy(), beta=beta, mode=hs.MODE_ORDERED)
+        assert got.tobytes() == want.tobytes(), (name, ndev, xname)
+    m.close()
+
+
+@pytest.mark.parametrize("kernel,mode", [("vcache_split", hs.MODE_FAST), ("csr_vector", hs.MODE_FAST),
+                                         ("vcache", hs.MODE_ORDERED)])
+def test_multi_equals_single_device(gpu, kernel, mode):
+    n = 1 << 17
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, 1 << 20, 32)
+    colptr, rowind, cvals = oracle.csr2csc(n, 1 << 20, rowptr, colind, vals)
+    x = hs.gen_vector(1 << 20, 3)
+    one = hs.Handle.from_csc(colptr, rowind, cvals, n, 1 << 20)
+    one.set_kernel(kernel)
+    y1 = one.exec(x, beta=0, mode=mode)
+    one.close()
+    m = hs.MultiHandle(colptr, rowind, cvals, n, 1 << 20, _devices(4))
+    m.set_kernel(kernel)
+    y4 = m.exec(x, beta=0, mode=mode)
+    assert y4.tobytes() == y1.tobytes()
+    assert m.stat("execs") == 1 and m.stat("kernel_ns") > 0
+    assert m.stat("alg_bytes") == 12 * colind.size + 4 * (n + 4) + 4 * 8 * (1 << 20) + 8 * n
+    m.close()
+
+
+def test_multi_more_devices_than_rows(gpu):
+    rows, cols, colptr, rowind, vals = fx.load("i64")
+    m = hs.MultiHandle(colptr, rowind, vals, rows, cols, _devices(5))
+    x = np.arange(1, cols + 1, dtype=np.float64)
+    assert m.exec(x).tobytes() == oracle.spmv_csc(colptr, rowind, vals, x, rows=rows).tobytes()
+    m.close()
+
+
+def test_multi_invalid(gpu):
+    rows, cols, colptr, rowind, vals = fx.load("i64")
+    with pytest.raises(hs.HipSpMVError):
+        hs.MultiHandle(colptr, rowind, vals, rows, cols, [])
+    with pytest.raises(hs.HipSpMVError):
+        hs.MultiHandle(colptr, rowind, vals, rows, cols, [0, 999])

@@ -187,16 +187,21 @@ def test_plugin_surface_spmvbench(gpu):
     # software/main.cpp pipeline through HWSpMVFactory -> HIPSpMV; diffFromGolden == 0
     import subprocess
     names = fx.ALL_FIXTURES
-    out = subprocess.run([f"{hs.LIB_DIR}/spmvbench", "--dir", fx.MATRICES, "--confs", "hip", "--cms", "1", *names],
-                         capture_output=True, text=True)
+    out = subprocess.run([f"{hs.LIB_DIR}/spmvbench", "--dir", fx.MATRICES, "--confs", "hip,hip3", "--cms", "1",
+                          *names], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     lines = out.stdout.splitlines()
     hdr = next(l for l in lines if l.startswith("diffFromGolden,"))
     keys = hdr.rstrip(",").split(",")
     recs = [dict(zip(keys, l.rstrip(",").split(","))) for l in lines if l[:1].isdigit()]
-    assert len(recs) == len(names)
-    for r in recs:
+    assert len(recs) == 2 * len(names)
+    for i, r in enumerate(recs):
         assert r["diffFromGolden"] == "0" and r["accType"] == "HIPSpMV" and r["error"] == "0", r
+        assert r["numDevices"] == ("1" if i < len(names) else "3"), r
+        # the GPU preprocessing statistics (SoftwareSpMV.cpp:72-95 keys), masked CMS marks
+        rows, cols, colptr, rowind, _ = fx.load(r["matrix"])
+        assert int(r["maxAlive"]) == oracle.max_alive(rowind, rows), r
+        assert int(r["maxColSpan"]) == oracle.max_col_span(colptr, rowind), r
 
 
 def test_c3_split_deterministic_and_within_bound(gpu):
