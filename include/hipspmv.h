@@ -107,6 +107,9 @@ int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void 
  * "device" "kernel" (last kernel run) "setup_ns" "kernel_ns" (last timed
  * exec) "h2d_ns" "d2h_ns" "alg_bytes" (beta 0) "alg_bytes_beta1" "flops"
  * "device_bytes" "vcache_blocks" "vcache_panels" "vcache_rows_per_block"
+ * "vcache_max_segment" "vcache_eligible" "vcache_split_eligible"
+ * "vcache_split_units" "vcache_split_rows_per_block" "vcache_x_bytes"
+ * "vcache_split_x_bytes" (x bytes one launch streams into LDS) "row_groups"
  * "max_row_len" "empty_rows" "execs". */
 int hipspmv_stat(hipspmv_t *h, const char *key, uint64_t *out);
 

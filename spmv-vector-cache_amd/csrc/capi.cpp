@@ -379,6 +379,10 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "vcache_split_eligible") *out = h->vc[1].ok;
   else if (k == "vcache_split_units") *out = (uint64_t)h->vc[1].nblocks * h->vc[1].split;
   else if (k == "vcache_split_rows_per_block") *out = h->vc[1].rows_per_block;
+  // x bytes a launch streams from L2/MALL into LDS: every row block reads all
+  // columns once (split: its two halves read one half each)
+  else if (k == "vcache_x_bytes") *out = h->vc[0].ok ? 8ull * h->vc[0].nblocks * h->cols : 0;
+  else if (k == "vcache_split_x_bytes") *out = h->vc[1].ok ? 8ull * h->vc[1].nblocks * h->cols : 0;
   else if (k == "row_groups") *out = h->ngroups;
   else if (k == "max_row_len") *out = h->max_row_len;
   else if (k == "empty_rows") *out = h->empty_rows;

@@ -213,6 +213,8 @@ def test_c3_split_deterministic_and_within_bound(gpu):
     h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
     assert h.stat("vcache_split_eligible") == 1
     assert h.kernel_name(hs.MODE_FAST) == "vcache_split"
+    # x streamed into LDS per launch: 256 ordered units x 8 MB, 128 split row blocks x 8 MB
+    assert h.stat("vcache_x_bytes") == 256 * 8 * n and h.stat("vcache_split_x_bytes") == 128 * 8 * n
     ys = [h.exec(x, beta=0, mode=hs.MODE_FAST) for _ in range(3)]
     assert ys[0].tobytes() == ys[1].tobytes() == ys[2].tobytes()
     colptr, rowind, cvals = oracle.csr2csc(n, n, rowptr, colind, vals)
