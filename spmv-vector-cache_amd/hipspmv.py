@@ -150,7 +150,13 @@ def load_host() -> C.CDLL:
     lib.spmvhost_partition_rows.restype = None
     lib.spmvhost_load_matrix.argtypes = [C.c_char_p, C.c_char_p, _u32p, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.spmvhost_load_matrix.restype = C.c_int
-    lib.spmvhost_convert_mtx.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]
+    lib.spmvhost_convert_mtx.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int]
+    lib.spmvhost_row_len_histogram.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, _u32p, _u32p, _u32p, _u32p,
+                                               C.c_uint32]
+    lib.spmvhost_row_len_histogram.restype = C.c_uint32
+    lib.spmvhost_permute_longest_row_first.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, _u32p, _u32p, _u64p,
+                                                       _u32p, _u32p, _u32p, _u64p]
+    lib.spmvhost_permute_longest_row_first.restype = None
     lib.spmvhost_convert_mtx.restype = C.c_int
     _host = lib
     return lib
@@ -403,8 +409,32 @@ def load_matrix(directory: str, name: str):
     return rows, cols, colptr, rowind, (vals if is_u64 else vals.view(np.float64))
 
 
-def convert_mtx(mtx_path: str, outdir: str, name: str, golden: bool = True) -> None:
-    """Matrix Market -> reference .bin layout (+ golden.bin) via libspmvhost."""
+def convert_mtx(mtx_path: str, outdir: str, name: str, golden: bool = True, permute: bool = False) -> None:
+    """Matrix Market -> reference .bin layout (+ golden.bin) via libspmvhost;
+    permute: rows longest first (matrixutils.py:149-158) before writing."""
     os.makedirs(os.path.join(outdir, name), exist_ok=True)
-    _check(load_host().spmvhost_convert_mtx(mtx_path.encode(), outdir.encode(), name.encode(), int(golden)),
-           f"convert {mtx_path}")
+    _check(load_host().spmvhost_convert_mtx(mtx_path.encode(), outdir.encode(), name.encode(), int(golden),
+                                            int(permute)), f"convert {mtx_path}")
+
+
+def row_len_histogram(colptr, rowind, rows: int) -> dict:
+    """generateRowLenHistogram (matrixutils.py:116-126) via libspmvhost."""
+    colptr = np.ascontiguousarray(colptr, dtype=np.uint32)
+    rowind = np.ascontiguousarray(rowind, dtype=np.uint32)
+    cap = rows + 1
+    lens, counts = np.empty(cap, np.uint32), np.empty(cap, np.uint32)
+    n = load_host().spmvhost_row_len_histogram(rows, colptr.size - 1, rowind.size, colptr, rowind, lens, counts, cap)
+    return {int(k): int(v) for k, v in zip(lens[:n], counts[:n])}
+
+
+def permute_longest_row_first(colptr, rowind, vals, rows: int):
+    """permuteLongestRowFirst (matrixutils.py:140-158): (perm, colptr, rowind, vals)."""
+    colptr = np.ascontiguousarray(colptr, dtype=np.uint32)
+    rowind = np.ascontiguousarray(rowind, dtype=np.uint32)
+    vals = np.ascontiguousarray(vals)
+    cols, nz = colptr.size - 1, rowind.size
+    perm = np.empty(rows, np.uint32)
+    cp, ri, v = np.empty(cols + 1, np.uint32), np.empty(nz, np.uint32), np.empty(nz, np.uint64)
+    load_host().spmvhost_permute_longest_row_first(rows, cols, nz, colptr, rowind, vals.view(np.uint64), perm, cp,
+                                                   ri, v)
+    return perm, cp, ri, v.view(vals.dtype)

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "MatrixIO.h"
+#include "MatrixOps.h"
 #include "Synthetic.h"
 #include "csr2csc.h"
 
@@ -92,11 +93,55 @@ int spmvhost_load_matrix(const char* dir, const char* name, uint32_t* dims /*row
   return 0;
 }
 
+// Row-length histogram (matrixutils.py:116-126, MatrixOps.h): writes up to
+// cap (length, count) pairs in ascending length; returns the number of pairs.
+uint32_t spmvhost_row_len_histogram(uint32_t rows, uint32_t cols, uint32_t nz, const uint32_t* colptr,
+                                    const uint32_t* rowind, uint32_t* lens, uint32_t* counts, uint32_t cap) {
+  SparseMatrix* A = SparseMatrix::fromArrays(rows, cols, nz, const_cast<uint32_t*>(colptr),
+                                             const_cast<uint32_t*>(rowind), nullptr);
+  const auto h = rowLenHistogram(A);
+  delete A;
+  uint32_t i = 0;
+  for (const auto& kv : h) {
+    if (i < cap) {
+      lens[i] = kv.first;
+      counts[i] = kv.second;
+    }
+    ++i;
+  }
+  return i;
+}
+
+// permuteLongestRowFirst (matrixutils.py:140-158) on CSC arrays: perm[rows]
+// and the permuted CSC (colptr[cols+1], rowind[nz], vals[nz] 8-byte words).
+void spmvhost_permute_longest_row_first(uint32_t rows, uint32_t cols, uint32_t nz, const uint32_t* colptr,
+                                        const uint32_t* rowind, const uint64_t* vals, uint32_t* perm,
+                                        uint32_t* colptr_out, uint32_t* rowind_out, uint64_t* vals_out) {
+  SparseMatrix* A = SparseMatrix::fromArrays(rows, cols, nz, const_cast<uint32_t*>(colptr),
+                                             const_cast<uint32_t*>(rowind),
+                                             reinterpret_cast<SpMVData*>(const_cast<uint64_t*>(vals)));
+  const std::vector<uint32_t> p = longestRowFirstPermutation(A);
+  SparseMatrix* B = permuteRows(A, p);
+  std::memcpy(perm, p.data(), 4ull * rows);
+  std::memcpy(colptr_out, B->getIndPtrs(), 4ull * (cols + 1));
+  std::memcpy(rowind_out, B->getInds(), 4ull * nz);
+  std::memcpy(vals_out, B->getNzData(), 8ull * nz);
+  delete B;
+  delete A;
+}
+
 // Matrix Market -> reference .bin files (+ golden.bin) under <outdir>/<name>/,
-// the job of matrices/matrixutils.py:187-260 and :108-113.  Returns 0 on success.
-int spmvhost_convert_mtx(const char* mtx_path, const char* outdir, const char* name, int write_golden) {
+// the job of matrices/matrixutils.py:187-260 and :108-113; with permute, rows
+// are reordered longest first before writing (:149-158).  Returns 0 on success.
+int spmvhost_convert_mtx(const char* mtx_path, const char* outdir, const char* name, int write_golden,
+                         int permute) {
   SparseMatrix* A = loadMatrixMarket(mtx_path);
   if (!A) return 1;
+  if (permute) {
+    SparseMatrix* B = permuteLongestRowFirst(A);
+    delete A;
+    A = B;
+  }
   bool ok = writeSparseMatrix(A, outdir, name);
   if (ok && write_golden) ok = writeGolden(A, std::string(outdir) + "/" + name + "/golden.bin");
   delete A;

@@ -147,3 +147,66 @@ def test_generators_independent_of_thread_count(monkeypatch):
         outs.add(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                                 check=True).stdout)
     assert len(outs) == 1
+
+
+def _scipy_csc(name):
+    import scipy.sparse as sp
+    rows, cols, colptr, rowind, vals = fx.load(name)
+    return sp.csc_matrix((vals, rowind, colptr), shape=(rows, cols)), (rows, cols, colptr, rowind, vals)
+
+
+def _ref_row_len_histogram(matrix):
+    # matrices/matrixutils.py:116-126 restated (Python 3): note the loop bound
+    csr = matrix.tocsr()
+    h = {}
+    for j in range(1, csr.shape[1]):
+        n = int(csr.indptr[j] - csr.indptr[j - 1])
+        h[n] = h.get(n, 0) + 1
+    return h
+
+
+def _ref_permute_longest_row_first(matrix):
+    # matrices/matrixutils.py:140-158 restated (Python 3, scipy as the reference)
+    import scipy.sparse as sp
+    csr = matrix.tocsr()
+    csr.sort_indices()
+    lens = sorted(zip([int(csr.indptr[i + 1] - csr.indptr[i]) for i in range(csr.shape[0])],
+                      range(csr.shape[0])), reverse=True)
+    perm = [x[1] for x in lens]
+    P = sp.coo_matrix(([1 for _ in perm], (range(len(perm)), perm)))
+    return perm, (P * csr).tocsc()
+
+
+@pytest.mark.parametrize("name", ["circuit204", "i1k", "row64k", "dia64-uint64", "rowvec64-uint64"])
+def test_row_len_histogram_matches_matrixutils(name):
+    A, (rows, cols, colptr, rowind, vals) = _scipy_csc(name)
+    assert hs.row_len_histogram(colptr, rowind, rows) == _ref_row_len_histogram(A)
+
+
+@pytest.mark.parametrize("name", ["circuit204", "i64", "rowvec64-uint64", "dia64-uint64"])
+def test_permute_longest_row_first_matches_matrixutils(name):
+    A, (rows, cols, colptr, rowind, vals) = _scipy_csc(name)
+    perm, cp, ri, v = hs.permute_longest_row_first(colptr, rowind, vals, rows)
+    ref_perm, B = _ref_permute_longest_row_first(A.astype(np.float64))
+    assert perm.tolist() == ref_perm
+    B.sort_indices()
+    assert np.array_equal(cp, B.indptr) and np.array_equal(ri, B.indices)
+    if vals.dtype == np.float64:
+        assert v.tobytes() == B.data.astype(np.float64).tobytes()
+    else:
+        assert np.array_equal(v, B.data.astype(np.uint64))
+
+
+def test_convert_mtx_permuted(tmp_path):
+    import scipy.io as sio
+    mtx = os.path.join(fx.MATRICES, "mtx", "circuit204.mtx")
+    hs.convert_mtx(mtx, str(tmp_path), "c204p", golden=True, permute=True)
+    rows, cols, colptr, rowind, vals = hs.load_matrix(str(tmp_path), "c204p")
+    _, B = _ref_permute_longest_row_first(sio.mmread(mtx).tocsc())
+    B.sort_indices()
+    assert np.array_equal(colptr, B.indptr) and np.array_equal(rowind, B.indices)
+    assert vals.tobytes() == B.data.tobytes()
+    # golden of the permuted matrix = the reference golden permuted
+    g = np.fromfile(os.path.join(str(tmp_path), "c204p", "golden.bin"), dtype=np.float64)
+    perm, *_ = hs.permute_longest_row_first(*fx.load("circuit204")[2:5], 1020)
+    assert g.tobytes() == fx.golden("circuit204")[perm].tobytes()
