@@ -66,6 +66,10 @@ extern "C" {
 #define HIPSPMV_KERNEL_CSR_VECTOR 3 /* wave segmented DPP reduction over CSR; fast */
 #define HIPSPMV_KERNEL_VCACHE_SPLIT 4 /* vcache over two column halves, fixed-order
                                          combine p0 + p1; fast, deterministic */
+#define HIPSPMV_KERNEL_VCACHE_SPLIT4 5 /* four column parts, p0+p1+p2+p3; fast,
+                                          deterministic; experimental: never
+                                          chosen by AUTO, layout built only
+                                          when HIPSPMV_EXPERIMENTAL=1 at create */
 
 typedef struct hipspmv_handle hipspmv_t;
 
@@ -86,7 +90,8 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
                        uint32_t cols, uint32_t nnz, int dtype, int device, hipspmv_t **out);
 
 /* Options: "kernel" (HIPSPMV_KERNEL_*), "mode" (default mode for exec with
- * HIPSPMV_MODE_AUTO), "timing" (1 = record per-exec kernel events). */
+ * HIPSPMV_MODE_AUTO), "timing" (1 = record per-exec kernel events),
+ * "vcache_dma" (1 = vcache kernels stage x by LDS-DMA; experimental). */
 int hipspmv_set_option(hipspmv_t *h, const char *key, int64_t value);
 
 /* Replaces HardwareSpMV::exec()'s reset -> init -> regular -> write sequence
@@ -109,7 +114,8 @@ int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void 
  * "device_bytes" "vcache_blocks" "vcache_panels" "vcache_rows_per_block"
  * "vcache_max_segment" "vcache_eligible" "vcache_split_eligible"
  * "vcache_split_units" "vcache_split_rows_per_block" "vcache_x_bytes"
- * "vcache_split_x_bytes" (x bytes one launch streams into LDS) "row_groups"
+ * "vcache_split_x_bytes" (x bytes one launch streams into LDS)
+ * "vcache_split4_eligible" "vcache_split4_x_bytes" "row_groups"
  * "max_row_len" "empty_rows" "execs". */
 int hipspmv_stat(hipspmv_t *h, const char *key, uint64_t *out);
 

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -77,7 +78,8 @@ struct hipspmv_handle {
     uint64_t *d_vals = nullptr, *d_partial = nullptr;
     uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, part_panels = 0, npad = 0, max_seg = 0;
     int split = 1;
-  } vc[2];  // [0] ordered (kVcOrdered), [1] split (kVcSplit)
+  } vc[3];  // [0] ordered (kVcOrdered), [1] split (kVcSplit), [2] split4 (kVcSplit4, experimental)
+  int vcache_dma = 0;  // option "vcache_dma": LDS-DMA x loader (experimental)
   void *d_x = nullptr, *d_y = nullptr;
   int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
   uint64_t setup_ns = 0, kernel_ns = 0, h2d_ns = 0, d2h_ns = 0, execs = 0, device_bytes = 0;
@@ -121,8 +123,12 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   build_row_groups(a, groups);
   h->ngroups = (uint32_t)groups.size() - 1;
   if ((st = dev_upload(&h->d_groups, groups.data(), groups.size(), h->device_bytes))) return st;
-  const VcGeom geoms[2] = {kVcOrdered, kVcSplit};
-  for (int k = 0; k < 2; ++k) {
+  const VcGeom geoms[3] = {kVcOrdered, kVcSplit, kVcSplit4};
+  // the experimental four-part layout is built only on request
+  // (HIPSPMV_EXPERIMENTAL=1): it costs another copy of the entries
+  const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
+  const int nlayouts = exp && std::strcmp(exp, "1") == 0 ? 3 : 2;
+  for (int k = 0; k < nlayouts; ++k) {
     auto& v = h->vc[k];
     v.ok = vcache_eligible(a, geoms[k]);
     if (!v.ok) continue;
@@ -197,6 +203,9 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
     case HIPSPMV_KERNEL_VCACHE_SPLIT:
       if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
       return h->vc[1].ok ? HIPSPMV_KERNEL_VCACHE_SPLIT : -HIPSPMV_ERR_UNSUPPORTED;
+    case HIPSPMV_KERNEL_VCACHE_SPLIT4:
+      if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
+      return h->vc[2].ok ? HIPSPMV_KERNEL_VCACHE_SPLIT4 : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_LANE:
       return HIPSPMV_KERNEL_CSR_LANE;
     case HIPSPMV_KERNEL_CSR_VECTOR:
@@ -219,11 +228,14 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
 static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in, void* d_y_out, int beta,
                   hipStream_t s) {
   hipError_t e = hipSuccess;
-  if (kernel == HIPSPMV_KERNEL_VCACHE || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT) {
-    const auto& v = h->vc[kernel == HIPSPMV_KERNEL_VCACHE ? 0 : 1];
+  if (kernel == HIPSPMV_KERNEL_VCACHE || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ||
+      kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
+    const int k = kernel == HIPSPMV_KERNEL_VCACHE ? 0 : kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1 : 2;
+    const auto& v = h->vc[k];
+    const VcGeom geoms[3] = {kVcOrdered, kVcSplit, kVcSplit4};
     VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    v.d_partial,
                  v.d_tickets, h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
-                 v.npad,      h->nnz - 1, v.split,   beta};
+                 v.npad,      h->nnz - 1, v.split,   beta, h->vcache_dma, (uint32_t)geoms[k].panel};
     e = launch_vcache(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
@@ -280,8 +292,10 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   if (!h || !key) return HIPSPMV_ERR_INVALID_ARG;
   const std::string k(key);
   if (k == "kernel") {
-    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_VCACHE_SPLIT) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_VCACHE_SPLIT4) return HIPSPMV_ERR_INVALID_ARG;
     h->kernel_opt = (int)value;
+  } else if (k == "vcache_dma") {
+    h->vcache_dma = value ? 1 : 0;
   } else if (k == "mode") {
     if (value != HIPSPMV_MODE_ORDERED && value != HIPSPMV_MODE_FAST) return HIPSPMV_ERR_INVALID_ARG;
     h->mode_opt = (int)value;
@@ -383,6 +397,8 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   // columns once (split: its two halves read one half each)
   else if (k == "vcache_x_bytes") *out = h->vc[0].ok ? 8ull * h->vc[0].nblocks * h->cols : 0;
   else if (k == "vcache_split_x_bytes") *out = h->vc[1].ok ? 8ull * h->vc[1].nblocks * h->cols : 0;
+  else if (k == "vcache_split4_eligible") *out = h->vc[2].ok;
+  else if (k == "vcache_split4_x_bytes") *out = h->vc[2].ok ? 8ull * h->vc[2].nblocks * h->cols : 0;
   else if (k == "row_groups") *out = h->ngroups;
   else if (k == "max_row_len") *out = h->max_row_len;
   else if (k == "empty_rows") *out = h->empty_rows;
@@ -396,6 +412,7 @@ const char* hipspmv_kernel_name(hipspmv_t* h, int mode) {
   switch (choose_kernel(h, mode)) {
     case HIPSPMV_KERNEL_VCACHE: return "vcache";
     case HIPSPMV_KERNEL_VCACHE_SPLIT: return "vcache_split";
+    case HIPSPMV_KERNEL_VCACHE_SPLIT4: return "vcache_split4";
     case HIPSPMV_KERNEL_CSR_LANE: return "csr_lane";
     case HIPSPMV_KERNEL_CSR_VECTOR: return "csr_vector";
     default: return "unsupported";

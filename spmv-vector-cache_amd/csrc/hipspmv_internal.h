@@ -24,6 +24,8 @@ struct VcGeom {
 };
 constexpr VcGeom kVcOrdered{4096, 8128, 1};
 constexpr VcGeom kVcSplit{8192, 6080, 2};
+//   split4 : 16384 rows, 4 parts: 131072 + 2*1984*8 + 1024 (experimental)
+constexpr VcGeom kVcSplit4{16384, 1984, 4};
 constexpr int kVcThreads = 1024;
 constexpr int kVcSegMax = 256;        // npad + 1 <= kVcSegMax per unit
 constexpr int kVcEpt = 2;             // entries per thread held in registers per panel

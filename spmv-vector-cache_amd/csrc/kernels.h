@@ -18,6 +18,8 @@ struct VcacheArgs {
   uint32_t* tickets;   // split == 2: [nblocks] arrival counters, zero between launches
   uint32_t rows, cols, rows_per_block, nblocks, npanels, part_panels, npad, last;
   int split, beta;
+  int dma = 0;        // x panels by LDS-DMA (experimental loader, option "vcache_dma")
+  uint32_t panel = 0; // the layout's panel width: checked against the kernel's
 };
 
 struct CsrArgs {

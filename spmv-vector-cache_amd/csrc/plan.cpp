@@ -93,6 +93,7 @@ bool vcache_eligible(const HostCSR& a, const VcGeom& g) {
   const uint32_t np = (a.cols + g.panel - 1) / g.panel;
   if (np < (uint32_t)g.split) return false;  // every column part needs >= 1 panel
   const uint32_t part = (np + g.split - 1) / g.split;
+  if ((uint64_t)(g.split - 1) * part >= np) return false;  // every part must own >= 1 panel
   const uint32_t npad = part;  // the kernel clamps prefetches past its last panel
   if (npad + 1 > (uint32_t)kVcSegMax) return false;
   // panel order must equal each row's summation order: columns non-decreasing

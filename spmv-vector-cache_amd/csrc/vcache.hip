@@ -9,16 +9,19 @@
 //
 // Work unit = (row block b, column part h).  SPLIT == 1 (ordered geometry):
 // one part, every row's products are added in ascending column order, starting
-// from y_in or +0.0 -- bit-identical to SoftwareSpMV.  SPLIT == 2: two column
-// halves per block (halving the x bytes each CU streams, the measured limit),
-// combined in fixed order y = p0 + p1 by whichever workgroup finishes second:
-// deterministic, FAST-mode tolerance.
+// from y_in or +0.0 -- bit-identical to SoftwareSpMV.  SPLIT == 2 (4): two
+// (four) column parts per block (halving (quartering) the x bytes each CU
+// streams, the measured limit), combined in fixed order y = p0 + p1 (+ p2 +
+// p3) by whichever workgroup of the block finishes last: deterministic,
+// FAST-mode tolerance.
 //
 // Waves are specialised (producer/consumer): waves [0, WL) stream x panels
-// into LDS (register-staged, two panels ahead); waves [WL, 16) stream the
-// unit's entries (DE panels ahead) and apply them.  Each role waits only on
-// its own vmcnt, so the L2-served x stream and the HBM-served entry stream
-// overlap; one workgroup barrier per panel hands the next x panel over.
+// into LDS (LD == 0: register-staged, two panels ahead; LD == 1: LDS-DMA,
+// global_load_lds_dwordx4 straight into the next slot, one panel ahead);
+// waves [WL, 16) stream the unit's entries (DE panels ahead) and apply them.
+// Each role waits only on its own vmcnt, so the L2-served x stream and the
+// HBM-served entry stream overlap; one workgroup barrier per panel hands the
+// next x panel over.
 #include <hip/hip_runtime.h>
 
 #include "device_common.h"
@@ -38,13 +41,17 @@ template <>
 struct VcCfg<2> {  // 8192 rows; x panel 47.5 KiB; 6 loader waves (8 pairs/lane), 10 compute waves
   static constexpr int VR = kVcSplit.rows, VP = kVcSplit.panel, WL = 6, DE = 4, EPT = 3;
 };
+template <>
+struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane), 14 compute waves
+  static constexpr int VR = kVcSplit4.rows, VP = kVcSplit4.panel, WL = 2, DE = 4, EPT = 2;
+};
 
 // AB: ablation mask for the diagnostic build (tools/vc_ablate.hip); the
 // product instantiates AB = 0 and every hook folds away.  Bits: 1 no x loads,
 // 2 no x LDS stores, 4 no entry loads, 8 no compute, 16 x always from panel 0,
 // 32 no per-panel barrier (wrong results, timing only).
 template <typename T, int SPLIT, int WL = VcCfg<SPLIT>::WL, int DE = VcCfg<SPLIT>::DE, int EPT = VcCfg<SPLIT>::EPT,
-          int AB = 0, int MAP = 0, bool NT = false>
+          int AB = 0, int MAP = 0, bool NT = false, int LD = 0>
 __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restrict__ seg,
                                                         const uint32_t* __restrict__ ecode,
                                                         const T* __restrict__ evals, const T* __restrict__ x,
@@ -61,6 +68,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   constexpr int NJ = (PAIRS + LT - 1) / LT;  // pairs per loader lane per panel
   static_assert(VR * 8 + 2 * VP * 8 + kVcSegMax * 4 <= 163840, "LDS budget");
   static_assert(WL > 0 && WC > 0, "both roles need waves");
+  static_assert(SPLIT == 1 || SPLIT == 2 || SPLIT == 4, "column parts");
   __shared__ T ylds[VR];
   __shared__ T xb[2][VP];
   __shared__ uint32_t segl[kVcSegMax];
@@ -74,8 +82,8 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     const uint32_t grp = blockIdx.x % 8;
     h = grp / 4;
     b = (blockIdx.x / 8) * 4 + grp % 4;
-  } else if (SPLIT == 2) {  // unit i -> (b, h): the parts of a block are 8 dispatch slots apart
-    const uint32_t g = blockIdx.x / 16, rem = blockIdx.x % 16;
+  } else if (SPLIT > 1) {  // unit i -> (b, h): the parts of a block are 8 dispatch slots apart
+    const uint32_t g = blockIdx.x / (8 * SPLIT), rem = blockIdx.x % (8 * SPLIT);
     const uint32_t nbg = min(8u, nblocks - g * 8);
     h = rem / nbg;
     b = g * 8 + rem % nbg;
@@ -99,6 +107,31 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
       r[j] = *reinterpret_cast<const u64x2*>(x + min(base + 2 * (t + j * LT), cmax));
+  };
+  // LD == 1: the loader lanes' 16-byte chunks go straight into LDS.  A
+  // wave-instruction writes 64 consecutive chunks (wave-uniform base + lane *
+  // 16 B); chunk c of a panel is issued by wave (c / 64) % WL in its
+  // instruction c / (64 * WL), lanes past the panel's end masked off.
+  constexpr int NDMA = (PAIRS + LT - 1) / LT;
+  const uint32_t wl = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+  auto dma_x = [&](uint32_t s) {
+    if (AB & 1) return;
+    const uint32_t base = (AB & 16) ? 0 : (p0 + min(s, npu - 1)) * VP;
+    T* slot = xb[s & 1];
+#pragma unroll
+    for (int j = 0; j < NDMA; ++j) {
+      const uint32_t c0 = (j * WL + wl) * 64;  // first chunk of this wave-instruction
+      if (c0 + lane < PAIRS)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(x + min(base + 2 * (c0 + lane), cmax)),
+            (__attribute__((address_space(3))) void*)(slot + 2 * c0), 16, 0, 0);
+    }
+  };
+  auto patch_x = [&](uint32_t s) {  // odd cols: the last element, after this wave's DMA landed
+    if ((cols & 1) && p0 + s == npanels - 1) {
+      const uint32_t sl = cols - 1 - (p0 + s) * VP, c = sl >> 1;
+      if (c < PAIRS && ((c / 64) % WL) == wl && (c & 63) == lane) xb[s & 1][sl] = xlast;
+    }
   };
   auto store_x = [&](uint32_t s, const u64x2* r) {
     if (AB & 2) return;
@@ -172,7 +205,20 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
   __syncthreads();  // segl visible
-  if (loader) {
+  if (loader && LD == 1) {
+    // panel s+1 is fetched into slot (s+1)&1 during step s; the slot was last
+    // read in step s-1, which the previous barrier closed
+    dma_x(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    patch_x(0);
+    barrier();
+    for (uint32_t s = 0; s < npu; ++s) {
+      if (s + 1 < npu) dma_x(s + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (s + 1 < npu) patch_x(s + 1);
+      barrier();
+    }
+  } else if (loader) {
     u64x2 R[2][NJ];  // R[(s+1)&1] holds x(s+1) during step s
     load_x(0, R[0]);
     store_x(0, R[0]);
@@ -210,11 +256,12 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
     return;
   }
-  // ---- combine the two column parts, fixed order p0 + p1.  Hand-off per
-  // MI355X_MICROARCH.md (Valid forms, table row 1): every partial byte stored
-  // write-through (sc1: agent-scope relaxed atomic store), each storing wave
-  // drains vmcnt, one lane adds to the block's counter after the barrier; the
-  // workgroup whose add returned 1 reads the other partial with sc1 loads.
+  // ---- combine the column parts, fixed order p0 + p1 (+ p2 + p3).  Hand-off
+  // per MI355X_MICROARCH.md (Valid forms, table row 1): every partial byte
+  // stored write-through (sc1: agent-scope relaxed atomic store), each storing
+  // wave drains vmcnt, one lane adds to the block's counter after the barrier;
+  // the workgroup whose add returned SPLIT-1 reads the other partials with sc1
+  // loads and adds all parts in part order, its own from LDS.
   uint64_t* mine = reinterpret_cast<uint64_t*>(partial) + (size_t)h * rows;
   for (uint32_t i = t; i < nr; i += VT)
     __hip_atomic_store(mine + r0 + i, __builtin_bit_cast(uint64_t, ylds[i]), __ATOMIC_RELAXED,
@@ -223,11 +270,12 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   __syncthreads();
   if (t == 0) {
     const uint32_t old = __hip_atomic_fetch_add(tickets + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == 1) __hip_atomic_store(tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    if (old == (uint32_t)SPLIT - 1)
+      __hip_atomic_store(tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
     segl[0] = old;
   }
   __syncthreads();
-  if (segl[0] == 1) {
+  if (SPLIT == 2 && segl[0] == 1) {  // (the round-1 validated form of the two-part case)
     const uint64_t* other = reinterpret_cast<const uint64_t*>(partial) + (size_t)(1 - h) * rows;
     for (uint32_t i = t; i < nr; i += VT) {
       const T o = __builtin_bit_cast(
@@ -235,20 +283,47 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       const T m = ylds[i];
       y_out[r0 + i] = h == 0 ? m + o : o + m;
     }
+  } else if (SPLIT > 2 && segl[0] == (uint32_t)SPLIT - 1) {
+    const uint64_t* parts = reinterpret_cast<const uint64_t*>(partial);
+    for (uint32_t i = t; i < nr; i += VT) {
+      T acc = T(0);
+#pragma unroll
+      for (int q = 0; q < SPLIT; ++q) {
+        const T v = (uint32_t)q == h ? ylds[i]
+                                     : __builtin_bit_cast(T, __hip_atomic_load(parts + (size_t)q * rows + r0 + i,
+                                                                                __ATOMIC_RELAXED,
+                                                                                __HIP_MEMORY_SCOPE_AGENT));
+        acc = q == 0 ? v : acc + v;
+      }
+      y_out[r0 + i] = acc;
+    }
   }
+}
+
+template <typename T, int SPLIT, int LD>
+static void launch_one(const VcacheArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((k_vcache<T, SPLIT, VcCfg<SPLIT>::WL, VcCfg<SPLIT>::DE, VcCfg<SPLIT>::EPT, 0, 0, false, LD>),
+                     dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s, a.seg, a.code, (const T*)a.vals,
+                     (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets, a.rows, a.cols,
+                     a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta);
 }
 
 template <typename T>
 hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
-  const uint32_t units = a.nblocks * a.split;
+  // the layout's geometry must be the one the kernel is compiled for
+  const VcGeom g = a.split == 1 ? kVcOrdered : a.split == 2 ? kVcSplit : kVcSplit4;
+  if ((a.split != 1 && a.split != 2 && a.split != 4) || a.panel != (uint32_t)g.panel ||
+      a.rows_per_block > (uint32_t)g.rows ||
+      (uint64_t)a.nblocks * a.rows_per_block < a.rows || a.part_panels * (uint64_t)a.split < a.npanels ||
+      (uint64_t)a.part_panels * (a.split - 1) >= a.npanels ||
+      (uint64_t)a.npanels * g.panel < a.cols || a.npad + 1 > (uint32_t)kVcSegMax)
+    return hipErrorInvalidValue;
   if (a.split == 1)
-    hipLaunchKernelGGL((k_vcache<T, 1>), dim3(units), dim3(kVcThreads), 0, s, a.seg, a.code, (const T*)a.vals,
-                       (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets, a.rows, a.cols,
-                       a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta);
+    a.dma ? launch_one<T, 1, 1>(a, s) : launch_one<T, 1, 0>(a, s);
+  else if (a.split == 2)
+    a.dma ? launch_one<T, 2, 1>(a, s) : launch_one<T, 2, 0>(a, s);
   else
-    hipLaunchKernelGGL((k_vcache<T, 2>), dim3(units), dim3(kVcThreads), 0, s, a.seg, a.code, (const T*)a.vals,
-                       (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets, a.rows, a.cols,
-                       a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta);
+    a.dma ? launch_one<T, 4, 1>(a, s) : launch_one<T, 4, 0>(a, s);
   return hipGetLastError();
 }
 

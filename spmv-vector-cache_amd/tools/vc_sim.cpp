@@ -56,6 +56,7 @@ struct Buf {  // bounds-checked global array
 // kernel configuration mirrored from vcache.hip VcCfg<SPLIT>
 struct Cfg {
   int VR, VP, WL, DE, EPT, SPLIT;
+  int LD = 0;  // 0: register-staged x loader, 1: LDS-DMA loader
 };
 
 static double madd(double acc, double a, double b) {
@@ -82,8 +83,8 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
   std::vector<uint32_t> b_of(units), h_of(units);
   for (uint32_t bid = 0; bid < units; ++bid) {
     uint32_t b = bid, h = 0;
-    if (c.SPLIT == 2) {
-      const uint32_t g = bid / 16, rem = bid % 16;
+    if (c.SPLIT > 1) {
+      const uint32_t g = bid / (8 * c.SPLIT), rem = bid % (8 * c.SPLIT);
       const uint32_t nbg = std::min(8u, nblocks - g * 8);
       h = rem / nbg;
       b = g * 8 + rem % nbg;
@@ -109,6 +110,33 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
     auto panel = [&](uint32_t s) {
       std::vector<double> xb(c.VP, NAN);
       const uint32_t base = (p0 + std::min(s, npu - 1)) * c.VP;
+      if (c.LD == 1) {  // dma_x + patch_x: wave wl, instruction j, lane -> chunk (j*WL + wl)*64 + lane
+        const int NDMA = (PAIRS + LT - 1) / LT;
+        int patched = 0;
+        for (int wl = 0; wl < c.WL; ++wl)
+          for (int j = 0; j < NDMA; ++j)
+            for (uint32_t lane = 0; lane < 64; ++lane) {
+              const uint32_t c0 = (j * c.WL + wl) * 64, ch = c0 + lane;
+              if (ch >= PAIRS) continue;
+              const uint32_t a = std::min(base + 2 * ch, cmax);
+              const uint32_t dst = 2 * c0 + 2 * lane;  // wave-uniform base + lane * 16 B
+              CHECK(dst + 1 < (uint32_t)c.VP, "dma LDS dst %u", dst);
+              xb[dst] = X.get(a);
+              xb[dst + 1] = X.get(a + 1);
+            }
+        if ((cols & 1) && p0 + s == npanels - 1) {
+          const uint32_t sl = cols - 1 - (p0 + s) * c.VP, ch = sl >> 1;
+          for (int wl = 0; wl < c.WL; ++wl)
+            for (uint32_t lane = 0; lane < 64; ++lane)
+              if (ch < PAIRS && (ch / 64) % c.WL == (uint32_t)wl && (ch & 63) == lane) {
+                CHECK(sl < (uint32_t)c.VP, "odd patch slot %u", sl);
+                xb[sl] = xlast;
+                ++patched;
+              }
+          CHECK(patched == 1, "odd patch applied %d times", patched);
+        }
+        return xb;
+      }
       for (int t = 0; t < LT; ++t)
         for (int j = 0; j < NJ; ++j) {
           const uint32_t a = std::min(base + 2 * (t + j * LT), cmax);
@@ -185,17 +213,22 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
       ylds_of[bid] = ylds;
     }
   }
-  if (c.SPLIT == 2) {  // every block: the second arriver (either order) writes p0 + p1
+  if (c.SPLIT > 1) {  // every block: the last arriver (any order) writes p0 + p1 (+ p2 + p3)
     for (uint32_t bid = 0; bid < units; ++bid) {
       const uint32_t b = b_of[bid], h = h_of[bid];
-      if (++tickets[b] != 2) continue;  // arrival order = unit order here; the sum is order-independent
+      if (++tickets[b] != (uint32_t)c.SPLIT) continue;  // arrival order = unit order here
       const uint32_t r0 = b * rpb, nr = std::min(rpb, rows - r0);
       for (uint32_t i = 0; i < nr; ++i) {
-        const double o = partial.get((size_t)(1 - h) * rows + r0 + i), m = ylds_of[bid][i];
-        Y.put(r0 + i, h == 0 ? m + o : o + m);
+        double acc = 0;
+        for (int q = 0; q < c.SPLIT; ++q) {
+          const double v = (uint32_t)q == h ? ylds_of[bid][i] : partial.get((size_t)q * rows + r0 + i);
+          acc = q == 0 ? v : acc + v;
+        }
+        Y.put(r0 + i, acc);
       }
     }
-    for (uint32_t b = 0; b < nblocks; ++b) CHECK(tickets[b] == 2, "block %u tickets %u", b, tickets[b]);
+    for (uint32_t b = 0; b < nblocks; ++b)
+      CHECK(tickets[b] == (uint32_t)c.SPLIT, "block %u tickets %u", b, tickets[b]);
   }
   return Y.v;
 }
@@ -294,7 +327,12 @@ int main(int argc, char** argv) {
   cases.push_back({"random 257x12161 dense rows", random_csr(257, 12161, 0.3, 11, true)});
   cases.push_back({"random 70000x13001", random_csr(70000, 13001, 0.0008, 13, false)});
   // must match VcCfg<1>/VcCfg<2> in csrc/vcache.hip (WL, DE, EPT)
-  const Cfg cfgs[] = {{kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1}, {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2}};
+  const Cfg cfgs[] = {{kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 0},
+                      {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 0},
+                      {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0},
+                      {kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 1},
+                      {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 1},
+                      {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 1}};
   int failures = 0;
   for (auto& cs : cases) {
     std::vector<double> x(cs.A.cols), yin(cs.A.rows);
@@ -303,7 +341,7 @@ int main(int argc, char** argv) {
     for (const Cfg& c : cfgs) {
       const VcGeom g{c.VR, c.VP, c.SPLIT};
       if (!vcache_eligible(cs.A, g)) {
-        std::printf("%-28s split=%d: not eligible\n", cs.name.c_str(), c.SPLIT);
+        std::printf("%-28s split=%d ld=%d: not eligible\n", cs.name.c_str(), c.SPLIT, c.LD);
         continue;
       }
       VcacheLayout L;
@@ -329,8 +367,8 @@ int main(int argc, char** argv) {
         }
         const bool ok = bad == 0 && g_errors == 0;
         failures += !ok;
-        std::printf("%-28s split=%d beta=%d units=%u panels=%u: %s (%zu rows off, %d violations)\n",
-                    cs.name.c_str(), c.SPLIT, beta, L.nblocks * c.SPLIT, L.npanels, ok ? "ok" : "FAIL", bad,
+        std::printf("%-28s split=%d ld=%d beta=%d units=%u panels=%u: %s (%zu rows off, %d violations)\n",
+                    cs.name.c_str(), c.SPLIT, c.LD, beta, L.nblocks * c.SPLIT, L.npanels, ok ? "ok" : "FAIL", bad,
                     g_errors);
       }
     }

@@ -5,6 +5,8 @@ to SoftwareSpMV (oracle.spmv_csc); the fast f64 kernel (csr_vector) must meet
 the per-row bound of include/hipspmv.h:
     |y - y_ref| <= 2*len*2^-53 * (sum_j |a_ij x_j| + |y_in|)  (+ tiny abs slack)
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -226,3 +228,51 @@ def test_c3_split_deterministic_and_within_bound(gpu):
     y0 = np.random.default_rng(4).uniform(-1, 1, n)
     y1 = h.exec(x, y0.copy(), beta=1, mode=hs.MODE_FAST)
     assert np.all(np.abs(y1 - (y_ref + y0)) <= _fast_bound(np.full(n, 33), absprod + np.abs(y0), 0) * 2)
+
+
+# ---- experimental vcache variants (never chosen by AUTO): four column parts
+# and the LDS-DMA x loader.  Addressing is replayed on the CPU by
+# tests/test_vcache_sim.py; on the GPU they run only with HIPSPMV_EXPERIMENTAL=1
+# until they have been measured on an MI355X.
+EXPERIMENTAL = os.environ.get("HIPSPMV_EXPERIMENTAL") == "1"
+
+
+@pytest.mark.skipif(not EXPERIMENTAL, reason="experimental kernels: set HIPSPMV_EXPERIMENTAL=1")
+@pytest.mark.parametrize("kernel,dma", [("vcache_split4", 0), ("vcache_split4", 1), ("vcache_split", 1),
+                                        ("vcache", 1)])
+def test_experimental_vcache_variants(gpu, kernel, dma):
+    cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20)]
+    for rows, cols in cases:
+        rng = np.random.default_rng(rows)
+        if cols == 1 << 20:
+            rowptr, colind, vals = hs.gen_stripe_csr(0, rows, cols, 32)
+        else:
+            lens = rng.integers(0, 12, rows)
+            rowptr = np.zeros(rows + 1, np.uint32)
+            rowptr[1:] = np.cumsum(lens)
+            colind = np.concatenate([np.sort(rng.choice(cols, n, replace=False)) for n in lens]).astype(np.uint32)
+            vals = rng.uniform(-1, 1, colind.size)
+        x = rng.uniform(-1, 1, cols)
+        h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+        key = {"vcache_split4": "vcache_split4_eligible", "vcache_split": "vcache_split_eligible"}.get(
+            kernel, "vcache_eligible")
+        if not h.stat(key):
+            continue
+        h.set_kernel(kernel)
+        h.set_option("vcache_dma", dma)
+        mode = hs.MODE_ORDERED if kernel == "vcache" else hs.MODE_FAST
+        colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+        for beta in (0, 1):
+            y0 = rng.uniform(-1, 1, rows)
+            y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else None), rows=rows)
+            ys = [h.exec(x, y0.copy(), beta=beta, mode=mode) for _ in range(2)]
+            assert ys[0].tobytes() == ys[1].tobytes()  # deterministic
+            if mode == hs.MODE_ORDERED:
+                assert ys[0].tobytes() == y_ref.tobytes(), (rows, cols, beta)
+            else:
+                lens = np.diff(rowptr.astype(np.int64))
+                absprod = np.bincount(np.repeat(np.arange(rows), lens), weights=np.abs(vals * x[colind]),
+                                      minlength=rows)
+                bound = 2.0 * (lens + 1) * 2.0 ** -53 * (absprod + (np.abs(y0) if beta else 0)) + 1e-300
+                assert np.all(np.abs(ys[0] - y_ref) <= bound), (rows, cols, beta)
+        h.close()
