@@ -48,7 +48,7 @@ int main(int argc, char** argv) {
   double* dx = up(x);
   double *dy, *dpart;
   CK(hipMalloc(&dy, 8ull * n));
-  CK(hipMalloc(&dpart, 16ull * n));
+  CK(hipMalloc(&dpart, 8ull * 4 * n));  // [split][rows] partials, split <= 4
   const double alg = 12.0 * a.nnz + 4.0 * (n + 1) + 16.0 * n;
   auto timeit = [&](auto launch) {
     hipEvent_t e0, e1;
@@ -69,7 +69,7 @@ int main(int argc, char** argv) {
     return ts[ts.size() / 2];
   };
   std::vector<double> yref;
-  for (VcGeom g : {kVcOrdered, kVcSplit}) {
+  for (VcGeom g : {kVcOrdered, kVcSplit, kVcSplit4}) {
     VcacheLayout L;
     build_vcache(a, g, L);
     VcacheArgs A{up(L.seg), up(L.code), up(L.vals), dx, dy, dy, dpart, up(std::vector<uint32_t>(L.nblocks, 0)),
@@ -77,7 +77,14 @@ int main(int argc, char** argv) {
                  g.split, 0};
     std::printf("geometry rows=%d panel=%d split=%d: units=%u npad=%u max_seg=%u\n", g.rows, g.panel, g.split,
                 L.nblocks * g.split, L.npad, L.max_seg);
-    auto variant = [&](auto kern, const char* nm, int mask) {
+    // kern must be compiled for this geometry (the round-1 fault was a split=1
+    // kernel launched on the split layout's grid): SPLIT is checked here
+    auto variant = [&](auto kern, int kernel_split, const char* nm, int mask) {
+      if (kernel_split != g.split || L.rows_per_block > (uint32_t)g.rows ||
+          (uint64_t)L.part_panels * (g.split - 1) >= L.npanels) {
+        std::printf("  %-30s SKIPPED: kernel split %d vs layout split %d\n", nm, kernel_split, g.split);
+        return;
+      }
       const double us = timeit([&] {
         hipLaunchKernelGGL(kern, dim3(A.nblocks * A.split), dim3(kVcThreads), 0, nullptr, A.seg, A.code,
                            (const double*)A.vals, (const double*)A.x, (const double*)A.y_in, (double*)A.y_out,
@@ -95,33 +102,36 @@ int main(int argc, char** argv) {
       }
       std::printf("\n");
     };
+    // template: <T, SPLIT, WL, DE, EPT, AB, MAP, NT, LD>
     if (g.split == 1) {
-      variant(k_vcache<double, 1>, "default (WL8 DE4 EPT3)", 0);
-      variant(k_vcache<double, 1, 4, 4, 2>, "WL4 DE4 EPT2", 0);
-      variant(k_vcache<double, 1, 8, 2, 3>, "WL8 DE2 EPT3", 0);
-      variant(k_vcache<double, 1, 8, 6, 3>, "WL8 DE6 EPT3", 0);
-      variant(k_vcache<double, 1, 8, 4, 3, 3>, "no x", 3);
-      variant(k_vcache<double, 1, 8, 4, 3, 12>, "no entries/compute", 12);
-      variant(k_vcache<double, 1, 8, 4, 3, 15>, "skeleton", 15);
+      variant(k_vcache<double, 1>, 1, "default (WL8 DE4 EPT3)", 0);
+      variant(k_vcache<double, 1, 2, 4, 3, 0, 0, false, 1>, 1, "DMA WL2 DE4 EPT3", 0);
+      variant(k_vcache<double, 1, 1, 4, 3, 0, 0, false, 1>, 1, "DMA WL1 DE4 EPT3", 0);
+      variant(k_vcache<double, 1, 2, 4, 2, 0, 0, false, 1>, 1, "DMA WL2 DE4 EPT2", 0);
+      variant(k_vcache<double, 1, 8, 4, 3, 3>, 1, "no x", 3);
+      variant(k_vcache<double, 1, 8, 4, 3, 12>, 1, "no entries/compute", 12);
+      variant(k_vcache<double, 1, 8, 4, 3, 15>, 1, "skeleton", 15);
+    } else if (g.split == 2) {
+      variant(k_vcache<double, 2>, 2, "default (WL6 DE4 EPT3)", 0);
+      variant(k_vcache<double, 2, 2, 4, 3, 0, 0, false, 1>, 2, "DMA WL2 DE4 EPT3", 0);
+      variant(k_vcache<double, 2, 1, 4, 3, 0, 0, false, 1>, 2, "DMA WL1 DE4 EPT3", 0);
+      variant(k_vcache<double, 2, 2, 4, 2, 0, 0, false, 1>, 2, "DMA WL2 DE4 EPT2", 0);
+      variant(k_vcache<double, 2, 4, 4, 2, 0, 0, false, 1>, 2, "DMA WL4 DE4 EPT2", 0);
+      variant(k_vcache<double, 2, 2, 6, 2, 0, 0, false, 1>, 2, "DMA WL2 DE6 EPT2", 0);
+      variant(k_vcache<double, 2, 6, 4, 3, 3>, 2, "no x", 3);
+      variant(k_vcache<double, 2, 6, 4, 3, 12>, 2, "no entries/compute", 12);
+      variant(k_vcache<double, 2, 6, 4, 3, 15>, 2, "skeleton", 15);
+      variant(k_vcache<double, 2, 2, 4, 3, 12, 0, false, 1>, 2, "DMA no entries/compute", 12);
     } else {
-      variant(k_vcache<double, 2>, "default (WL4 DE4 EPT3)", 0);
-      variant(k_vcache<double, 2, 4, 2, 3>, "WL4 DE2 EPT3", 0);
-      variant(k_vcache<double, 2, 4, 6, 3>, "WL4 DE6 EPT3", 0);
-      variant(k_vcache<double, 2, 6, 4, 3>, "WL6 DE4 EPT3", 0);
-      variant(k_vcache<double, 2, 8, 4, 4>, "WL8 DE4 EPT4", 0);
-      variant(k_vcache<double, 2, 6, 4, 3, 0, 1, false>, "WL6 MAP1", 0);
-      variant(k_vcache<double, 2, 6, 4, 3, 0, 0, true>, "WL6 NT", 0);
-      variant(k_vcache<double, 2, 6, 4, 3, 0, 1, true>, "WL6 MAP1 NT", 0);
-      variant(k_vcache<double, 2, 6, 4, 3, 16, 1, true>, "WL6 MAP1 NT x-L2hot", 16);
-      variant(k_vcache<double, 2, 6, 4, 3, 12, 1, true>, "WL6 MAP1 NT no entries", 12);
-      variant(k_vcache<double, 2, 4, 4, 3, 1>, "no x loads", 1);
-      variant(k_vcache<double, 2, 4, 4, 3, 3>, "no x", 3);
-      variant(k_vcache<double, 2, 4, 4, 3, 4>, "no entry loads", 4);
-      variant(k_vcache<double, 2, 4, 4, 3, 8>, "no compute", 8);
-      variant(k_vcache<double, 2, 4, 4, 3, 12>, "no entries/compute", 12);
-      variant(k_vcache<double, 2, 4, 4, 3, 15>, "skeleton", 15);
-      variant(k_vcache<double, 2, 4, 4, 3, 16>, "x L2-hot", 16);
-      variant(k_vcache<double, 2, 4, 4, 3, 47>, "skeleton no barrier", 47);
+      variant(k_vcache<double, 4>, 4, "default (WL2 DE4 EPT2)", 0);
+      variant(k_vcache<double, 4, 4, 4, 2>, 4, "WL4 DE4 EPT2", 0);
+      variant(k_vcache<double, 4, 2, 6, 2>, 4, "WL2 DE6 EPT2", 0);
+      variant(k_vcache<double, 4, 2, 4, 3>, 4, "WL2 DE4 EPT3", 0);
+      variant(k_vcache<double, 4, 1, 4, 2, 0, 0, false, 1>, 4, "DMA WL1 DE4 EPT2", 0);
+      variant(k_vcache<double, 4, 2, 4, 2, 0, 0, false, 1>, 4, "DMA WL2 DE4 EPT2", 0);
+      variant(k_vcache<double, 4, 2, 4, 2, 3>, 4, "no x", 3);
+      variant(k_vcache<double, 4, 2, 4, 2, 12>, 4, "no entries/compute", 12);
+      variant(k_vcache<double, 4, 2, 4, 2, 15>, 4, "skeleton", 15);
     }
   }
   return 0;
