@@ -28,6 +28,11 @@ for s in $STEPS; do
     pmc) export TMPDIR=/tmp; step pmc 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
          step pmc2 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     micro) step micro 300 ./spmv-vector-cache_amd/tools/microbench ;;
+    exp) HIPSPMV_EXPERIMENTAL=1 step pytest_exp 600 python -m pytest tests/test_gpu_parity.py -m gpu -q -x -p no:cacheprovider -k experimental ;;
+    ablate) step ablate 600 ./spmv-vector-cache_amd/lib/vc_ablate ;;
+    c4) step bench_c4 900 python bench.py --workload c4 --steps 20 --warmup 5 ;;
+    c5) step bench_c5 900 python bench.py --workload c5 --steps 20 --warmup 5 ;;
+    multi) step spmvbench_multi 300 ./spmv-vector-cache_amd/lib/spmvbench --dir tests/golden/matrices --confs hip,hip4 --cms 0 --reps 3 circuit204 i64k row64k ;;
   esac
 done
 echo "session done"
