@@ -70,6 +70,9 @@ extern "C" {
                                           deterministic; experimental: never
                                           chosen by AUTO, layout built only
                                           when HIPSPMV_EXPERIMENTAL=1 at create */
+#define HIPSPMV_KERNEL_WGATHER 6 /* y block in LDS, x gathered from global in
+                                    2^17-column windows (wide x: C4/C5);
+                                    ordered; experimental like VCACHE_SPLIT4 */
 
 typedef struct hipspmv_handle hipspmv_t;
 
@@ -115,7 +118,8 @@ int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void 
  * "vcache_max_segment" "vcache_eligible" "vcache_split_eligible"
  * "vcache_split_units" "vcache_split_rows_per_block" "vcache_x_bytes"
  * "vcache_split_x_bytes" (x bytes one launch streams into LDS)
- * "vcache_split4_eligible" "vcache_split4_x_bytes" "row_groups"
+ * "vcache_split4_eligible" "vcache_split4_x_bytes" "wgather_eligible"
+ * "wgather_windows" "row_groups"
  * "max_row_len" "empty_rows" "execs". */
 int hipspmv_stat(hipspmv_t *h, const char *key, uint64_t *out);
 

@@ -78,7 +78,7 @@ struct hipspmv_handle {
     uint64_t *d_vals = nullptr, *d_partial = nullptr;
     uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, part_panels = 0, npad = 0, max_seg = 0;
     int split = 1;
-  } vc[3];  // [0] ordered (kVcOrdered), [1] split (kVcSplit), [2] split4 (kVcSplit4, experimental)
+  } vc[4];  // [0] ordered (kVcOrdered), [1] split (kVcSplit); experimental: [2] split4, [3] wgather windows
   int vcache_dma = 0;  // option "vcache_dma": LDS-DMA x loader (experimental)
   void *d_x = nullptr, *d_y = nullptr;
   int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
@@ -123,11 +123,11 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   build_row_groups(a, groups);
   h->ngroups = (uint32_t)groups.size() - 1;
   if ((st = dev_upload(&h->d_groups, groups.data(), groups.size(), h->device_bytes))) return st;
-  const VcGeom geoms[3] = {kVcOrdered, kVcSplit, kVcSplit4};
-  // the experimental four-part layout is built only on request
-  // (HIPSPMV_EXPERIMENTAL=1): it costs another copy of the entries
+  const VcGeom geoms[4] = {kVcOrdered, kVcSplit, kVcSplit4, kWgWindow};
+  // the experimental layouts are built only on request
+  // (HIPSPMV_EXPERIMENTAL=1): each costs another copy of the entries
   const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
-  const int nlayouts = exp && std::strcmp(exp, "1") == 0 ? 3 : 2;
+  const int nlayouts = exp && std::strcmp(exp, "1") == 0 ? 4 : 2;
   for (int k = 0; k < nlayouts; ++k) {
     auto& v = h->vc[k];
     v.ok = vcache_eligible(a, geoms[k]);
@@ -206,6 +206,8 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
     case HIPSPMV_KERNEL_VCACHE_SPLIT4:
       if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
       return h->vc[2].ok ? HIPSPMV_KERNEL_VCACHE_SPLIT4 : -HIPSPMV_ERR_UNSUPPORTED;
+    case HIPSPMV_KERNEL_WGATHER:  // ordered: valid in both modes
+      return h->vc[3].ok ? HIPSPMV_KERNEL_WGATHER : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_LANE:
       return HIPSPMV_KERNEL_CSR_LANE;
     case HIPSPMV_KERNEL_CSR_VECTOR:
@@ -237,6 +239,12 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                  v.d_tickets, h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
                  v.npad,      h->nnz - 1, v.split,   beta, h->vcache_dma, (uint32_t)geoms[k].panel};
     e = launch_vcache(h->dtype, a, s);
+  } else if (kernel == HIPSPMV_KERNEL_WGATHER) {
+    const auto& v = h->vc[3];
+    VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    nullptr,
+                 nullptr,     h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
+                 v.npad,      h->nnz - 1, 1,         beta, 0,       (uint32_t)kWgWindow.panel};
+    e = launch_wgather(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
     e = kernel == HIPSPMV_KERNEL_CSR_LANE ? launch_csr_lane(h->dtype, a, s) : launch_csr_vector(h->dtype, a, s);
@@ -292,7 +300,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   if (!h || !key) return HIPSPMV_ERR_INVALID_ARG;
   const std::string k(key);
   if (k == "kernel") {
-    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_VCACHE_SPLIT4) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_WGATHER) return HIPSPMV_ERR_INVALID_ARG;
     h->kernel_opt = (int)value;
   } else if (k == "vcache_dma") {
     h->vcache_dma = value ? 1 : 0;
@@ -398,6 +406,8 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "vcache_x_bytes") *out = h->vc[0].ok ? 8ull * h->vc[0].nblocks * h->cols : 0;
   else if (k == "vcache_split_x_bytes") *out = h->vc[1].ok ? 8ull * h->vc[1].nblocks * h->cols : 0;
   else if (k == "vcache_split4_eligible") *out = h->vc[2].ok;
+  else if (k == "wgather_eligible") *out = h->vc[3].ok;
+  else if (k == "wgather_windows") *out = h->vc[3].npanels;
   else if (k == "vcache_split4_x_bytes") *out = h->vc[2].ok ? 8ull * h->vc[2].nblocks * h->cols : 0;
   else if (k == "row_groups") *out = h->ngroups;
   else if (k == "max_row_len") *out = h->max_row_len;
@@ -413,6 +423,7 @@ const char* hipspmv_kernel_name(hipspmv_t* h, int mode) {
     case HIPSPMV_KERNEL_VCACHE: return "vcache";
     case HIPSPMV_KERNEL_VCACHE_SPLIT: return "vcache_split";
     case HIPSPMV_KERNEL_VCACHE_SPLIT4: return "vcache_split4";
+    case HIPSPMV_KERNEL_WGATHER: return "wgather";
     case HIPSPMV_KERNEL_CSR_LANE: return "csr_lane";
     case HIPSPMV_KERNEL_CSR_VECTOR: return "csr_vector";
     default: return "unsupported";

@@ -21,11 +21,17 @@ namespace hipspmv {
 // (p0 + p1), so it is deterministic but not bit-identical: FAST mode.
 struct VcGeom {
   int rows, panel, split;
+  int colbits = 16;  // entry code: col_local | row_local << colbits | CONT | MORE
 };
 constexpr VcGeom kVcOrdered{4096, 8128, 1};
 constexpr VcGeom kVcSplit{8192, 6080, 2};
 //   split4 : 16384 rows, 4 parts: 131072 + 2*1984*8 + 1024 (experimental)
 constexpr VcGeom kVcSplit4{16384, 1984, 4};
+// ---- k_wgather: the same segment layout over column WINDOWS of 2^17 columns
+// (1 MiB of x, L2-resident) with x gathered from global memory instead of
+// staged in LDS -- for matrices whose x is too wide for LDS streaming to pay
+// (C4/C5: 16M columns).  y block in LDS (<= 8192 rows, 13 bits), ORDERED.
+constexpr VcGeom kWgWindow{8192, 1 << 17, 1, 17};
 constexpr int kVcThreads = 1024;
 constexpr int kVcSegMax = 256;        // npad + 1 <= kVcSegMax per unit
 constexpr int kVcEpt = 2;             // entries per thread held in registers per panel

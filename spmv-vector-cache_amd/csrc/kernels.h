@@ -35,6 +35,7 @@ struct CsrArgs {
 };
 
 hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);
+hipError_t launch_wgather(int dtype, const VcacheArgs& a, hipStream_t s);
 hipError_t launch_csr_lane(int dtype, const CsrArgs& a, hipStream_t s);
 hipError_t launch_csr_vector(int dtype, const CsrArgs& a, hipStream_t s);
 

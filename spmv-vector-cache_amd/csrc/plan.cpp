@@ -90,6 +90,8 @@ static uint32_t vcache_rows_per_block(uint32_t rows, const VcGeom& g) {
 
 bool vcache_eligible(const HostCSR& a, const VcGeom& g) {
   if (a.cols < 2 || a.rows == 0 || a.nnz == 0) return false;
+  // the entry code must hold col_local and row_local
+  if ((uint64_t)g.panel > (1ull << g.colbits) || (uint64_t)g.rows > (1ull << (30 - g.colbits))) return false;
   const uint32_t np = (a.cols + g.panel - 1) / g.panel;
   if (np < (uint32_t)g.split) return false;  // every column part needs >= 1 panel
   const uint32_t part = (np + g.split - 1) / g.split;
@@ -147,7 +149,7 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
       for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
         const uint32_t c = a.colind[e], p = c / P;
         const uint32_t d = base + cur[p]++;
-        uint32_t code = (c - p * P) | ((r - r0) << 16);
+        uint32_t code = (c - p * P) | ((r - r0) << g.colbits);
         if (p == prev_p && d == prev_d + 1) {  // same row, same segment, adjacent: extend the run
           code |= kVcCont;
           out.code[prev_d] |= kVcMore;

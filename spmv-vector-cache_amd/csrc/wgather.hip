@@ -1,0 +1,120 @@
+// k_wgather: windowed-gather SpMV for wide x (experimental).
+//
+// When x is too wide for the LDS vector cache to pay (C4/C5: 16M columns,
+// x = 128 MB; every row block would have to stream all of it), x stays in
+// global memory and is gathered per nonzero -- but in column WINDOWS: the
+// entries of row block b that fall into window w (2^CB columns, 1 MiB of x)
+// form segment (b, w) of the vcache layout (csrc/plan.cpp build_vcache with
+// kWgWindow), and every workgroup walks the windows in the same order, so the
+// whole chip gathers from one L2-resident window at a time instead of from
+// all 128 MB.  The row block's y accumulators live in LDS as in k_vcache;
+// within a window each row is one run processed by one lane in column order,
+// windows are separated by a barrier, so every row is summed in ascending
+// column order from y_in or +0.0: ORDERED, bit-identical to SoftwareSpMV.
+//
+// Bytes per launch: 12 per nonzero (entries) + 8 per distinct (block, column)
+// gather line touched + 8 per row of y (+8 for beta 1).
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "hipspmv_internal.h"
+#include "kernels.h"
+
+namespace hipspmv {
+
+template <typename T, int CB, int DE, int EPT>
+__global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restrict__ seg,
+                                                         const uint32_t* __restrict__ ecode,
+                                                         const T* __restrict__ evals, const T* __restrict__ x,
+                                                         const T* __restrict__ y_in, T* __restrict__ y_out,
+                                                         uint32_t rows, uint32_t rows_per_block, uint32_t npanels,
+                                                         uint32_t npad, uint32_t last, int beta) {
+#pragma clang fp contract(off)
+  constexpr int VT = kVcThreads;
+  constexpr uint32_t W = 1u << CB, CMASK = W - 1, RMASK = (1u << (30 - CB)) - 1;
+  constexpr int VR = 1 << (30 - CB);
+  __shared__ T ylds[VR];
+  __shared__ uint32_t segl[kVcSegMax];
+  const int t = threadIdx.x;
+  const uint32_t b = blockIdx.x;
+  const uint32_t r0 = b * rows_per_block;
+  const uint32_t nr = min(rows_per_block, rows - r0);
+  const uint32_t* sp = seg + (size_t)b * (npad + 1);
+  if ((uint32_t)t <= npad) segl[t] = sp[t];
+  for (uint32_t i = t; i < nr; i += VT) ylds[i] = beta ? y_in[r0 + i] : T(0);
+  __syncthreads();
+
+  auto load_e = [&](uint32_t s, uint32_t* c, T* v) {
+    const uint32_t beg = segl[min(s, npad)];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const uint32_t i = min(beg + t + j * VT, last);  // clamped, validity checked at use
+      c[j] = ecode[i];
+      v[j] = evals[i];
+    }
+  };
+  auto run = [&](uint32_t i, uint32_t code, T v, T xv, const T* xs) {
+    const uint32_t row = (code >> CB) & RMASK;
+    T acc = madd(ylds[row], v, xv);
+    while (code & kVcMore) {  // several entries of one row in this window (rare)
+      ++i;
+      code = ecode[i];
+      acc = madd(acc, evals[i], xs[code & CMASK]);
+    }
+    ylds[row] = acc;
+  };
+  auto apply = [&](uint32_t s, const uint32_t* c, const T* v) {
+    const T* xs = x + (size_t)s * W;
+    const uint32_t beg = segl[s], end = segl[s + 1];
+    T xv[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {  // all gathers first, then the LDS updates
+      const bool act = beg + t + j * VT < end && !(c[j] & kVcCont);
+      xv[j] = act ? xs[c[j] & CMASK] : T(0);
+    }
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const uint32_t q = beg + t + j * VT;
+      if (q < end && !(c[j] & kVcCont)) run(q, c[j], v[j], xv[j], xs);
+    }
+    for (uint32_t q = beg + EPT * VT + t; q < end; q += VT) {  // beyond the register window
+      const uint32_t code = ecode[q];
+      if (!(code & kVcCont)) run(q, code, evals[q], xs[code & CMASK], xs);
+    }
+  };
+
+  uint32_t EC[DE][EPT];
+  T EV[DE][EPT];
+#pragma unroll
+  for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i]);
+  for (uint32_t base = 0; base < npanels; base += DE) {
+#pragma unroll
+    for (int i = 0; i < DE; ++i) {
+      const uint32_t s = base + i;
+      if (s >= npanels) break;
+      apply(s, EC[i], EV[i]);
+      load_e(s + DE, EC[i], EV[i]);
+      __syncthreads();  // window s's y updates before window s+1's
+    }
+  }
+  for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
+}
+
+template <typename T>
+static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((k_wgather<T, 17, 4, 2>), dim3(a.nblocks), dim3(kVcThreads), 0, s, a.seg, a.code,
+                     (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
+                     a.npanels, a.npad, a.last, a.beta);
+  return hipGetLastError();
+}
+
+hipError_t launch_wgather(int dtype, const VcacheArgs& a, hipStream_t s) {
+  // the layout must be kWgWindow's (window width, row-block bound, one part)
+  if (a.split != 1 || a.panel != (uint32_t)kWgWindow.panel || a.rows_per_block > (uint32_t)kWgWindow.rows ||
+      (uint64_t)a.nblocks * a.rows_per_block < a.rows || (uint64_t)a.npanels * kWgWindow.panel < a.cols ||
+      a.part_panels != a.npanels || a.npad + 1 > (uint32_t)kVcSegMax)
+    return hipErrorInvalidValue;
+  return dtype ? launch_wgather_t<uint64_t>(a, s) : launch_wgather_t<double>(a, s);
+}
+
+}  // namespace hipspmv

@@ -32,6 +32,7 @@ for s in $STEPS; do
     ablate) step ablate 600 ./spmv-vector-cache_amd/lib/vc_ablate ;;
     c4) step bench_c4 900 python bench.py --workload c4 --steps 20 --warmup 5 ;;
     c5) step bench_c5 900 python bench.py --workload c5 --steps 20 --warmup 5 ;;
+    c4wg) HIPSPMV_EXPERIMENTAL=1 step bench_c4_wgather 900 python bench.py --workload c4 --scale 24 --kernel wgather --mode ordered --steps 10 --warmup 3 --no-secondary ;;
     multi) step spmvbench_multi 300 ./spmv-vector-cache_amd/lib/spmvbench --dir tests/golden/matrices --confs hip,hip4 --cms 0 --reps 3 circuit204 i64k row64k ;;
   esac
 done

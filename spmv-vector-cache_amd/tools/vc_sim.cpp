@@ -13,6 +13,7 @@
 //
 // Test infrastructure (tests/test_vcache_sim.py); not part of the product.
 //   g++ -O2 -std=c++17 -Icsrc -I../include tools/vc_sim.cpp csrc/plan.cpp host/Synthetic.cpp -o lib/vc_sim
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -56,7 +57,8 @@ struct Buf {  // bounds-checked global array
 // kernel configuration mirrored from vcache.hip VcCfg<SPLIT>
 struct Cfg {
   int VR, VP, WL, DE, EPT, SPLIT;
-  int LD = 0;  // 0: register-staged x loader, 1: LDS-DMA loader
+  int LD = 0;  // 0: register-staged x loader, 1: LDS-DMA loader, 2: k_wgather (x gathered from global)
+  int CB = 16; // column bits of the entry code
 };
 
 static double madd(double acc, double a, double b) {
@@ -67,9 +69,11 @@ static double madd(double acc, double a, double b) {
 // Replays k_vcache for every unit; returns y.
 static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, const Cfg& c, const std::vector<double>& x,
                                     const std::vector<double>& yin, int beta) {
-  const int VT = 1024, NW = VT / 64, WC = NW - c.WL, LT = c.WL * 64, CT = WC * 64;
+  const bool gather = c.LD == 2;  // k_wgather: every wave computes, no loader role
+  const int VT = 1024, NW = VT / 64, WC = gather ? NW : NW - c.WL, LT = c.WL * 64, CT = WC * 64;
+  const uint32_t CMASK = (1u << c.CB) - 1, RMASK = (1u << (30 - c.CB)) - 1;
   const uint32_t PAIRS = c.VP / 2;
-  const int NJ = (PAIRS + LT - 1) / LT;
+  const int NJ = LT ? (int)((PAIRS + LT - 1) / LT) : 0;
   const uint32_t rows = A.rows, cols = A.cols, nblocks = L.nblocks, npanels = L.npanels, part = L.part_panels,
                  npad = L.npad, rpb = L.rows_per_block, last = (uint32_t)L.code.size() - 1;
   Buf<uint32_t> seg{"seg", L.seg}, code{"ecode", L.code};
@@ -108,8 +112,9 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
     const double xlast = X.get(cols - 1);
     // loader: the LDS image of x panel s (load_x + store_x)
     auto panel = [&](uint32_t s) {
-      std::vector<double> xb(c.VP, NAN);
+      std::vector<double> xb(gather ? 0 : c.VP, NAN);
       const uint32_t base = (p0 + std::min(s, npu - 1)) * c.VP;
+      if (gather) return xb;  // x read from global at use (xat)
       if (c.LD == 1) {  // dma_x + patch_x: wave wl, instruction j, lane -> chunk (j*WL + wl)*64 + lane
         const int NDMA = (PAIRS + LT - 1) / LT;
         int patched = 0;
@@ -156,7 +161,16 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
       return xb;
     };
     for (uint32_t s = 0; s < npu; ++s) {
-      const std::vector<double> xs = panel(s);
+      const std::vector<double> xsv = panel(s);
+      const uint64_t wbase = (uint64_t)(p0 + s) * c.VP;
+      auto xs_at = [&](uint32_t col) {
+        if (gather) {
+          CHECK(wbase + col < cols, "gather x[%llu] beyond cols %u", (unsigned long long)(wbase + col), cols);
+          return X.get(wbase + col);
+        }
+        CHECK(col < (uint32_t)c.VP, "x LDS col %u", col);
+        return xsv[col];
+      };
       const uint32_t beg = segl[s], end = segl[s + 1];
       CHECK(beg <= end, "segment %u [%u,%u)", s, beg, end);
       std::set<uint32_t> written;  // y rows written this step (race check)
@@ -173,18 +187,18 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
           const uint32_t ei = beg + ct + j * CT;
           const bool act = ei < end && !(cc[j] & kVcCont);
           if (!act) continue;
-          const uint32_t row = (cc[j] >> 16) & 0x3FFF, col = cc[j] & 0xFFFF;
+          const uint32_t row = (cc[j] >> c.CB) & RMASK, col = cc[j] & CMASK;
           CHECK(row < nr, "row_local %u >= nr %u (unit %u step %u)", row, nr, bid, s);
           CHECK(col < (uint32_t)c.VP, "col_local %u", col);
           CHECK(!written.count(row), "race: row %u written twice in step %u of unit %u", row, s, bid);
           written.insert(row);
-          double acc = madd(ylds[row], vv[j], xs[col]);
+          double acc = madd(ylds[row], vv[j], xs_at(col));
           if (cc[j] & kVcMore) {
             uint32_t i = ei, cd = cc[j];
             do {
               ++i;
               cd = code.get(i);
-              acc = madd(acc, vals.get(i), xs[cd & 0xFFFF]);
+              acc = madd(acc, vals.get(i), xs_at(cd & CMASK));
             } while (cd & kVcMore);
           }
           ylds[row] = acc;
@@ -192,15 +206,15 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
         for (uint32_t q = beg + c.EPT * CT + ct; q < end; q += CT) {  // overflow
           uint32_t cd = code.get(q);
           if (cd & kVcCont) continue;
-          const uint32_t row = (cd >> 16) & 0x3FFF;
+          const uint32_t row = (cd >> c.CB) & RMASK;
           CHECK(row < nr && !written.count(row), "overflow row %u", row);
           written.insert(row);
-          double acc = madd(ylds[row], vals.get(q), xs[cd & 0xFFFF]);
+          double acc = madd(ylds[row], vals.get(q), xs_at(cd & CMASK));
           uint32_t i = q;
           while (cd & kVcMore) {
             ++i;
             cd = code.get(i);
-            acc = madd(acc, vals.get(i), xs[cd & 0xFFFF]);
+            acc = madd(acc, vals.get(i), xs_at(cd & CMASK));
           }
           ylds[row] = acc;
         }
@@ -322,6 +336,21 @@ int main(int argc, char** argv) {
     std::memcpy(A.vals.data(), v.data(), 8ull * A.nnz);
     cases.push_back({"rmat s14", std::move(A)});
   }
+  // wide x (32 gather windows) and tall (more than 256 row blocks of 8192)
+  for (const auto& shp : {std::array<uint32_t, 3>{20000, 1u << 22, 32}, std::array<uint32_t, 3>{2200001, 5003, 1}}) {
+    const uint32_t n = shp[0], cols = shp[1], k = shp[2];
+    HostCSR A;
+    A.rows = n;
+    A.cols = cols;
+    A.nnz = n * k;
+    A.rowptr.resize(n + 1);
+    A.colind.resize(A.nnz);
+    std::vector<double> v(A.nnz);
+    genStripeCSR(7, n, cols, k, 1, 2, A.rowptr.data(), A.colind.data(), v.data());
+    A.vals.resize(A.nnz);
+    std::memcpy(A.vals.data(), v.data(), 8ull * A.nnz);
+    cases.push_back({"stripe " + std::to_string(n) + "x" + std::to_string(cols), std::move(A)});
+  }
   cases.push_back({"random 3000x20001", random_csr(3000, 20001, 0.002, 7, true)});
   cases.push_back({"random 5000x333", random_csr(5000, 333, 0.12, 9, false)});
   cases.push_back({"random 257x12161 dense rows", random_csr(257, 12161, 0.3, 11, true)});
@@ -332,14 +361,15 @@ int main(int argc, char** argv) {
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0},
                       {kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 1},
                       {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 1},
-                      {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 1}};
+                      {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 1},
+                      {kWgWindow.rows, kWgWindow.panel, 0, 4, 2, 1, 2, kWgWindow.colbits}};
   int failures = 0;
   for (auto& cs : cases) {
     std::vector<double> x(cs.A.cols), yin(cs.A.rows);
     for (uint32_t i = 0; i < cs.A.cols; ++i) x[i] = uniform11(splitmix64_at(3, i));
     for (uint32_t i = 0; i < cs.A.rows; ++i) yin[i] = uniform11(splitmix64_at(5, i));
     for (const Cfg& c : cfgs) {
-      const VcGeom g{c.VR, c.VP, c.SPLIT};
+      const VcGeom g{c.VR, c.VP, c.SPLIT, c.CB};
       if (!vcache_eligible(cs.A, g)) {
         std::printf("%-28s split=%d ld=%d: not eligible\n", cs.name.c_str(), c.SPLIT, c.LD);
         continue;

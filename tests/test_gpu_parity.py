@@ -239,12 +239,12 @@ EXPERIMENTAL = os.environ.get("HIPSPMV_EXPERIMENTAL") == "1"
 
 @pytest.mark.skipif(not EXPERIMENTAL, reason="experimental kernels: set HIPSPMV_EXPERIMENTAL=1")
 @pytest.mark.parametrize("kernel,dma", [("vcache_split4", 0), ("vcache_split4", 1), ("vcache_split", 1),
-                                        ("vcache", 1)])
+                                        ("vcache", 1), ("wgather", 0)])
 def test_experimental_vcache_variants(gpu, kernel, dma):
-    cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20)]
+    cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20), (20000, 1 << 22)]
     for rows, cols in cases:
         rng = np.random.default_rng(rows)
-        if cols == 1 << 20:
+        if cols >= 1 << 20:
             rowptr, colind, vals = hs.gen_stripe_csr(0, rows, cols, 32)
         else:
             lens = rng.integers(0, 12, rows)
@@ -254,13 +254,13 @@ def test_experimental_vcache_variants(gpu, kernel, dma):
             vals = rng.uniform(-1, 1, colind.size)
         x = rng.uniform(-1, 1, cols)
         h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
-        key = {"vcache_split4": "vcache_split4_eligible", "vcache_split": "vcache_split_eligible"}.get(
-            kernel, "vcache_eligible")
+        key = {"vcache_split4": "vcache_split4_eligible", "vcache_split": "vcache_split_eligible",
+               "wgather": "wgather_eligible"}.get(kernel, "vcache_eligible")
         if not h.stat(key):
             continue
         h.set_kernel(kernel)
         h.set_option("vcache_dma", dma)
-        mode = hs.MODE_ORDERED if kernel == "vcache" else hs.MODE_FAST
+        mode = hs.MODE_ORDERED if kernel in ("vcache", "wgather") else hs.MODE_FAST
         colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
         for beta in (0, 1):
             y0 = rng.uniform(-1, 1, rows)
