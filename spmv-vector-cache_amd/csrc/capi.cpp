@@ -218,7 +218,7 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
       return -HIPSPMV_ERR_INVALID_ARG;
   }
   // The LDS vector cache pays when each x element a work unit streams feeds
-  // enough nonzeros (DESIGN.md §6.5).
+  // enough nonzeros (DESIGN.md §6.6).
   auto worth = [&](const hipspmv_handle::Vc& v) {
     return v.ok && (uint64_t)h->nnz * 16 * v.split >= (uint64_t)v.nblocks * v.split * h->cols;
   };

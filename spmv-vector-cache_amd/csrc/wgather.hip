@@ -1,4 +1,4 @@
-// k_wgather: windowed-gather SpMV for wide x (DESIGN.md §6.6; experimental).
+// k_wgather: windowed-gather SpMV for wide x (DESIGN.md §6.5; experimental).
 //
 // When x is too wide for the LDS vector cache to pay (C4/C5: 16M columns,
 // x = 128 MB; every row block would have to stream all of it), x stays in
