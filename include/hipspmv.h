@@ -94,7 +94,11 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
 
 /* Options: "kernel" (HIPSPMV_KERNEL_*), "mode" (default mode for exec with
  * HIPSPMV_MODE_AUTO), "timing" (1 = record per-exec kernel events),
- * "vcache_dma" (1 = vcache kernels stage x by LDS-DMA; experimental). */
+ * "vcache_dma" (1 = vcache kernels stage x by LDS-DMA; experimental),
+ * "vcache_xlane" (1 = vcache run continuations across lanes instead of
+ * reloads; 2 = that plus register rings loaded by inline asm with explicit
+ * vmcnt waits, so the DE-deep entry prefetch survives the loop header;
+ * experimental). */
 int hipspmv_set_option(hipspmv_t *h, const char *key, int64_t value);
 
 /* Replaces HardwareSpMV::exec()'s reset -> init -> regular -> write sequence

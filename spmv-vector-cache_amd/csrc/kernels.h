@@ -20,6 +20,8 @@ struct VcacheArgs {
   int split, beta;
   int dma = 0;        // x panels by LDS-DMA (experimental loader, option "vcache_dma")
   uint32_t panel = 0; // the layout's panel width: checked against the kernel's
+  int xlane = 0;      // cross-lane run continuation (experimental, option "vcache_xlane")
+  uint32_t max_seg = 0;  // longest segment of the layout (xlane needs it in the register window)
 };
 
 struct CsrArgs {

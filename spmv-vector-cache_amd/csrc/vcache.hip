@@ -46,12 +46,42 @@ struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane
   static constexpr int VR = kVcSplit4.rows, VP = kVcSplit4.panel, WL = 2, DE = 4, EPT = 2;
 };
 
+// Loads the compiler's waitcnt pass does not see (CX == 2 / LD == 2 rings):
+// hipcc (ROCm 7.2) merges the pending-load state pessimistically at a loop
+// header and emits s_waitcnt vmcnt(0) there -- draining a DE-deep register
+// ring once per unrolled group (tools probe: a 4-slot ring gets vmcnt(0) at
+// the header and vmcnt(3) elsewhere).  Loads issued by inline asm are
+// invisible to that pass; the kernel then waits with explicit, exact counts
+// (vmcnt is in order for loads on gfx9).  Only the ring's own loads may be in
+// flight between a load and its wait for the counts to hold.
+__device__ __forceinline__ uint32_t ald_u32(const uint32_t* p) {
+  uint32_t r;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ T ald_64(const T* p) {
+  uint64_t r;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return __builtin_bit_cast(T, r);
+}
+__device__ __forceinline__ u64x2 ald_128(const void* p) {
+  u64x2 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // AB: ablation mask for the diagnostic build (tools/vc_ablate.hip); the
 // product instantiates AB = 0 and every hook folds away.  Bits: 1 no x loads,
 // 2 no x LDS stores, 4 no entry loads, 8 no compute, 16 x always from panel 0,
 // 32 no per-panel barrier (wrong results, timing only).
 template <typename T, int SPLIT, int WL = VcCfg<SPLIT>::WL, int DE = VcCfg<SPLIT>::DE, int EPT = VcCfg<SPLIT>::EPT,
-          int AB = 0, int MAP = 0, bool NT = false, int LD = 0>
+          int AB = 0, int MAP = 0, bool NT = false, int LD = 0, int CX = 0>
 __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restrict__ seg,
                                                         const uint32_t* __restrict__ ecode,
                                                         const T* __restrict__ evals, const T* __restrict__ x,
@@ -105,8 +135,10 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     if (AB & 1) return;
     const uint32_t base = (AB & 16) ? 0 : (p0 + min(s, npu - 1)) * VP;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      r[j] = *reinterpret_cast<const u64x2*>(x + min(base + 2 * (t + j * LT), cmax));
+    for (int j = 0; j < NJ; ++j) {
+      const T* src = x + min(base + 2 * (t + j * LT), cmax);
+      r[j] = LD == 2 ? ald_128(src) : *reinterpret_cast<const u64x2*>(src);
+    }
   };
   // LD == 1: the loader lanes' 16-byte chunks go straight into LDS.  A
   // wave-instruction writes 64 consecutive chunks (wave-uniform base + lane *
@@ -161,7 +193,10 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const uint32_t i = min(beg + ct + j * CT, last);
-      if (NT) {  // streamed once: non-temporal, so the entries do not evict x from L2
+      if (CX == 2) {
+        c[j] = ald_u32(ecode + i);
+        v[j] = ald_64(evals + i);
+      } else if (NT) {  // streamed once: non-temporal, so the entries do not evict x from L2
         c[j] = __builtin_nontemporal_load(ecode + i);
         v[j] = __builtin_nontemporal_load(evals + i);
       } else {
@@ -195,6 +230,75 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     }
   };
 
+  // CX == 1: the same arithmetic with no vector-memory access besides the
+  // entry ring, so every wave's vmcnt waits stay partial and the DE-deep
+  // prefetch survives (a run continuation or overflow load is the youngest
+  // VMEM op and its wait drains the whole ring: measured round 1, see
+  // DESIGN.md §6.5).  Every valid lane forms its product; a run head adds its
+  // continuation products taken from the next lanes of its wave
+  // (__shfl_down: LDS crossbar, lgkmcnt); a run that continues past the wave
+  // (lane 63 -> next wave) finishes with scalar loads.  Requires every segment
+  // to fit the register window (max_seg <= EPT*CT, checked at launch).
+  const uint32_t lw = t & 63;
+  auto sload32 = [](const uint32_t* p) {
+    uint32_t r;
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
+    return r;
+  };
+  auto sload64 = [](const T* p) {
+    uint64_t r;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
+    return __builtin_bit_cast(T, r);
+  };
+  auto apply_cx = [&](uint32_t s, const uint32_t* c, const T* v) {
+    if (AB & 8) return;
+    const T* xs = xb[s & 1];
+    const uint32_t beg = segl[s], end = segl[s + 1];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const uint32_t q = beg + ct + j * CT;
+      const uint32_t code = c[j];
+      const bool valid = q < end;
+      const T p = valid ? v[j] * xs[code & 0xFFFF] : T(0);  // rounded product (contract off)
+      const bool own = valid && !(code & kVcCont);
+      const uint32_t row = (code >> 16) & 0x3FFF;
+      T acc = own ? ylds[row] + p : T(0);
+      bool more = own && (code & kVcMore);
+      bool fb = false;
+      uint32_t fbi = 0;
+      for (uint32_t k = 1; __builtin_amdgcn_ballot_w64(more) != 0; ++k) {  // wave-uniform trip count
+        const T pk = __shfl_down(p, k);
+        const uint32_t ck = __shfl_down(code, k);
+        if (more) {
+          if (lw + k < 64) {
+            acc = acc + pk;
+            more = (ck & kVcMore) != 0;
+          } else {  // the run continues in the next wave's lanes
+            fb = true;
+            fbi = q + k;
+            more = false;
+          }
+        }
+      }
+      for (uint64_t m = __builtin_amdgcn_ballot_w64(fb); m; m &= m - 1) {  // rare
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        uint32_t i = __builtin_amdgcn_readlane(fbi, l);
+        const uint64_t ab = __builtin_bit_cast(uint64_t, acc);
+        T a = __builtin_bit_cast(T, (uint64_t)__builtin_amdgcn_readlane((uint32_t)ab, l) |
+                                        ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ab >> 32), l) << 32));
+        uint32_t cd;
+        do {
+          cd = sload32(ecode + i);
+          const T pv = sload64(evals + i) * xs[cd & 0xFFFF];
+          a = a + pv;
+          ++i;
+        } while (cd & kVcMore);
+        if (lw == l) acc = a;
+      }
+      if (own) ylds[row] = acc;
+    }
+  };
+
   // Each role runs its own loop with exactly one workgroup barrier per panel
   // (npu + 1 barriers in all, the same count in both), so the two register
   // rings are never live together and the allocator overlays them.
@@ -218,6 +322,28 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       if (s + 1 < npu) patch_x(s + 1);
       barrier();
     }
+  } else if (loader && LD == 2) {
+    // same ring, asm loads: storing x(s+1) waits for it with x(s+2)'s NJ
+    // loads (issued one step later) still in flight
+    u64x2 R[2][NJ];
+    load_x(0, R[0]);
+    vm_wait<0>();
+    store_x(0, R[0]);
+    load_x(1, R[1]);
+    load_x(2, R[0]);
+    barrier();
+    for (uint32_t base = 0; base < npu; base += 2) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t s = base + i;
+        if (s >= npu) break;
+        vm_wait<(AB & 1) ? 0 : NJ>();
+        if (s + 1 < npu) store_x(s + 1, R[(i + 1) & 1]);
+        load_x(s + 3, R[(i + 1) & 1]);
+        barrier();
+      }
+    }
+    vm_wait<0>();
   } else if (loader) {
     u64x2 R[2][NJ];  // R[(s+1)&1] holds x(s+1) during step s
     load_x(0, R[0]);
@@ -246,11 +372,16 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       for (int i = 0; i < DE; ++i) {
         const uint32_t s = base + i;
         if (s >= npu) break;
-        apply(s, EC[i], EV[i]);
+        if (CX == 2) vm_wait<(AB & 4) ? 0 : (DE - 1) * 2 * EPT>();  // slot i landed, DE-1 steps still in flight
+        if (CX)
+          apply_cx(s, EC[i], EV[i]);
+        else
+          apply(s, EC[i], EV[i]);
         load_e(s + DE, EC[i], EV[i]);
         barrier();
       }
     }
+    if (CX == 2) vm_wait<0>();  // the clamped prefetches past the last panel
   }
   if (SPLIT == 1) {
     for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
@@ -300,12 +431,23 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   }
 }
 
-template <typename T, int SPLIT, int LD>
+template <typename T, int SPLIT, int LD, int CX = 0>
 static void launch_one(const VcacheArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_vcache<T, SPLIT, VcCfg<SPLIT>::WL, VcCfg<SPLIT>::DE, VcCfg<SPLIT>::EPT, 0, 0, false, LD>),
+  hipLaunchKernelGGL((k_vcache<T, SPLIT, VcCfg<SPLIT>::WL, VcCfg<SPLIT>::DE, VcCfg<SPLIT>::EPT, 0, 0, false, LD, CX>),
                      dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s, a.seg, a.code, (const T*)a.vals,
                      (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets, a.rows, a.cols,
                      a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta);
+}
+
+template <typename T, int SPLIT>
+static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
+  if (cx == 0) {
+    ld == 1 ? launch_one<T, SPLIT, 1, 0>(a, s) : launch_one<T, SPLIT, 0, 0>(a, s);
+  } else if (cx == 1) {
+    ld == 1 ? launch_one<T, SPLIT, 1, 1>(a, s) : launch_one<T, SPLIT, 0, 1>(a, s);
+  } else {
+    ld == 1 ? launch_one<T, SPLIT, 1, 2>(a, s) : launch_one<T, SPLIT, 2, 2>(a, s);
+  }
 }
 
 template <typename T>
@@ -318,12 +460,22 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
       (uint64_t)a.part_panels * (a.split - 1) >= a.npanels ||
       (uint64_t)a.npanels * g.panel < a.cols || a.npad + 1 > (uint32_t)kVcSegMax)
     return hipErrorInvalidValue;
+  // cross-lane continuation needs every segment inside the register window
+  auto window = [](int split) {
+    const int wl = split == 1 ? VcCfg<1>::WL : split == 2 ? VcCfg<2>::WL : VcCfg<4>::WL;
+    const int ept = split == 1 ? VcCfg<1>::EPT : split == 2 ? VcCfg<2>::EPT : VcCfg<4>::EPT;
+    return (uint32_t)((kVcThreads / 64 - wl) * 64 * ept);
+  };
+  // xlane 1: cross-lane continuation; 2: also the asm rings (entries, and x
+  // unless LDS-DMA stages it) with explicit vmcnt waits
+  const int cx = a.xlane && a.max_seg <= window(a.split) ? (a.xlane >= 2 ? 2 : 1) : 0;
+  const int ld = a.dma ? 1 : cx == 2 ? 2 : 0;
   if (a.split == 1)
-    a.dma ? launch_one<T, 1, 1>(a, s) : launch_one<T, 1, 0>(a, s);
+    dispatch<T, 1>(a, s, ld, cx);
   else if (a.split == 2)
-    a.dma ? launch_one<T, 2, 1>(a, s) : launch_one<T, 2, 0>(a, s);
+    dispatch<T, 2>(a, s, ld, cx);
   else
-    a.dma ? launch_one<T, 4, 1>(a, s) : launch_one<T, 4, 0>(a, s);
+    dispatch<T, 4>(a, s, ld, cx);
   return hipGetLastError();
 }
 

@@ -59,6 +59,7 @@ struct Cfg {
   int VR, VP, WL, DE, EPT, SPLIT;
   int LD = 0;  // 0: register-staged x loader, 1: LDS-DMA loader, 2: k_wgather (x gathered from global)
   int CB = 16; // column bits of the entry code
+  int CX = 0;   // 1/2: cross-lane run continuation (needs every segment in the register window)
 };
 
 static double madd(double acc, double a, double b) {
@@ -175,6 +176,54 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
       CHECK(beg <= end, "segment %u [%u,%u)", s, beg, end);
       std::set<uint32_t> written;  // y rows written this step (race check)
       const uint32_t lbeg = segl[std::min(s, npad)];  // load_e(s), issued DE steps earlier
+      if (c.CX) {  // apply_cx: products by every valid lane, continuations from lanes lw+k of the wave
+        CHECK(end - beg <= (uint32_t)(c.EPT * CT), "segment %u of unit %u exceeds the register window", s, bid);
+        std::vector<uint32_t> cc((size_t)CT * c.EPT);
+        std::vector<double> pp((size_t)CT * c.EPT, 0.0);
+        for (int ct = 0; ct < CT; ++ct)
+          for (int j = 0; j < c.EPT; ++j) {
+            const uint32_t i = std::min(lbeg + ct + j * CT, last);
+            const uint32_t ei = beg + ct + j * CT;
+            cc[(size_t)j * CT + ct] = code.get(i);
+            if (ei < end) {
+              CHECK(i == ei, "prefetched entry %u != used entry %u", i, ei);
+              volatile double pr = vals.get(i) * xs_at(cc[(size_t)j * CT + ct] & CMASK);
+              pp[(size_t)j * CT + ct] = pr;
+            }
+          }
+        for (int j = 0; j < c.EPT; ++j)
+          for (int ct = 0; ct < CT; ++ct) {
+            const uint32_t ei = beg + ct + j * CT, cd0 = cc[(size_t)j * CT + ct];
+            if (!(ei < end) || (cd0 & kVcCont)) continue;
+            const uint32_t row = (cd0 >> c.CB) & RMASK;
+            CHECK(row < nr, "row_local %u >= nr %u", row, nr);
+            CHECK(!written.count(row), "race: row %u twice in step %u of unit %u", row, s, bid);
+            written.insert(row);
+            double acc = ylds[row] + pp[(size_t)j * CT + ct];
+            bool more = (cd0 & kVcMore) != 0;
+            for (uint32_t k = 1; more; ++k) {
+              if ((uint32_t)(ct & 63) + k < 64) {
+                const uint32_t nb = (uint32_t)ct + k, ni = beg + nb + j * CT, nc = cc[(size_t)j * CT + nb];
+                CHECK(nb < (uint32_t)CT && ni == ei + k && ni < end && (nc & kVcCont),
+                      "continuation lane %u: entry %u code %08x", nb, ni, nc);
+                acc = acc + pp[(size_t)j * CT + nb];
+                more = (nc & kVcMore) != 0;
+              } else {  // scalar fallback from memory
+                uint32_t i = ei + k, cd;
+                do {
+                  cd = code.get(i);
+                  CHECK(i < end && (cd & kVcCont), "fallback entry %u", i);
+                  volatile double pr = vals.get(i) * xs_at(cd & CMASK);
+                  acc = acc + pr;
+                  ++i;
+                } while (cd & kVcMore);
+                more = false;
+              }
+            }
+            ylds[row] = acc;
+          }
+        continue;
+      }
       for (int ct = 0; ct < CT; ++ct) {
         std::vector<uint32_t> cc(c.EPT);
         std::vector<double> vv(c.EPT);
@@ -362,7 +411,10 @@ int main(int argc, char** argv) {
                       {kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 1},
                       {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 1},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 1},
-                      {kWgWindow.rows, kWgWindow.panel, 0, 4, 2, 1, 2, kWgWindow.colbits}};
+                      {kWgWindow.rows, kWgWindow.panel, 0, 4, 2, 1, 2, kWgWindow.colbits},
+                      {kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 0, 16, 2},
+                      {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 0, 16, 2},
+                      {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0, 16, 2}};
   int failures = 0;
   for (auto& cs : cases) {
     std::vector<double> x(cs.A.cols), yin(cs.A.rows);
@@ -376,6 +428,10 @@ int main(int argc, char** argv) {
       }
       VcacheLayout L;
       build_vcache(cs.A, g, L);
+      if (c.CX && L.max_seg > (uint32_t)((16 - c.WL) * 64 * c.EPT)) {  // launch_vcache falls back to CX 0
+        std::printf("%-28s split=%d cx=%d: segments exceed the window, CX 0 runs\n", cs.name.c_str(), c.SPLIT, c.CX);
+        continue;
+      }
       for (int beta = 0; beta < 2; ++beta) {
         g_errors = 0;
         const auto y = simulate(cs.A, L, c, x, yin, beta);
@@ -397,9 +453,9 @@ int main(int argc, char** argv) {
         }
         const bool ok = bad == 0 && g_errors == 0;
         failures += !ok;
-        std::printf("%-28s split=%d ld=%d beta=%d units=%u panels=%u: %s (%zu rows off, %d violations)\n",
-                    cs.name.c_str(), c.SPLIT, c.LD, beta, L.nblocks * c.SPLIT, L.npanels, ok ? "ok" : "FAIL", bad,
-                    g_errors);
+        std::printf("%-28s split=%d ld=%d cx=%d beta=%d units=%u panels=%u: %s (%zu rows off, %d violations)\n",
+                    cs.name.c_str(), c.SPLIT, c.LD, c.CX, beta, L.nblocks * c.SPLIT, L.npanels, ok ? "ok" : "FAIL",
+                    bad, g_errors);
       }
     }
   }

@@ -6,7 +6,6 @@ covered by the -m gpu tests; this only guards the script itself."""
 import io
 import json
 import os
-import socket
 import sys
 import time
 from contextlib import redirect_stdout
@@ -109,17 +108,9 @@ def test_bench_json_contract_single(monkeypatch):
     assert out["secondary"]["mode"] == "ordered" and out["secondary"]["parity"] == "bit-exact vs oracle"
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def _rank_main(rank, world, port, q, extra=()):
+def _rank_main(rank, world, store_path, q, extra=()):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+                      MASTER_PORT="0")
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "spmv-vector-cache_amd"))
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -131,24 +122,33 @@ def _rank_main(rank, world, port, q, extra=()):
 
     bench = _patch(MP())
     real_init = dist.init_process_group
-    dist.init_process_group = lambda backend, device_id=None: real_init("gloo", rank=rank, world_size=world)
-    out = _run(bench, ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--log2-rows", "10",
-                       "--log2-cols", "10", "--no-cpu-baseline", *extra])
+    # file rendezvous: no TCP port to race for between consecutive tests
+    dist.init_process_group = lambda backend, device_id=None: real_init(
+        "gloo", init_method=f"file://{store_path}", rank=rank, world_size=world)
+    try:
+        out = _run(bench, ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--log2-rows", "10",
+                           "--log2-cols", "10", "--no-cpu-baseline", *extra])
+    except BaseException as e:  # report it to the parent instead of a bare exit code
+        q.put((rank, f"ERROR: {type(e).__name__}: {e}"))
+        raise
     q.put((rank, out))
 
 
 def _multi_rank(extra, world=2):
     import multiprocessing as mp
+    import tempfile
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, tuple(extra))) for r in range(world)]
+    store = os.path.join(tempfile.mkdtemp(prefix="bench_gloo_"), "store")
+    procs = [ctx.Process(target=_rank_main, args=(r, world, store, q, tuple(extra))) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-        assert p.exitcode == 0
+    errors = [v for v in res.values() if isinstance(v, str)]
+    assert not errors, errors
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     return res
 
 
@@ -179,17 +179,7 @@ def test_bench_strong_workloads_gloo(workload, scale):
 
 
 def test_bench_multi_rank_gloo():
-    import multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=240) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    res = _multi_rank([])
     assert res[1] is None  # only rank 0 prints the line
     out = res[0]
     assert out["n_gpus"] == 2 and out["x_bcast_us"] is not None

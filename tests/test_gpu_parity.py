@@ -238,9 +238,11 @@ EXPERIMENTAL = os.environ.get("HIPSPMV_EXPERIMENTAL") == "1"
 
 
 @pytest.mark.skipif(not EXPERIMENTAL, reason="experimental kernels: set HIPSPMV_EXPERIMENTAL=1")
-@pytest.mark.parametrize("kernel,dma", [("vcache_split4", 0), ("vcache_split4", 1), ("vcache_split", 1),
-                                        ("vcache", 1), ("wgather", 0)])
-def test_experimental_vcache_variants(gpu, kernel, dma):
+@pytest.mark.parametrize("kernel,dma,xlane", [("vcache_split4", 0, 0), ("vcache_split4", 1, 0), ("vcache_split", 1, 0),
+                                              ("vcache", 1, 0), ("wgather", 0, 0), ("vcache", 0, 1),
+                                              ("vcache", 0, 2), ("vcache_split", 0, 1), ("vcache_split", 0, 2),
+                                              ("vcache_split", 1, 2), ("vcache_split4", 0, 2)])
+def test_experimental_vcache_variants(gpu, kernel, dma, xlane):
     cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20), (20000, 1 << 22)]
     for rows, cols in cases:
         rng = np.random.default_rng(rows)
@@ -260,6 +262,7 @@ def test_experimental_vcache_variants(gpu, kernel, dma):
             continue
         h.set_kernel(kernel)
         h.set_option("vcache_dma", dma)
+        h.set_option("vcache_xlane", xlane)
         mode = hs.MODE_ORDERED if kernel in ("vcache", "wgather") else hs.MODE_FAST
         colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
         for beta in (0, 1):
