@@ -32,16 +32,39 @@ x = torch.from_numpy(hs.gen_vector(cols, 3)).cuda()
 y = torch.empty(rows, dtype=torch.float64, device="cuda")
 alg = h.stat("alg_bytes")
 s = torch.cuda.current_stream()
-cands = [("vcache", hs.MODE_ORDERED), ("csr_lane", hs.MODE_ORDERED), ("vcache_split", hs.MODE_FAST),
-         ("csr_vector", hs.MODE_FAST)]
-res = {}
+O, F = hs.MODE_ORDERED, hs.MODE_FAST
+# (label, kernel, mode, options); the experimental ones need HIPSPMV_EXPERIMENTAL=1 at create
+cands = [("vcache", "vcache", O, {}), ("csr_lane", "csr_lane", O, {}), ("vcache_split", "vcache_split", F, {}),
+         ("csr_vector", "csr_vector", F, {})]
+if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
+    cands += [("vcache xl1", "vcache", O, {"vcache_xlane": 1}), ("vcache xl2", "vcache", O, {"vcache_xlane": 2}),
+              ("vcache dma", "vcache", O, {"vcache_dma": 1}),
+              ("vcache dma xl2", "vcache", O, {"vcache_dma": 1, "vcache_xlane": 2}),
+              ("split xl1", "vcache_split", F, {"vcache_xlane": 1}), ("split xl2", "vcache_split", F, {"vcache_xlane": 2}),
+              ("split dma", "vcache_split", F, {"vcache_dma": 1}),
+              ("split dma xl2", "vcache_split", F, {"vcache_dma": 1, "vcache_xlane": 2}),
+              ("split4", "vcache_split4", F, {}), ("split4 xl2", "vcache_split4", F, {"vcache_xlane": 2}),
+              ("split4 dma xl2", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 2}),
+              ("wgather", "wgather", O, {})]
+ref = None
+res, check = {}, {}
 for rnd in range(a.rounds):  # interleaved rounds in one process (methodology rule 24)
-    for kname, mode in cands:
+    for label, kname, mode, opts in cands:
         try:
             h.set_kernel(kname)
+            for k in ("vcache_dma", "vcache_xlane"):
+                h.set_option(k, opts.get(k, 0))
             h.exec_device(x, y, beta=0, mode=mode, stream=s)
         except hs.HipSpMVError:
             continue
+        if rnd == 0:  # correctness vs the first ordered result: bits (ordered) or relative size (fast)
+            torch.cuda.synchronize()
+            yy = y.cpu().numpy().copy()
+            if ref is None and mode == O:
+                ref = yy
+            if ref is not None:
+                check[label] = ("bit-exact" if yy.tobytes() == ref.tobytes() else
+                                f"max|d|={float(np.max(np.abs(yy - ref))):.2e}")
         for _ in range(3):
             h.exec_device(x, y, beta=0, mode=mode, stream=s)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -50,9 +73,9 @@ for rnd in range(a.rounds):  # interleaved rounds in one process (methodology ru
             h.exec_device(x, y, beta=0, mode=mode, stream=s)
         e1.record(s)
         torch.cuda.synchronize()
-        res.setdefault(kname, []).append(e0.elapsed_time(e1) / a.reps * 1e3)
+        res.setdefault(label, []).append(e0.elapsed_time(e1) / a.reps * 1e3)
 print(f"{name}: nnz={colind.size} alg_bytes={alg}")
-for kname, ts in res.items():
+for label, ts in res.items():
     us = float(np.median(ts))
-    print(f"  {kname:14s} {us:9.2f} us  {alg / us / 1e3:8.1f} GB/s  {2 * colind.size / us / 1e3:8.1f} GFLOP/s"
-          f"  frac8TB={alg / us / 1e3 / 8000:.3f}  (rounds: {', '.join(f'{t:.1f}' for t in ts)})")
+    print(f"  {label:16s} {us:9.2f} us  {alg / us / 1e3:8.1f} GB/s  {2 * colind.size / us / 1e3:8.1f} GFLOP/s"
+          f"  frac8TB={alg / us / 1e3 / 8000:.3f}  {check.get(label, '')}  (rounds: {', '.join(f'{t:.1f}' for t in ts)})")
