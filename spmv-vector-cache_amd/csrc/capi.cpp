@@ -245,7 +245,8 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     const auto& v = h->vc[3];
     VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    nullptr,
                  nullptr,     h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
-                 v.npad,      h->nnz - 1, 1,         beta, 0,       (uint32_t)kWgWindow.panel};
+                 v.npad,      h->nnz - 1, 1,         beta, 0,       (uint32_t)kWgWindow.panel,
+                 h->vcache_xlane, v.max_seg};
     e = launch_wgather(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};

@@ -46,36 +46,6 @@ struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane
   static constexpr int VR = kVcSplit4.rows, VP = kVcSplit4.panel, WL = 2, DE = 4, EPT = 2;
 };
 
-// Loads the compiler's waitcnt pass does not see (CX == 2 / LD == 2 rings):
-// hipcc (ROCm 7.2) merges the pending-load state pessimistically at a loop
-// header and emits s_waitcnt vmcnt(0) there -- draining a DE-deep register
-// ring once per unrolled group (tools probe: a 4-slot ring gets vmcnt(0) at
-// the header and vmcnt(3) elsewhere).  Loads issued by inline asm are
-// invisible to that pass; the kernel then waits with explicit, exact counts
-// (vmcnt is in order for loads on gfx9).  Only the ring's own loads may be in
-// flight between a load and its wait for the counts to hold.
-__device__ __forceinline__ uint32_t ald_u32(const uint32_t* p) {
-  uint32_t r;
-  asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p) : "memory");
-  return r;
-}
-template <typename T>
-__device__ __forceinline__ T ald_64(const T* p) {
-  uint64_t r;
-  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
-  return __builtin_bit_cast(T, r);
-}
-__device__ __forceinline__ u64x2 ald_128(const void* p) {
-  u64x2 r;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
-  return r;
-}
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt field");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 // AB: ablation mask for the diagnostic build (tools/vc_ablate.hip); the
 // product instantiates AB = 0 and every hook folds away.  Bits: 1 no x loads,
 // 2 no x LDS stores, 4 no entry loads, 8 no compute, 16 x always from panel 0,

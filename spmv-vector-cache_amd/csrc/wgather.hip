@@ -100,11 +100,148 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
   for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
 }
 
+// Pipelined form (option vcache_xlane 2; every segment must fit the register
+// window, EPT*1024 entries): the entry ring and the x gathers are inline-asm
+// loads with exact vmcnt waits (device_common.h), so nothing drains the ring:
+// step s issues the gathers of step s+1 (their codes landed DE-1 steps
+// earlier) and then the entries of step s+DE, and consumes the gathers issued
+// one step before.  Per step, in issue order: G(s+1) [EPT], E(s+DE) [2 EPT].
+//   wait E(s+1): younger = steps s+2-DE .. s-1 = (DE-2) * 3 EPT
+//   wait G(s)  : younger = E(s-1+DE) + G(s+1) = 3 EPT   (s == 0: G(1) only, EPT)
+// Run continuations come from the next lanes of the wave (products formed by
+// every lane), or, past the wave, from scalar loads (lgkmcnt).
+template <typename T, int CB, int DE, int EPT>
+__global__ __launch_bounds__(kVcThreads) void k_wgather_pipe(const uint32_t* __restrict__ seg,
+                                                              const uint32_t* __restrict__ ecode,
+                                                              const T* __restrict__ evals, const T* __restrict__ x,
+                                                              const T* __restrict__ y_in, T* __restrict__ y_out,
+                                                              uint32_t rows, uint32_t rows_per_block,
+                                                              uint32_t npanels, uint32_t npad, uint32_t last,
+                                                              int beta) {
+#pragma clang fp contract(off)
+  constexpr int VT = kVcThreads;
+  constexpr uint32_t W = 1u << CB, CMASK = W - 1, RMASK = (1u << (30 - CB)) - 1;
+  constexpr int VR = 1 << (30 - CB);
+  static_assert(DE >= 2 && DE % 2 == 0, "ring depth: even, the gather buffer alternates");
+  __shared__ T ylds[VR];
+  __shared__ uint32_t segl[kVcSegMax];
+  const int t = threadIdx.x;
+  const uint32_t lw = t & 63;
+  const uint32_t b = blockIdx.x;
+  const uint32_t r0 = b * rows_per_block;
+  const uint32_t nr = min(rows_per_block, rows - r0);
+  const uint32_t* sp = seg + (size_t)b * (npad + 1);
+  if ((uint32_t)t <= npad) segl[t] = sp[t];
+  for (uint32_t i = t; i < nr; i += VT) ylds[i] = beta ? y_in[r0 + i] : T(0);
+  __syncthreads();
+
+  auto load_e = [&](uint32_t s, uint32_t* c, T* v) {  // 2*EPT loads, always issued
+    const uint32_t beg = segl[min(s, npad)];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const uint32_t i = min(beg + t + j * VT, last);
+      c[j] = ald_u32(ecode + i);
+      v[j] = ald_64(evals + i);
+    }
+  };
+  auto gather = [&](uint32_t s, const uint32_t* c, T* g) {  // EPT loads, always issued (x[0] when idle)
+    const uint32_t beg = segl[min(s, npad)], end = segl[min(s + 1, npad)];
+    const T* xs = x + (size_t)min(s, npanels - 1) * W;
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const bool ok = s < npanels && beg + t + j * VT < end;
+      g[j] = ald_64(ok ? xs + (c[j] & CMASK) : x);
+    }
+  };
+  auto apply = [&](uint32_t s, const uint32_t* c, const T* v, const T* g) {
+    const T* xs = x + (size_t)s * W;
+    const uint32_t beg = segl[s], end = segl[s + 1];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const uint32_t q = beg + t + j * VT;
+      const uint32_t code = c[j];
+      const bool valid = q < end;
+      const T p = valid ? v[j] * g[j] : T(0);
+      const bool own = valid && !(code & kVcCont);
+      const uint32_t row = (code >> CB) & RMASK;
+      T acc = own ? ylds[row] + p : T(0);
+      bool more = own && (code & kVcMore);
+      bool fb = false;
+      uint32_t fbi = 0;
+      for (uint32_t k = 1; __builtin_amdgcn_ballot_w64(more) != 0; ++k) {
+        const T pk = __shfl_down(p, k);
+        const uint32_t ck = __shfl_down(code, k);
+        if (more) {
+          if (lw + k < 64) {
+            acc = acc + pk;
+            more = (ck & kVcMore) != 0;
+          } else {
+            fb = true;
+            fbi = q + k;
+            more = false;
+          }
+        }
+      }
+      for (uint64_t m = __builtin_amdgcn_ballot_w64(fb); m; m &= m - 1) {  // rare
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        uint32_t i = __builtin_amdgcn_readlane(fbi, l);
+        const uint64_t ab = __builtin_bit_cast(uint64_t, acc);
+        T a = __builtin_bit_cast(T, (uint64_t)__builtin_amdgcn_readlane((uint32_t)ab, l) |
+                                        ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ab >> 32), l) << 32));
+        uint32_t cd;
+        do {
+          cd = sld_32(ecode + i);
+          const T pv = __builtin_bit_cast(T, sld_64(evals + i)) * __builtin_bit_cast(T, sld_64(xs + (cd & CMASK)));
+          a = a + pv;
+          ++i;
+        } while (cd & kVcMore);
+        if (lw == l) acc = a;
+      }
+      if (own) ylds[row] = acc;
+    }
+  };
+
+  uint32_t EC[DE][EPT];
+  T EV[DE][EPT];
+  T G[2][EPT];
+#pragma unroll
+  for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i]);
+  vm_wait<0>();
+  gather(0, EC[0], G[0]);
+  for (uint32_t base = 0; base < npanels; base += DE) {
+#pragma unroll
+    for (int i = 0; i < DE; ++i) {
+      const uint32_t s = base + i;
+      if (s >= npanels) break;
+      vm_wait<(DE - 2) * 3 * EPT>();  // E(s+1) landed
+      gather(s + 1, EC[(i + 1) % DE], G[(i + 1) & 1]);
+      if (s == 0)
+        vm_wait<EPT>();  // G(0): only G(1) is younger
+      else
+        vm_wait<3 * EPT>();  // G(s) landed
+      apply(s, EC[i], EV[i], G[i & 1]);
+      load_e(s + DE, EC[i], EV[i]);
+      __syncthreads();  // window s's y updates before window s+1's
+    }
+  }
+  vm_wait<0>();
+  for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
+}
+
 template <typename T>
 static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_wgather<T, 17, 4, 2>), dim3(a.nblocks), dim3(kVcThreads), 0, s, a.seg, a.code,
-                     (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
-                     a.npanels, a.npad, a.last, a.beta);
+  if (a.xlane >= 2 && a.max_seg <= 2u * kVcThreads)
+    hipLaunchKernelGGL((k_wgather_pipe<T, 17, 4, 2>), dim3(a.nblocks), dim3(kVcThreads), 0, s, a.seg, a.code,
+                       (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
+                       a.npanels, a.npad, a.last, a.beta);
+  else if (a.xlane >= 2 && a.max_seg <= 4u * kVcThreads)
+    hipLaunchKernelGGL((k_wgather_pipe<T, 17, 4, 4>), dim3(a.nblocks), dim3(kVcThreads), 0, s, a.seg, a.code,
+                       (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
+                       a.npanels, a.npad, a.last, a.beta);
+  else
+    hipLaunchKernelGGL((k_wgather<T, 17, 4, 2>), dim3(a.nblocks), dim3(kVcThreads), 0, s, a.seg, a.code,
+                       (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
+                       a.npanels, a.npad, a.last, a.beta);
   return hipGetLastError();
 }
 

@@ -45,7 +45,7 @@ if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
               ("split dma xl2", "vcache_split", F, {"vcache_dma": 1, "vcache_xlane": 2}),
               ("split4", "vcache_split4", F, {}), ("split4 xl2", "vcache_split4", F, {"vcache_xlane": 2}),
               ("split4 dma xl2", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 2}),
-              ("wgather", "wgather", O, {})]
+              ("wgather", "wgather", O, {}), ("wgather xl2", "wgather", O, {"vcache_xlane": 2})]
 ref = None
 res, check = {}, {}
 for rnd in range(a.rounds):  # interleaved rounds in one process (methodology rule 24)

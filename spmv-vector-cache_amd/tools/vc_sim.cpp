@@ -414,7 +414,8 @@ int main(int argc, char** argv) {
                       {kWgWindow.rows, kWgWindow.panel, 0, 4, 2, 1, 2, kWgWindow.colbits},
                       {kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 0, 16, 2},
                       {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 0, 16, 2},
-                      {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0, 16, 2}};
+                      {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0, 16, 2},
+                      {kWgWindow.rows, kWgWindow.panel, 0, 4, 4, 1, 2, kWgWindow.colbits, 2}};
   int failures = 0;
   for (auto& cs : cases) {
     std::vector<double> x(cs.A.cols), yin(cs.A.rows);
