@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true", help="skip timing the other mode")
+    p.add_argument("--vcache-xlane", type=int, default=0, choices=[0, 1, 2],
+                   help="experimental vcache option (include/hipspmv.h); not the default path")
+    p.add_argument("--vcache-dma", type=int, default=0, choices=[0, 1], help="experimental LDS-DMA x loader")
     p.add_argument("--traffic-csv", default=None,
                    help="rocprofv3 --pmc counter CSV (FETCH_SIZE, WRITE_SIZE) of this workload, for roofline.traffic")
     return p.parse_args()
@@ -145,6 +148,9 @@ def main():
     h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols, device=local)
     if a.kernel != "auto":
         h.set_kernel(a.kernel)
+    if a.vcache_xlane or a.vcache_dma:
+        h.set_option("vcache_xlane", a.vcache_xlane)
+        h.set_option("vcache_dma", a.vcache_dma)
     setup_s = time.perf_counter() - t0
     nnz = int(colind.size)
 
@@ -277,7 +283,9 @@ def main():
             "config": {"workload": workload,
                        "rows_per_gpu": rows, "cols": cols, "nnz_per_gpu": nnz,
                        "nnz_total": int(nnz_t.item()), "kernel": kname,
-                       "mode": a.mode, "parallelism": f"row-partition x{world}, x broadcast (RCCL) before timing"},
+                       "mode": a.mode, "parallelism": f"row-partition x{world}, x broadcast (RCCL) before timing",
+                       **({"vcache_xlane": a.vcache_xlane, "vcache_dma": a.vcache_dma}
+                          if a.vcache_xlane or a.vcache_dma else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic),

@@ -34,6 +34,10 @@ class FakeHandle:
     def set_kernel(self, k):
         self.kernel = k
 
+    def set_option(self, key, value):
+        self.opts = getattr(self, "opts", {})
+        self.opts[key] = value
+
     def kernel_name(self, mode):
         return "vcache_split" if mode == hs.MODE_FAST else "vcache"
 
