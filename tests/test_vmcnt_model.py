@@ -1,0 +1,123 @@
+"""Issue-order model of the explicit vmcnt waits in the asm-loaded rings
+(csrc/vcache.hip CX == 2 / LD == 2, csrc/wgather.hip k_wgather_pipe).
+
+On gfx9 vector-memory loads retire in issue order, so `s_waitcnt vmcnt(N)`
+guarantees every load except the N youngest has landed.  Each model below
+replays one wave's sequence of loads and waits exactly as the kernel issues
+them (prologue, the DE-unrolled steps, the early exit) and checks that every
+register-ring value is consumed only after a wait that retired its load --
+and that no wait is stronger than necessary would not be a correctness issue,
+so only the safety direction is asserted.  Test infrastructure, CPU only."""
+import pytest
+
+
+class Wave:
+    def __init__(self):
+        self.issued = []  # load ids in issue order
+        self.landed = set()
+
+    def load(self, tag):
+        self.issued.append(tag)
+
+    def wait(self, n):  # vmcnt(n): all but the n youngest have landed
+        pending = [t for t in self.issued if t not in self.landed]
+        for t in pending[:max(0, len(pending) - n)]:
+            self.landed.add(t)
+
+    def use(self, tag):
+        assert tag in self.landed, f"{tag} consumed before its load retired"
+
+
+def vcache_compute_ring(npu, DE, EPT):
+    """k_vcache compute role, CX == 2: load_e(s) issues 2*EPT loads; step s
+    waits vmcnt((DE-1)*2*EPT), consumes slot s, issues load_e(s+DE)."""
+    w = Wave()
+    for s in range(DE):
+        for j in range(2 * EPT):
+            w.load(("e", s, j))
+    for s in range(npu):
+        w.wait((DE - 1) * 2 * EPT)
+        for j in range(2 * EPT):
+            w.use(("e", s, j))
+        for j in range(2 * EPT):
+            w.load(("e", s + DE, j))
+    w.wait(0)
+
+
+def vcache_loader_ring(npu, NJ):
+    """k_vcache loader role, LD == 2: load x0, wait 0, store x0, load x1, x2;
+    step s waits vmcnt(NJ), stores x(s+1), loads x(s+3)."""
+    w = Wave()
+    for j in range(NJ):
+        w.load(("x", 0, j))
+    w.wait(0)
+    for j in range(NJ):
+        w.use(("x", 0, j))
+    for p in (1, 2):
+        for j in range(NJ):
+            w.load(("x", p, j))
+    for s in range(npu):
+        w.wait(NJ)
+        if s + 1 < npu:
+            for j in range(NJ):
+                w.use(("x", s + 1, j))
+        for j in range(NJ):
+            w.load(("x", s + 3, j))
+    w.wait(0)
+
+
+def wgather_pipe(npanels, DE, EPT):
+    """k_wgather_pipe: E(0..DE-1), wait 0, G(0); step s: wait (DE-2)*3*EPT,
+    G(s+1) [needs E(s+1)], wait EPT (s == 0) or 3*EPT, consume E(s), G(s),
+    issue E(s+DE)."""
+    w = Wave()
+    for s in range(DE):
+        for j in range(2 * EPT):
+            w.load(("e", s, j))
+    w.wait(0)
+    for j in range(2 * EPT):
+        w.use(("e", 0, j))  # gather(0) reads the codes of step 0
+    for j in range(EPT):
+        w.load(("g", 0, j))
+    for s in range(npanels):
+        w.wait((DE - 2) * 3 * EPT)
+        for j in range(2 * EPT):
+            w.use(("e", s + 1, j))  # gather(s+1) reads the codes of step s+1
+        for j in range(EPT):
+            w.load(("g", s + 1, j))
+        w.wait(EPT if s == 0 else 3 * EPT)
+        for j in range(EPT):
+            w.use(("g", s, j))
+        for j in range(2 * EPT):
+            w.use(("e", s, j))
+        for j in range(2 * EPT):
+            w.load(("e", s + DE, j))
+    w.wait(0)
+
+
+@pytest.mark.parametrize("npu", [1, 2, 3, 4, 5, 7, 8, 87, 133])
+@pytest.mark.parametrize("DE,EPT", [(4, 3), (4, 2), (2, 3), (6, 2)])
+def test_vcache_compute_ring_waits(npu, DE, EPT):
+    vcache_compute_ring(npu, DE, EPT)
+
+
+@pytest.mark.parametrize("npu", [1, 2, 3, 4, 87, 130])
+@pytest.mark.parametrize("NJ", [8, 4, 1])
+def test_vcache_loader_ring_waits(npu, NJ):
+    vcache_loader_ring(npu, NJ)
+
+
+@pytest.mark.parametrize("npanels", [1, 2, 3, 4, 5, 8, 128])
+@pytest.mark.parametrize("DE,EPT", [(4, 2), (4, 4), (2, 2), (6, 3)])
+def test_wgather_pipe_waits(npanels, DE, EPT):
+    wgather_pipe(npanels, DE, EPT)
+
+
+def test_model_catches_a_short_wait():
+    # the model must reject a wait that leaves the consumed load in flight
+    w = Wave()
+    w.load("a")
+    w.load("b")
+    w.wait(2)
+    with pytest.raises(AssertionError):
+        w.use("a")
