@@ -307,7 +307,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       for (int i = 0; i < 2; ++i) {
         const uint32_t s = base + i;
         if (s >= npu) break;
-        vm_wait<(AB & 1) ? 0 : NJ>();
+        vm_wait<((AB & 1) || LD != 2) ? 0 : NJ>();  // (branch only live for LD == 2)
         if (s + 1 < npu) store_x(s + 1, R[(i + 1) & 1]);
         load_x(s + 3, R[(i + 1) & 1]);
         barrier();

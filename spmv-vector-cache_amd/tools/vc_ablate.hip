@@ -79,10 +79,15 @@ int main(int argc, char** argv) {
                 L.nblocks * g.split, L.npad, L.max_seg);
     // kern must be compiled for this geometry (the round-1 fault was a split=1
     // kernel launched on the split layout's grid): SPLIT is checked here
-    auto variant = [&](auto kern, int kernel_split, const char* nm, int mask) {
+    // window: entries a CX variant holds in registers per step (0: no limit)
+    auto variant = [&](auto kern, int kernel_split, const char* nm, int mask, uint32_t window = 0) {
       if (kernel_split != g.split || L.rows_per_block > (uint32_t)g.rows ||
           (uint64_t)L.part_panels * (g.split - 1) >= L.npanels) {
         std::printf("  %-30s SKIPPED: kernel split %d vs layout split %d\n", nm, kernel_split, g.split);
+        return;
+      }
+      if (window && L.max_seg > window) {
+        std::printf("  %-30s SKIPPED: max segment %u > register window %u\n", nm, L.max_seg, window);
         return;
       }
       const double us = timeit([&] {
@@ -102,9 +107,15 @@ int main(int argc, char** argv) {
       }
       std::printf("\n");
     };
-    // template: <T, SPLIT, WL, DE, EPT, AB, MAP, NT, LD>
+    // template: <T, SPLIT, WL, DE, EPT, AB, MAP, NT, LD, CX>
     if (g.split == 1) {
       variant(k_vcache<double, 1>, 1, "default (WL8 DE4 EPT3)", 0);
+      variant(k_vcache<double, 1, 8, 4, 3, 0, 0, false, 0, 1>, 1, "xlane1", 0, 8 * 64 * 3);
+      variant(k_vcache<double, 1, 8, 4, 3, 0, 0, false, 2, 2>, 1, "xlane2 (asm rings)", 0, 8 * 64 * 3);
+      variant(k_vcache<double, 1, 8, 6, 3, 0, 0, false, 2, 2>, 1, "xlane2 DE6", 0, 8 * 64 * 3);
+      variant(k_vcache<double, 1, 4, 4, 2, 0, 0, false, 2, 2>, 1, "xlane2 WL4 EPT2", 0, 12 * 64 * 2);
+      variant(k_vcache<double, 1, 8, 4, 3, 12, 0, false, 2, 2>, 1, "xlane2 no entries/compute", 12, 8 * 64 * 3);
+      variant(k_vcache<double, 1, 8, 4, 3, 3, 0, false, 2, 2>, 1, "xlane2 no x", 3, 8 * 64 * 3);
       variant(k_vcache<double, 1, 2, 4, 3, 0, 0, false, 1>, 1, "DMA WL2 DE4 EPT3", 0);
       variant(k_vcache<double, 1, 1, 4, 3, 0, 0, false, 1>, 1, "DMA WL1 DE4 EPT3", 0);
       variant(k_vcache<double, 1, 2, 4, 2, 0, 0, false, 1>, 1, "DMA WL2 DE4 EPT2", 0);
@@ -113,6 +124,13 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 1, 8, 4, 3, 15>, 1, "skeleton", 15);
     } else if (g.split == 2) {
       variant(k_vcache<double, 2>, 2, "default (WL6 DE4 EPT3)", 0);
+      variant(k_vcache<double, 2, 6, 4, 3, 0, 0, false, 0, 1>, 2, "xlane1", 0, 10 * 64 * 3);
+      variant(k_vcache<double, 2, 6, 4, 3, 0, 0, false, 2, 2>, 2, "xlane2 (asm rings)", 0, 10 * 64 * 3);
+      variant(k_vcache<double, 2, 6, 6, 3, 0, 0, false, 2, 2>, 2, "xlane2 DE6", 0, 10 * 64 * 3);
+      variant(k_vcache<double, 2, 4, 4, 3, 0, 0, false, 2, 2>, 2, "xlane2 WL4", 0, 12 * 64 * 3);
+      variant(k_vcache<double, 2, 2, 4, 3, 0, 0, false, 1, 2>, 2, "xlane2 DMA WL2", 0, 14 * 64 * 3);
+      variant(k_vcache<double, 2, 6, 4, 3, 12, 0, false, 2, 2>, 2, "xlane2 no entries/compute", 12, 10 * 64 * 3);
+      variant(k_vcache<double, 2, 6, 4, 3, 3, 0, false, 2, 2>, 2, "xlane2 no x", 3, 10 * 64 * 3);
       variant(k_vcache<double, 2, 2, 4, 3, 0, 0, false, 1>, 2, "DMA WL2 DE4 EPT3", 0);
       variant(k_vcache<double, 2, 1, 4, 3, 0, 0, false, 1>, 2, "DMA WL1 DE4 EPT3", 0);
       variant(k_vcache<double, 2, 2, 4, 2, 0, 0, false, 1>, 2, "DMA WL2 DE4 EPT2", 0);
@@ -124,6 +142,9 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 2, 2, 4, 3, 12, 0, false, 1>, 2, "DMA no entries/compute", 12);
     } else {
       variant(k_vcache<double, 4>, 4, "default (WL2 DE4 EPT2)", 0);
+      variant(k_vcache<double, 4, 2, 4, 2, 0, 0, false, 2, 2>, 4, "xlane2 (asm rings)", 0, 14 * 64 * 2);
+      variant(k_vcache<double, 4, 2, 6, 2, 0, 0, false, 2, 2>, 4, "xlane2 DE6", 0, 14 * 64 * 2);
+      variant(k_vcache<double, 4, 1, 4, 2, 0, 0, false, 1, 2>, 4, "xlane2 DMA WL1", 0, 15 * 64 * 2);
       variant(k_vcache<double, 4, 4, 4, 2>, 4, "WL4 DE4 EPT2", 0);
       variant(k_vcache<double, 4, 2, 6, 2>, 4, "WL2 DE6 EPT2", 0);
       variant(k_vcache<double, 4, 2, 4, 3>, 4, "WL2 DE4 EPT3", 0);
