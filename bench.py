@@ -22,7 +22,8 @@ the oracle -- and the bit-exact ORDERED mode is timed beside it ("ordered").
 Also reported: the dominant kernel's roofline (algorithmic bytes per launch /
 its average duration from HIP events on the launch stream, against 8 TB/s),
 and the CPU baseline (the oracle's SoftwareSpMV restatement, 1 core, on the
-same shard) on rank 0 at N=1.
+same shard) on rank 0 at N=1, with a row-parallel CSR run on the box's CPU
+share beside it (cpu_baseline_all_cores; reported, not a target).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode fast|ordered] [--workload c3|c4|c5]
                   [--kernel auto|vcache|vcache_split|csr_lane|csr_vector]
@@ -235,6 +236,7 @@ def main():
 
     # parity on rank 0 at N=1: the timed kernels' outputs vs the oracle (checker only)
     cpu = None
+    cpu_mt = None
     parity = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -254,6 +256,16 @@ def main():
                "sample": f"oracle SoftwareSpMV (CSC scatter) on {what}: {srows} rows, {snnz} nnz, "
                          f"x=U[-1,1), {reps + 1} execs, {t_avg * 1e3:.1f} ms each",
                "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+        # second, reported-only baseline: row-parallel CSR on the box's CPU share
+        nth = int(os.environ.get("SPMV_THREADS") or os.environ.get("OMP_NUM_THREADS") or
+                  min(16, len(os.sched_getaffinity(0))))
+        t_mt1, y_mt = oracle.time_spmv_csr_f64_mt(s_rowptr, s_colind, s_vals, x, 1, nth)
+        reps_mt = max(1, int(a.cpu_seconds / 2 / max(t_mt1, 1e-6)))
+        t_mt, _ = oracle.time_spmv_csr_f64_mt(s_rowptr, s_colind, s_vals, x, reps_mt, nth)
+        cpu_mt = {"value": round(2.0 * snnz / t_mt / 1e9, 4), "unit": "GFLOP/s", "cores": nth, "kind": "port",
+                  "sample": f"row-parallel CSR (pthreads, nnz-balanced rows) on the same {srows} rows, "
+                            f"{reps_mt + 1} execs, {t_mt * 1e3:.2f} ms each",
+                  "bit_exact_vs_softwarespmv": bool(y_mt.tobytes() == y_ref.tobytes())}
         # FAST bound per row (include/hipspmv.h): |y - y_ref| <= 2*len*2^-53*sum_j|a_ij x_j|
         lens = np.diff(s_rowptr.astype(np.int64))
         row_of = np.repeat(np.arange(srows), lens)
@@ -292,6 +304,7 @@ def main():
                          "kernel": "k_" + kname, "alg_bytes_per_launch": alg_bytes,
                          "kernel_us": round(kern_ms * 1e3, 3)},
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_mt,
             "parity": parity,
             "secondary": secondary,
             "x_bcast_us": None if bcast_us is None else round(bcast_us, 2),

@@ -10,6 +10,7 @@
 #include "oracle.h"
 
 #include <stdlib.h>
+#include <pthread.h>
 #include <string.h>
 #include <time.h>
 
@@ -113,6 +114,58 @@ double oracle_time_spmv_csc_f64(uint32_t rows, uint32_t cols, const uint32_t *co
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     oracle_spmv_csc_f64(cols, colptr, rowind, vals, x, y);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    total += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+  }
+  return reps > 0 ? total / reps : 0.0;
+}
+
+/* Second CPU baseline ("optionally, an OpenMP CSR
+ * row-parallel CPU run on all cores"): rows split into nthreads contiguous
+ * nnz-balanced ranges, one pthread each, every row summed sequentially in its
+ * CSR order -- for column-sorted CSR the same order, hence the same bits, as
+ * SoftwareSpMV's column scatter.  Returns the mean seconds per exec. */
+typedef struct {
+  const uint32_t *rowptr, *colind;
+  const double *vals, *x;
+  double *y;
+  uint32_t r0, r1;
+} csr_job_t;
+
+static void *csr_rows(void *arg) {
+  const csr_job_t *j = (const csr_job_t *)arg;
+  for (uint32_t r = j->r0; r < j->r1; r++) {
+    double acc = 0.0;
+    for (uint32_t e = j->rowptr[r]; e < j->rowptr[r + 1]; e++) {
+      const double p = j->vals[e] * j->x[j->colind[e]];
+      acc = acc + p;
+    }
+    j->y[r] = acc;
+  }
+  return NULL;
+}
+
+double oracle_time_spmv_csr_f64_mt(uint32_t rows, const uint32_t *rowptr, const uint32_t *colind,
+                                   const double *vals, const double *x, double *y, int reps, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  csr_job_t jobs[256];
+  pthread_t th[256];
+  const uint64_t nnz = rowptr[rows];
+  uint32_t r = 0;
+  for (int t = 0; t < nthreads; t++) {
+    const uint64_t target = nnz * (uint64_t)(t + 1) / (uint64_t)nthreads;
+    const uint32_t r0 = r;
+    while (r < rows && (t == nthreads - 1 || rowptr[r + 1] <= target)) r++;
+    jobs[t] = (csr_job_t){rowptr, colind, vals, x, y, r0, t == nthreads - 1 ? rows : r};
+  }
+  double total = 0.0;
+  for (int k = 0; k < reps; k++) {
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, csr_rows, &jobs[t]);
+    csr_rows(&jobs[0]);
+    for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     total += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
   }

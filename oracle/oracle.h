@@ -64,4 +64,9 @@ double oracle_time_spmv_csc_f64(uint32_t rows, uint32_t cols, const uint32_t *co
 #ifdef __cplusplus
 }
 #endif
+/* Row-parallel CSR SpMV on nthreads pthreads (second CPU baseline, bench.py);
+ * same bits as oracle_spmv_csc_f64 for column-sorted CSR.  Mean s/exec. */
+double oracle_time_spmv_csr_f64_mt(uint32_t rows, const uint32_t *rowptr, const uint32_t *colind,
+                                   const double *vals, const double *x, double *y, int reps, int nthreads);
+
 #endif

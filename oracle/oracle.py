@@ -41,6 +41,8 @@ def lib() -> C.CDLL:
         L.oracle_clear_row_markings.argtypes = [C.c_uint32, _u32, C.c_uint32]
         L.oracle_time_spmv_csc_f64.argtypes = [C.c_uint32, C.c_uint32, _u32, _u32, _f64, _f64, _f64, C.c_int]
         L.oracle_time_spmv_csc_f64.restype = C.c_double
+        L.oracle_time_spmv_csr_f64_mt.argtypes = [C.c_uint32, _u32, _u32, _f64, _f64, _f64, C.c_int, C.c_int]
+        L.oracle_time_spmv_csr_f64_mt.restype = C.c_double
         for f in (L.oracle_spmv_csc_f64, L.oracle_spmv_csc_u64, L.oracle_csr2csc, L.oracle_mark_row_starts,
                   L.oracle_clear_row_markings):
             f.restype = None
@@ -76,6 +78,17 @@ def csr2csc(n_rows, n_cols, rowptr, colind, vals):
 def time_spmv_csc_f64(colptr, rowind, vals, x, rows, reps):
     y = np.zeros(rows, dtype=np.float64)
     return lib().oracle_time_spmv_csc_f64(rows, colptr.size - 1, colptr, rowind, vals, x, y, reps), y
+
+
+def time_spmv_csr_f64_mt(rowptr, colind, vals, x, reps, nthreads):
+    """Row-parallel CSR baseline on nthreads threads: (mean s/exec, y)."""
+    rows = rowptr.size - 1
+    y = np.zeros(rows, dtype=np.float64)
+    t = lib().oracle_time_spmv_csr_f64_mt(rows, np.ascontiguousarray(rowptr, dtype=np.uint32),
+                                          np.ascontiguousarray(colind, dtype=np.uint32),
+                                          np.ascontiguousarray(vals, dtype=np.float64),
+                                          np.ascontiguousarray(x, dtype=np.float64), y, reps, nthreads)
+    return t, y
 
 
 def mark_row_starts(inds, rows, reverse=False, shift=31):

@@ -107,6 +107,8 @@ def test_bench_json_contract_single(monkeypatch):
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and abs(rf["frac"] - rf["achieved"] / 8000.0) < 1e-3
     cb = out["cpu_baseline"]
     assert cb["cores"] == 1 and cb["kind"] == "port" and cb["value"] > 0
+    mt = out["cpu_baseline_all_cores"]
+    assert mt["cores"] >= 1 and mt["value"] > 0 and mt["bit_exact_vs_softwarespmv"]
     # the stand-in computes the ordered result, so both legs must pass their parity checks
     assert out["parity"].startswith("within FAST bound")
     assert out["secondary"]["mode"] == "ordered" and out["secondary"]["parity"] == "bit-exact vs oracle"
