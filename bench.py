@@ -85,22 +85,31 @@ def cpu_model() -> str:
     return platform.processor()
 
 
-def traffic_from_csv(path: str, kernel_substr: str):
-    """Per-launch HBM bytes from a rocprofv3 counter CSV, corrected as
-    MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KB) x 2 (gfx950 reports
-    half of wide streaming reads) + WRITE_SIZE (KB), averaged over dispatches."""
+# PMC passes committed under profiles/ for kernels whose code has not changed
+# since they were collected (the product kernels are checked instruction for
+# instruction against the round-1 build): used for roofline.traffic when no
+# --traffic-csv is given, and named in roofline.traffic_source.
+PMC_PROFILES = {"vcache_split": "profiles/r01/pmc_vcache_split"}
+
+
+def traffic_from_csv(paths, kernel_substr: str):
+    """Per-launch HBM bytes from rocprofv3 counter CSVs (one counter group per
+    pass), corrected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KB)
+    x 2 (gfx950 tallies 128-B streaming requests at 64 B) + WRITE_SIZE (KB),
+    averaged over dispatches."""
     import csv
     fetch, write = {}, {}
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            if kernel_substr not in row.get("Kernel_Name", ""):
-                continue
-            d = row.get("Dispatch_Id") or row.get("Correlation_Id")
-            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
-            if name == "FETCH_SIZE":
-                fetch[d] = val
-            elif name == "WRITE_SIZE":
-                write[d] = val
+    for path in ([paths] if isinstance(paths, str) else paths):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if kernel_substr not in row.get("Kernel_Name", ""):
+                    continue
+                d = (path, row.get("Dispatch_Id") or row.get("Correlation_Id"))
+                name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
+                if name == "FETCH_SIZE":
+                    fetch[d] = val
+                elif name == "WRITE_SIZE":
+                    write[d] = val
     if not fetch:
         return None
     f = np.mean(list(fetch.values())) * 1024 * 2
@@ -230,9 +239,19 @@ def main():
             secondary = {"mode": other, "error": str(e)}
             y_other = None
 
-    traffic = None
+    traffic, traffic_src = None, None
+    ksub = "k_vcache" if "vcache" in kname else "k_" + kname
     if a.traffic_csv and os.path.exists(a.traffic_csv):
-        traffic = traffic_from_csv(a.traffic_csv, "k_vcache" if "vcache" in kname else "k_" + kname)
+        traffic, traffic_src = traffic_from_csv(a.traffic_csv, ksub), a.traffic_csv
+    elif kname in PMC_PROFILES and not (a.vcache_xlane or a.vcache_dma) and a.workload == "c3" and \
+            (rows, cols, k) == (1 << 20, 1 << 20, 32):
+        import glob
+        d = os.path.join(REPO, PMC_PROFILES[kname])
+        files = sorted(glob.glob(os.path.join(d, "pass*.csv")))
+        if files:
+            traffic = traffic_from_csv(files, ksub)
+            traffic_src = (f"{PMC_PROFILES[kname]}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this kernel "
+                           f"on this workload (committed profile, not this run)")
 
     # parity on rank 0 at N=1: the timed kernels' outputs vs the oracle (checker only)
     cpu = None
@@ -301,6 +320,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic),
+                         "traffic_source": traffic_src,
                          "kernel": "k_" + kname, "alg_bytes_per_launch": alg_bytes,
                          "kernel_us": round(kern_ms * 1e3, 3)},
             "cpu_baseline": cpu,
