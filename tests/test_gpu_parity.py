@@ -279,3 +279,47 @@ def test_experimental_vcache_variants(gpu, kernel, dma, xlane):
                 bound = 2.0 * (lens + 1) * 2.0 ** -53 * (absprod + (np.abs(y0) if beta else 0)) + 1e-300
                 assert np.all(np.abs(ys[0] - y_ref) <= bound), (rows, cols, beta)
         h.close()
+
+
+# ---- analogues of the backend known-answer test (chisel/tests/TestSpMVBackend.scala:122-178):
+# write-out mode (rows come back unchanged: y_in -> y_out with nothing to add) and the stream
+# sums sumUpTo(64) = 2080 carried by the nonzero-value stream and by the input-vector stream.
+@pytest.mark.parametrize("kernel", ["auto", "vcache", "csr_lane", "csr_vector", "vcache_split"])
+def test_backend_kat_writeout_empty_matrix(gpu, kernel):
+    rows = cols = 64
+    colptr = np.zeros(cols + 1, np.uint32)
+    h = hs.Handle.from_csc(colptr, np.zeros(0, np.uint32), np.zeros(0, np.uint64), rows, cols)
+    if kernel != "auto":
+        try:
+            h.set_kernel(kernel)
+            h.exec(np.ones(cols, np.uint64), np.zeros(rows, np.uint64), beta=1, mode=hs.MODE_FAST)
+        except hs.HipSpMVError:
+            pytest.skip(f"{kernel} not applicable to an empty matrix")
+    y_in = np.arange(rows, dtype=np.uint64)
+    for mode in (hs.MODE_ORDERED, hs.MODE_FAST):
+        try:
+            y = h.exec(np.ones(cols, np.uint64), y_in.copy(), beta=1, mode=mode)
+        except hs.HipSpMVError:
+            continue  # a FAST-only kernel in ORDERED mode
+        assert np.array_equal(y, np.arange(rows, dtype=np.uint64))
+        y0 = h.exec(np.ones(cols, np.uint64), y_in.copy(), beta=0, mode=mode)
+        assert not y0.any()
+
+
+@pytest.mark.parametrize("kernel", ["auto", "vcache", "csr_lane", "csr_vector", "vcache_split"])
+def test_backend_kat_stream_sums(gpu, kernel):
+    n = 64
+    # value stream i+1 in one row, x = 1: y0 = sumUpTo(64)
+    colptr = np.arange(n + 1, dtype=np.uint32)
+    rowvec = hs.Handle.from_csc(colptr, np.zeros(n, np.uint32), np.arange(1, n + 1, dtype=np.uint64), 1, n)
+    # input-vector stream i+1 through the identity: sum(y) = sumUpTo(64)
+    ident = hs.Handle.from_csc(colptr, np.arange(n, dtype=np.uint32), np.ones(n, np.uint64), n, n)
+    for h, x, check in ((rowvec, np.ones(n, np.uint64), lambda y: int(y[0]) == 2080),
+                        (ident, np.arange(1, n + 1, dtype=np.uint64), lambda y: int(y.sum()) == 2080)):
+        if kernel != "auto":
+            try:
+                h.set_kernel(kernel)
+                h.exec(x, beta=0, mode=hs.MODE_FAST)
+            except hs.HipSpMVError:
+                continue
+        assert check(h.exec(x, beta=0, mode=hs.MODE_FAST)), kernel
