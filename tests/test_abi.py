@@ -1,5 +1,6 @@
 """The C-ABI library loads and exports every symbol include/hipspmv.h declares
 (no compute: these run without a GPU)."""
+import os
 import ctypes as C
 import subprocess
 
@@ -54,3 +55,10 @@ def test_invalid_arguments_rejected_without_device():
 def test_device_count_callable():
     n = hs.device_count()
     assert n >= 0
+
+
+def test_integration_example_builds():
+    # the INTEGRATION.md example program links against both libraries (usage path: no device needed)
+    import subprocess
+    out = subprocess.run([os.path.join(hs.LIB_DIR, "plugin_example")], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 2 and "usage" in out.stderr

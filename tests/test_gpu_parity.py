@@ -323,3 +323,15 @@ def test_backend_kat_stream_sums(gpu, kernel):
             except hs.HipSpMVError:
                 continue
         assert check(h.exec(x, beta=0, mode=hs.MODE_FAST)), kernel
+
+
+def test_integration_example_program(gpu):
+    # INTEGRATION.md section A, compiled (tools/plugin_example.cpp): factory ->
+    # HIPSpMV on one device and on three blocks of this process, memcmp golden
+    import subprocess
+    out = subprocess.run([f"{hs.LIB_DIR}/plugin_example", fx.MATRICES, "circuit204", "3"], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = [l for l in out.stdout.splitlines() if l.startswith("HIPSpMV")]
+    assert len(lines) == 2 and all("diffFromGolden=0" in l for l in lines), out.stdout
+    assert "devices=1" in lines[0] and "devices=3" in lines[1]
