@@ -96,9 +96,10 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
  * HIPSPMV_MODE_AUTO), "timing" (1 = record per-exec kernel events),
  * "vcache_dma" (1 = vcache kernels stage x by LDS-DMA; experimental),
  * "vcache_xlane" (1 = vcache run continuations across lanes instead of
- * reloads; 2 = that plus register rings loaded by inline asm with explicit
- * vmcnt waits, so the DE-deep entry prefetch survives the loop header;
- * experimental). */
+ * reloads; 2 = that plus step loops padded to the unroll and register rings
+ * loaded by inline asm with explicit vmcnt waits; 3 = cross-lane and padded
+ * loops with the compiler's own waits -- 2 and 3 keep the DE-deep entry
+ * prefetch in flight across the loop header; experimental). */
 int hipspmv_set_option(hipspmv_t *h, const char *key, int64_t value);
 
 /* Replaces HardwareSpMV::exec()'s reset -> init -> regular -> write sequence

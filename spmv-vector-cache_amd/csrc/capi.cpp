@@ -308,7 +308,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "vcache_dma") {
     h->vcache_dma = value ? 1 : 0;
   } else if (k == "vcache_xlane") {
-    if (value < 0 || value > 2) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < 0 || value > 3) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_xlane = (int)value;
   } else if (k == "mode") {
     if (value != HIPSPMV_MODE_ORDERED && value != HIPSPMV_MODE_FAST) return HIPSPMV_ERR_INVALID_ARG;

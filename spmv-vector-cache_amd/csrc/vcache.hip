@@ -278,6 +278,15 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
+  // CX >= 2: both roles run a step count padded to the unroll (extra steps do
+  // no work but keep their loads and barrier), so no loop exits mid-group.
+  // An early exit inside the unrolled group is what makes hipcc's waitcnt
+  // pass merge a path with fewer loads in flight into the loop header and
+  // emit vmcnt(0) there (tools/vmcnt_check.py finds the same infeasible
+  // path); without it the compiler's own waits are exact (CX == 3).
+  constexpr bool PAD = CX >= 2;
+  constexpr uint32_t ALIGN = (DE % 2 == 0) ? DE : 2 * DE;
+  const uint32_t nsteps = PAD ? (npu + ALIGN - 1) / ALIGN * ALIGN : npu;
   __syncthreads();  // segl visible
   if (loader && LD == 1) {
     // panel s+1 is fetched into slot (s+1)&1 during step s; the slot was last
@@ -286,7 +295,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     patch_x(0);
     barrier();
-    for (uint32_t s = 0; s < npu; ++s) {
+    for (uint32_t s = 0; s < nsteps; ++s) {
       if (s + 1 < npu) dma_x(s + 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (s + 1 < npu) patch_x(s + 1);
@@ -302,11 +311,11 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     load_x(1, R[1]);
     load_x(2, R[0]);
     barrier();
-    for (uint32_t base = 0; base < npu; base += 2) {
+    for (uint32_t base = 0; base < nsteps; base += 2) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const uint32_t s = base + i;
-        if (s >= npu) break;
+        if (!PAD && s >= npu) break;
         vm_wait<((AB & 1) || LD != 2) ? 0 : NJ>();  // (branch only live for LD == 2)
         if (s + 1 < npu) store_x(s + 1, R[(i + 1) & 1]);
         load_x(s + 3, R[(i + 1) & 1]);
@@ -321,11 +330,11 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     load_x(1, R[1]);
     load_x(2, R[0]);
     barrier();
-    for (uint32_t base = 0; base < npu; base += 2) {
+    for (uint32_t base = 0; base < nsteps; base += 2) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const uint32_t s = base + i;  // parity of s == parity of i
-        if (s >= npu) break;
+        if (!PAD && s >= npu) break;
         if (s + 1 < npu) store_x(s + 1, R[(i + 1) & 1]);
         load_x(s + 3, R[(i + 1) & 1]);
         barrier();
@@ -337,16 +346,17 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
 #pragma unroll
     for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i]);
     barrier();
-    for (uint32_t base = 0; base < npu; base += DE) {
+    for (uint32_t base = 0; base < nsteps; base += DE) {
 #pragma unroll
       for (int i = 0; i < DE; ++i) {
         const uint32_t s = base + i;
-        if (s >= npu) break;
+        if (!PAD && s >= npu) break;
         if (CX == 2) vm_wait<(AB & 4) ? 0 : (DE - 1) * 2 * EPT>();  // slot i landed, DE-1 steps still in flight
-        if (CX)
-          apply_cx(s, EC[i], EV[i]);
-        else
+        if (CX) {
+          if (!PAD || s < npu) apply_cx(s, EC[i], EV[i]);
+        } else {
           apply(s, EC[i], EV[i]);
+        }
         load_e(s + DE, EC[i], EV[i]);
         barrier();
       }
@@ -415,8 +425,10 @@ static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
     ld == 1 ? launch_one<T, SPLIT, 1, 0>(a, s) : launch_one<T, SPLIT, 0, 0>(a, s);
   } else if (cx == 1) {
     ld == 1 ? launch_one<T, SPLIT, 1, 1>(a, s) : launch_one<T, SPLIT, 0, 1>(a, s);
-  } else {
+  } else if (cx == 2) {
     ld == 1 ? launch_one<T, SPLIT, 1, 2>(a, s) : launch_one<T, SPLIT, 2, 2>(a, s);
+  } else {
+    ld == 1 ? launch_one<T, SPLIT, 1, 3>(a, s) : launch_one<T, SPLIT, 0, 3>(a, s);
   }
 }
 
@@ -436,9 +448,10 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
     const int ept = split == 1 ? VcCfg<1>::EPT : split == 2 ? VcCfg<2>::EPT : VcCfg<4>::EPT;
     return (uint32_t)((kVcThreads / 64 - wl) * 64 * ept);
   };
-  // xlane 1: cross-lane continuation; 2: also the asm rings (entries, and x
-  // unless LDS-DMA stages it) with explicit vmcnt waits
-  const int cx = a.xlane && a.max_seg <= window(a.split) ? (a.xlane >= 2 ? 2 : 1) : 0;
+  // xlane 1: cross-lane continuation; 2: also padded loops and asm rings
+  // (entries, and x unless LDS-DMA stages it) with explicit vmcnt waits;
+  // 3: cross-lane continuation and padded loops, the compiler's own waits
+  const int cx = a.xlane && a.max_seg <= window(a.split) ? a.xlane : 0;
   const int ld = a.dma ? 1 : cx == 2 ? 2 : 0;
   if (a.split == 1)
     dispatch<T, 1>(a, s, ld, cx);

@@ -208,19 +208,25 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather_pipe(const uint32_t* __r
   for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i]);
   vm_wait<0>();
   gather(0, EC[0], G[0]);
-  for (uint32_t base = 0; base < npanels; base += DE) {
+  // step 0, peeled: G(0) has only G(1) younger than it
+  gather(1, EC[1], G[1]);
+  vm_wait<EPT>();
+  apply(0, EC[0], EV[0], G[0]);
+  load_e(DE, EC[0], EV[0]);
+  __syncthreads();
+  // steps 1 .. nsteps-1, padded to whole unrolled groups (extra steps do no
+  // work but keep their loads), so the loop has no early exit: every path
+  // through it issues the same loads, which is what the waits count on
+  const uint32_t nsteps = 1 + (npanels - 1 + DE - 1) / DE * DE;
+  for (uint32_t base = 1; base < nsteps; base += DE) {
 #pragma unroll
     for (int i = 0; i < DE; ++i) {
-      const uint32_t s = base + i;
-      if (s >= npanels) break;
+      const uint32_t s = base + i;  // ring slot (i + 1) % DE, gather buffer (i + 1) & 1
       vm_wait<(DE - 2) * 3 * EPT>();  // E(s+1) landed
-      gather(s + 1, EC[(i + 1) % DE], G[(i + 1) & 1]);
-      if (s == 0)
-        vm_wait<EPT>();  // G(0): only G(1) is younger
-      else
-        vm_wait<3 * EPT>();  // G(s) landed
-      apply(s, EC[i], EV[i], G[i & 1]);
-      load_e(s + DE, EC[i], EV[i]);
+      gather(s + 1, EC[(i + 2) % DE], G[i & 1]);
+      vm_wait<3 * EPT>();  // G(s) landed
+      if (s < npanels) apply(s, EC[(i + 1) % DE], EV[(i + 1) % DE], G[(i + 1) & 1]);
+      load_e(s + DE, EC[(i + 1) % DE], EV[(i + 1) % DE]);
       __syncthreads();  // window s's y updates before window s+1's
     }
   }

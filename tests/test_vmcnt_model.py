@@ -3,11 +3,13 @@
 
 On gfx9 vector-memory loads retire in issue order, so `s_waitcnt vmcnt(N)`
 guarantees every load except the N youngest has landed.  Each model below
-replays one wave's sequence of loads and waits exactly as the kernel issues
-them (prologue, the DE-unrolled steps, the early exit) and checks that every
-register-ring value is consumed only after a wait that retired its load --
-and that no wait is stronger than necessary would not be a correctness issue,
-so only the safety direction is asserted.  Test infrastructure, CPU only."""
+replays one wave's sequence of loads and waits as the kernel issues them
+(prologue, peeled first step, the padded DE-unrolled steps) and checks that
+every register-ring value is consumed only after a wait that retired its
+load; a wait stronger than necessary costs time, not correctness, so only
+the safety direction is asserted.  The last test runs tools/vmcnt_check.py
+(a dataflow check over the compiled kernels' control-flow graphs) on every
+k_vcache and gather instantiation.  Test infrastructure, CPU only."""
 import pytest
 
 
@@ -29,16 +31,19 @@ class Wave:
 
 
 def vcache_compute_ring(npu, DE, EPT):
-    """k_vcache compute role, CX == 2: load_e(s) issues 2*EPT loads; step s
-    waits vmcnt((DE-1)*2*EPT), consumes slot s, issues load_e(s+DE)."""
+    """k_vcache compute role, CX == 2: load_e(s) issues 2*EPT loads; every
+    step of the padded loop waits vmcnt((DE-1)*2*EPT), consumes slot s (a
+    real step only), issues load_e(s+DE)."""
     w = Wave()
     for s in range(DE):
         for j in range(2 * EPT):
             w.load(("e", s, j))
-    for s in range(npu):
+    align = DE if DE % 2 == 0 else 2 * DE
+    for s in range((npu + align - 1) // align * align):
         w.wait((DE - 1) * 2 * EPT)
-        for j in range(2 * EPT):
-            w.use(("e", s, j))
+        if s < npu:
+            for j in range(2 * EPT):
+                w.use(("e", s, j))
         for j in range(2 * EPT):
             w.load(("e", s + DE, j))
     w.wait(0)
@@ -56,7 +61,7 @@ def vcache_loader_ring(npu, NJ):
     for p in (1, 2):
         for j in range(NJ):
             w.load(("x", p, j))
-    for s in range(npu):
+    for s in range((npu + 3) // 4 * 4):  # padded like the compute role (DE = 4)
         w.wait(NJ)
         if s + 1 < npu:
             for j in range(NJ):
@@ -67,8 +72,9 @@ def vcache_loader_ring(npu, NJ):
 
 
 def wgather_pipe(npanels, DE, EPT):
-    """k_wgather_pipe: E(0..DE-1), wait 0, G(0); step s: wait (DE-2)*3*EPT,
-    G(s+1) [needs E(s+1)], wait EPT (s == 0) or 3*EPT, consume E(s), G(s),
+    """k_wgather_pipe: E(0..DE-1), wait 0, G(0); step 0 peeled: G(1), wait EPT,
+    consume, E(DE); steps 1 .. nsteps-1 (padded to whole groups of DE): wait
+    (DE-2)*3*EPT, G(s+1) [needs E(s+1)], wait 3*EPT, consume E(s), G(s),
     issue E(s+DE)."""
     w = Wave()
     for s in range(DE):
@@ -79,13 +85,23 @@ def wgather_pipe(npanels, DE, EPT):
         w.use(("e", 0, j))  # gather(0) reads the codes of step 0
     for j in range(EPT):
         w.load(("g", 0, j))
-    for s in range(npanels):
+    for j in range(2 * EPT):
+        w.use(("e", 1, j))  # gather(1) in the peeled step
+    for j in range(EPT):
+        w.load(("g", 1, j))
+    w.wait(EPT)
+    for j in range(EPT):
+        w.use(("g", 0, j))
+    for j in range(2 * EPT):
+        w.load(("e", DE, j))
+    nsteps = 1 + (npanels - 1 + DE - 1) // DE * DE
+    for s in range(1, nsteps):
         w.wait((DE - 2) * 3 * EPT)
         for j in range(2 * EPT):
             w.use(("e", s + 1, j))  # gather(s+1) reads the codes of step s+1
         for j in range(EPT):
             w.load(("g", s + 1, j))
-        w.wait(EPT if s == 0 else 3 * EPT)
+        w.wait(3 * EPT)
         for j in range(EPT):
             w.use(("g", s, j))
         for j in range(2 * EPT):
@@ -121,3 +137,23 @@ def test_model_catches_a_short_wait():
     w.wait(2)
     with pytest.raises(AssertionError):
         w.use("a")
+
+
+def test_compiled_rings_pass_the_dataflow_check(tmp_path):
+    """tools/vmcnt_check.py on the compiled kernels: every instantiation of
+    k_vcache (product and experimental) and of the gather kernels reads no
+    VGPR a vector-memory load may still be writing."""
+    import os
+    import subprocess
+    import sys
+    import hipspmv as hs
+    csrc = os.path.join(hs.PKG_DIR, "csrc")
+    for src in ("vcache.hip", "wgather.hip"):
+        asm = tmp_path / (src + ".s")
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                        f"-I{os.path.join(hs.REPO_DIR, 'include')}", f"-I{csrc}", "--cuda-device-only", "-S",
+                        os.path.join(csrc, src), "-o", str(asm)], check=True, capture_output=True)
+        out = subprocess.run([sys.executable, os.path.join(hs.PKG_DIR, "tools", "vmcnt_check.py"), str(asm)],
+                             capture_output=True, text=True)
+        assert out.returncode == 0, out.stdout
+        assert out.stdout.count(": 0 violations") >= (40 if src == "vcache.hip" else 6), out.stdout
