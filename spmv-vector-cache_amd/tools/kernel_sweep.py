@@ -43,6 +43,7 @@ if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
               ("split xl1", "vcache_split", F, {"vcache_xlane": 1}), ("split xl2", "vcache_split", F, {"vcache_xlane": 2}),
               ("split dma", "vcache_split", F, {"vcache_dma": 1}),
               ("split dma xl2", "vcache_split", F, {"vcache_dma": 1, "vcache_xlane": 2}),
+              ("vcache xl3", "vcache", O, {"vcache_xlane": 3}), ("split xl3", "vcache_split", F, {"vcache_xlane": 3}),
               ("split4", "vcache_split4", F, {}), ("split4 xl2", "vcache_split4", F, {"vcache_xlane": 2}),
               ("split4 dma xl2", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 2}),
               ("wgather", "wgather", O, {}), ("wgather xl2", "wgather", O, {"vcache_xlane": 2})]

@@ -112,6 +112,7 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 1>, 1, "default (WL8 DE4 EPT3)", 0);
       variant(k_vcache<double, 1, 8, 4, 3, 0, 0, false, 0, 1>, 1, "xlane1", 0, 8 * 64 * 3);
       variant(k_vcache<double, 1, 8, 4, 3, 0, 0, false, 2, 2>, 1, "xlane2 (asm rings)", 0, 8 * 64 * 3);
+      variant(k_vcache<double, 1, 8, 4, 3, 0, 0, false, 0, 3>, 1, "xlane3 (padded, compiler waits)", 0, 8 * 64 * 3);
       variant(k_vcache<double, 1, 8, 6, 3, 0, 0, false, 2, 2>, 1, "xlane2 DE6", 0, 8 * 64 * 3);
       variant(k_vcache<double, 1, 4, 4, 2, 0, 0, false, 2, 2>, 1, "xlane2 WL4 EPT2", 0, 12 * 64 * 2);
       variant(k_vcache<double, 1, 8, 4, 3, 12, 0, false, 2, 2>, 1, "xlane2 no entries/compute", 12, 8 * 64 * 3);
@@ -126,6 +127,7 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 2>, 2, "default (WL6 DE4 EPT3)", 0);
       variant(k_vcache<double, 2, 6, 4, 3, 0, 0, false, 0, 1>, 2, "xlane1", 0, 10 * 64 * 3);
       variant(k_vcache<double, 2, 6, 4, 3, 0, 0, false, 2, 2>, 2, "xlane2 (asm rings)", 0, 10 * 64 * 3);
+      variant(k_vcache<double, 2, 6, 4, 3, 0, 0, false, 0, 3>, 2, "xlane3 (padded, compiler waits)", 0, 10 * 64 * 3);
       variant(k_vcache<double, 2, 6, 6, 3, 0, 0, false, 2, 2>, 2, "xlane2 DE6", 0, 10 * 64 * 3);
       variant(k_vcache<double, 2, 4, 4, 3, 0, 0, false, 2, 2>, 2, "xlane2 WL4", 0, 12 * 64 * 3);
       variant(k_vcache<double, 2, 2, 4, 3, 0, 0, false, 1, 2>, 2, "xlane2 DMA WL2", 0, 14 * 64 * 3);

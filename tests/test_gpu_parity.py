@@ -241,7 +241,8 @@ EXPERIMENTAL = os.environ.get("HIPSPMV_EXPERIMENTAL") == "1"
 @pytest.mark.parametrize("kernel,dma,xlane", [("vcache_split4", 0, 0), ("vcache_split4", 1, 0), ("vcache_split", 1, 0),
                                               ("vcache", 1, 0), ("wgather", 0, 0), ("vcache", 0, 1),
                                               ("vcache", 0, 2), ("vcache_split", 0, 1), ("vcache_split", 0, 2),
-                                              ("vcache_split", 1, 2), ("vcache_split4", 0, 2), ("wgather", 0, 2)])
+                                              ("vcache_split", 1, 2), ("vcache_split4", 0, 2), ("wgather", 0, 2),
+                                              ("vcache", 0, 3), ("vcache_split", 0, 3)])
 def test_experimental_vcache_variants(gpu, kernel, dma, xlane):
     cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20), (20000, 1 << 22)]
     for rows, cols in cases:
