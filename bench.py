@@ -20,7 +20,10 @@ contract for f64 is "within a stated tolerance", checked here per row against
 the oracle -- and the bit-exact ORDERED mode is timed beside it ("ordered").
 
 Also reported: the dominant kernel's roofline (algorithmic bytes per launch /
-its average duration from HIP events on the launch stream, against 8 TB/s),
+its average duration from HIP events on the launch stream, against 8 TB/s;
+beside it the GB/s of a device copy measured on the same GPU, and the
+per-launch median from a separate event-per-launch pass), the PCIe legs of the
+host-buffer path (x upload, y download; never in `value`),
 and the CPU baseline (the oracle's SoftwareSpMV restatement, 1 core, on the
 same shard) on rank 0 at N=1, with a row-parallel CSR run on the box's CPU
 share beside it (cpu_baseline_all_cores; reported, not a target).
@@ -117,6 +120,50 @@ def traffic_from_csv(paths, kernel_substr: str):
     return float(f + w)
 
 
+COPY_BYTES = 1 << 30  # 1 GiB each way: far beyond the 256 MiB Infinity Cache
+
+
+def hbm_copy_gbs(dev, reps: int = 10) -> float:
+    """Measured HBM ceiling on this GPU: a device-to-device copy of `nbytes`
+    (read + write counted), the second denominator SURVEY §8(d) asks for."""
+    nbytes = COPY_BYTES
+    src = torch.empty(nbytes // 8, dtype=torch.float64, device=dev)
+    dst = torch.empty_like(src)
+    src.fill_(1.0)
+    for _ in range(2):
+        dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return gbs
+
+
+def host_transfer_us(xd, yd, reps: int = 5):
+    """PCIe legs of the host-buffer path (hipspmv_exec): x host->device and y
+    device->host through pinned buffers; reported, never part of `value`."""
+    pin = xd.is_cuda
+    xh = torch.empty(xd.shape, dtype=xd.dtype, pin_memory=pin)
+    yh = torch.empty(yd.shape, dtype=yd.dtype, pin_memory=pin)
+    xh.copy_(xd)
+    xs = torch.empty_like(xd)  # scratch target: x itself is left untouched
+    out = []
+    for dst, src in ((xs, xh), (yh, yd)):
+        dst.copy_(src)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        out.append((time.perf_counter() - t) / reps * 1e6)
+    return out[0], out[1]
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,10 +258,28 @@ def main():
         dist.all_gather(per, torch.tensor([kern], dtype=torch.float64, device=dev))
         return float(t.item()), kern, [float(v.item()) for v in per]
 
+    def per_launch_us(mode: int):
+        """A separate pass of K launches, one HIP event pair around each on the
+        launch stream: median and spread of the kernel time (the timed region
+        above carries no per-launch events, so its wall time is unperturbed)."""
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
+        h.exec_device(xd, yd, beta=0, mode=mode, stream=stream)
+        evs[0].record(stream)
+        for i in range(a.steps):
+            h.exec_device(xd, yd, beta=0, mode=mode, stream=stream)
+            evs[i + 1].record(stream)
+        torch.cuda.synchronize()
+        d = np.array([evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(a.steps)])
+        return {"median": round(float(np.median(d)), 3), "min": round(float(d.min()), 3),
+                "max": round(float(d.max()), 3), "launches": a.steps}
+
     mode = MODES[a.mode]
     kname = h.kernel_name(mode)
     wall_max, kern_ms, rank_kern_ms = timed(mode)
     y_main = yd.cpu().numpy().copy() if rank == 0 else None
+    launch_us = per_launch_us(mode)
+    copy_gbs = hbm_copy_gbs(dev)
+    h2d_us, d2h_us = host_transfer_us(xd, yd)
     ms_per_step = wall_max / a.steps * 1e3
     alg_bytes = h.stat("alg_bytes")  # 12*nnz + 4*(rows+1) + 8*cols + 8*rows per launch
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
@@ -322,12 +387,16 @@ def main():
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
                          "kernel": "k_" + kname, "alg_bytes_per_launch": alg_bytes,
-                         "kernel_us": round(kern_ms * 1e3, 3)},
+                         "kernel_us": round(kern_ms * 1e3, 3), "kernel_us_per_launch": launch_us,
+                         "measured_copy_gbs": round(copy_gbs, 1),
+                         "frac_of_measured_copy": round(achieved / copy_gbs, 4) if copy_gbs > 0 else None},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,
             "parity": parity,
             "secondary": secondary,
             "x_bcast_us": None if bcast_us is None else round(bcast_us, 2),
+            "pcie_us": {"x_h2d": round(h2d_us, 2), "y_d2h": round(d2h_us, 2),
+                        "note": "host-buffer path legs (hipspmv_exec), not in value"},
             "rank_kernel_us": [round(v * 1e3, 3) for v in rank_kern_ms],
             "setup_s": round(setup_s, 3),
         }

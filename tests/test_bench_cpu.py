@@ -77,6 +77,7 @@ def _patch(monkeypatch):
     monkeypatch.setattr(torch.cuda, "Event", FakeEvent)
     real_device = torch.device
     monkeypatch.setattr(bench.torch, "device", lambda *a, **k: real_device("cpu"))
+    monkeypatch.setattr(bench, "COPY_BYTES", 1 << 20)
     return bench
 
 
@@ -107,6 +108,9 @@ def test_bench_json_contract_single(monkeypatch):
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and abs(rf["frac"] - rf["achieved"] / 8000.0) < 1e-3
     cb = out["cpu_baseline"]
     assert cb["cores"] == 1 and cb["kind"] == "port" and cb["value"] > 0
+    assert rf["measured_copy_gbs"] >= 0 and rf["kernel_us_per_launch"]["launches"] == 2
+    assert rf["kernel_us_per_launch"]["min"] <= rf["kernel_us_per_launch"]["median"] <= rf["kernel_us_per_launch"]["max"]
+    assert out["pcie_us"]["x_h2d"] >= 0 and out["pcie_us"]["y_d2h"] >= 0
     mt = out["cpu_baseline_all_cores"]
     assert mt["cores"] >= 1 and mt["value"] > 0 and mt["bit_exact_vs_softwarespmv"]
     # the stand-in computes the ordered result, so both legs must pass their parity checks
