@@ -96,7 +96,7 @@ struct hipspmv_multi {
     hipspmv_t* h = nullptr;
     hipStream_t stream = nullptr;
     void *d_x = nullptr, *d_y = nullptr;
-    hipEvent_t ev[4] = {};  // start, x ready, kernel done, y copied
+    hipEvent_t ev[4] = {};  // start (root) / x on the root (others), x ready, kernel done, y copied
     uint64_t kernel_ns = 0;
   };
   std::vector<Shard> shards;
@@ -213,12 +213,14 @@ static int multi_exec(hipspmv_multi_t* m, const void* x, void* y, int beta, int 
     MTRY(hipMemcpyAsync(root.d_x, x, bx, hipMemcpyHostToDevice, root.stream));
     MTRY(hipEventRecord(root.ev[1], root.stream));
   }
-  // 2. broadcast root -> others, ordered after the upload
+  // 2. broadcast root -> others, ordered after the upload.  ev[0] of a
+  //    non-root shard marks "x is on the root" on that shard's own device, so
+  //    the broadcast time is measured between two events of one device.
   for (size_t i = 1; i < m->shards.size(); ++i) {
     auto& s = m->shards[i];
     DevGuard g(s.device);
-    MTRY(hipEventRecord(s.ev[0], s.stream));
     MTRY(hipStreamWaitEvent(s.stream, root.ev[1], 0));
+    MTRY(hipEventRecord(s.ev[0], s.stream));
   }
   if (m->shards.size() > 1) {
     if (!m->comms.empty()) {
@@ -264,13 +266,13 @@ static int multi_exec(hipspmv_multi_t* m, const void* x, void* y, int beta, int 
     DevGuard g(s.device);
     MTRY(hipStreamSynchronize(s.stream));
   }
-  // 4. times: broadcast = root upload done -> last device holding x; kernel =
+  // 4. times: broadcast = root upload done -> x on the device, slowest device; kernel =
   //    slowest shard (its x-ready -> kernel-done, which includes y in for beta 1)
   m->h2d_ns = (uint64_t)(ms_between(root.ev[0], root.ev[1]) * 1e6);
   uint64_t bc = 0, kern = 0, d2h = 0;
   for (size_t i = 0; i < m->shards.size(); ++i) {
     auto& s = m->shards[i];
-    if (i > 0) bc = std::max(bc, (uint64_t)(ms_between(root.ev[1], s.ev[1]) * 1e6));
+    if (i > 0) bc = std::max(bc, (uint64_t)(ms_between(s.ev[0], s.ev[1]) * 1e6));
     if (!s.rows) continue;
     s.kernel_ns = (uint64_t)(ms_between(s.ev[1], s.ev[2]) * 1e6);
     kern = std::max(kern, s.kernel_ns);
