@@ -395,6 +395,11 @@ def main():
             "parity": parity,
             "secondary": secondary,
             "x_bcast_us": None if bcast_us is None else round(bcast_us, 2),
+            # scaling both ways -- `value` is compute-only (x resident);
+            # this rate charges one x broadcast to every step (x changing per step)
+            "end_to_end": None if bcast_us is None else {
+                "value": round(total_flops / (ms_per_step * 1e-3 + bcast_us * 1e-6) / 1e9, 2), "unit": "GFLOP/s",
+                "ms_per_step": round(ms_per_step + bcast_us * 1e-3, 5), "includes": "one RCCL x broadcast per step"},
             "pcie_us": {"x_h2d": round(h2d_us, 2), "y_d2h": round(d2h_us, 2),
                         "note": "host-buffer path legs (hipspmv_exec), not in value"},
             "rank_kernel_us": [round(v * 1e3, 3) for v in rank_kern_ms],

@@ -193,6 +193,8 @@ def test_bench_multi_rank_gloo():
     assert res[1] is None  # only rank 0 prints the line
     out = res[0]
     assert out["n_gpus"] == 2 and out["x_bcast_us"] is not None
+    e2e = out["end_to_end"]
+    assert e2e["value"] <= out["value"] and abs(e2e["ms_per_step"] - out["ms_per_step"] - out["x_bcast_us"] * 1e-3) < 1e-3
     assert out["config"]["parallelism"].startswith("row-partition x2")
     # value is the whole-job rate: both ranks' flops over the max step time
     assert abs(out["value"] - 2 * 2 * out["config"]["nnz_per_gpu"] / (out["ms_per_step"] * 1e-3) / 1e9) < 0.02 * out["value"]
