@@ -343,6 +343,8 @@ int main(int argc, char** argv) {
   };
   std::vector<Case> cases;
   const int big = argc > 1 ? std::atoi(argv[1]) : 16;
+  // "small": only the scaled stripe, R-MAT and random cases (sanitizer builds)
+  const bool small = argc > 2 && std::string(argv[2]) == "small";
   {
     const uint32_t n = 1u << big, k = 32;
     HostCSR A;
@@ -359,6 +361,7 @@ int main(int argc, char** argv) {
   // row shards of the 2^20-column stripe matrix, as the row-partition and
   // golden-vector GPU tests create them (tests/test_golden_vectors.py)
   for (const uint32_t shard : {43691u, 65536u}) {
+    if (small) break;
     const uint32_t n = shard, cols = 1u << 20, k = 32;
     HostCSR A;
     A.rows = n;
@@ -387,6 +390,7 @@ int main(int argc, char** argv) {
   }
   // wide x (32 gather windows) and tall (more than 256 row blocks of 8192)
   for (const auto& shp : {std::array<uint32_t, 3>{20000, 1u << 22, 32}, std::array<uint32_t, 3>{2200001, 5003, 1}}) {
+    if (small) break;
     const uint32_t n = shp[0], cols = shp[1], k = shp[2];
     HostCSR A;
     A.rows = n;

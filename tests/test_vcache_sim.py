@@ -16,3 +16,14 @@ def test_vcache_addressing_replay():
     lines = [l for l in out.stdout.splitlines() if "split=" in l]
     assert sum(": ok" in l for l in lines) >= 16, out.stdout
     assert "VIOLATION" not in out.stderr
+
+
+def test_layout_builder_and_replay_under_sanitizers():
+    # csrc/plan.cpp (the layouts every vcache/wgather launch reads) built with
+    # ASan + UBSan, replayed on the scaled stripe, R-MAT and random cases
+    subprocess.run(["make", "-C", hs.PKG_DIR, "lib/vc_sim_san"], check=True, stdout=subprocess.DEVNULL)
+    out = subprocess.run([os.path.join(hs.LIB_DIR, "vc_sim_san"), "12", "small"], capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    assert sum(": ok" in l for l in out.stdout.splitlines()) >= 60
+    assert "runtime error" not in out.stderr and "AddressSanitizer" not in out.stderr
