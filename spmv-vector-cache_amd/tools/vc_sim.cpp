@@ -422,6 +422,34 @@ int main(int argc, char** argv) {
                       {kWgWindow.rows, kWgWindow.panel, 0, 4, 4, 1, 2, kWgWindow.colbits, 2}};
   int failures = 0;
   for (auto& cs : cases) {
+    // host-side planning beside the replay: CSC -> CSR (csc_to_csr, the
+    // hipspmv_create path) reproduces the case's CSR exactly, and the
+    // csr_vector row groups tile the rows
+    {
+      const HostCSR& A = cs.A;
+      std::vector<uint32_t> colptr(A.cols + 1, 0), rowind(A.nnz), cur;
+      std::vector<uint64_t> cv(A.nnz);
+      for (uint32_t e = 0; e < A.nnz; ++e) colptr[A.colind[e] + 1]++;
+      for (uint32_t c = 0; c < A.cols; ++c) colptr[c + 1] += colptr[c];
+      cur.assign(colptr.begin(), colptr.end() - 1);
+      for (uint32_t r = 0; r < A.rows; ++r)
+        for (uint32_t e = A.rowptr[r]; e < A.rowptr[r + 1]; ++e) {
+          const uint32_t d = cur[A.colind[e]]++;
+          rowind[d] = r | (e == A.rowptr[r] ? 1u << 31 : 0u);  // CMS marks are masked
+          cv[d] = A.vals[e];
+        }
+      HostCSR B;
+      std::string why;
+      const int st = csc_to_csr(colptr.data(), rowind.data(), cv.data(), A.rows, A.cols, A.nnz, B, why);
+      const bool same = st == 0 && B.rowptr == A.rowptr && B.colind == A.colind && B.vals == A.vals;
+      std::vector<uint32_t> groups;
+      build_row_groups(A, groups);
+      bool tiles = groups.size() >= 2 && groups.front() == 0 && groups.back() == A.rows;
+      for (size_t i = 1; i < groups.size(); ++i) tiles = tiles && groups[i - 1] < groups[i];
+      failures += !(same && tiles);
+      std::printf("%-28s csc_to_csr %s, row groups %s\n", cs.name.c_str(), same ? "ok" : "FAIL",
+                  tiles ? "ok" : "FAIL");
+    }
     std::vector<double> x(cs.A.cols), yin(cs.A.rows);
     for (uint32_t i = 0; i < cs.A.cols; ++i) x[i] = uniform11(splitmix64_at(3, i));
     for (uint32_t i = 0; i < cs.A.rows; ++i) yin[i] = uniform11(splitmix64_at(5, i));
