@@ -73,6 +73,11 @@ extern "C" {
 #define HIPSPMV_KERNEL_WGATHER 6 /* y block in LDS, x gathered from global in
                                     2^17-column windows (wide x: C4/C5);
                                     ordered; experimental like VCACHE_SPLIT4 */
+#define HIPSPMV_KERNEL_SELL 7 /* SELL-C-sigma: one lane per row over slices of
+                                 256 length-sorted rows, coalesced entries; rows
+                                 over 256 entries one wave each; ordered in
+                                 ORDERED mode (FAST: long rows tree-summed); any
+                                 matrix; layout built when first selected */
 
 typedef struct hipspmv_handle hipspmv_t;
 

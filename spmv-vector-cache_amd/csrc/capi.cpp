@@ -79,6 +79,14 @@ struct hipspmv_handle {
     uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, part_panels = 0, npad = 0, max_seg = 0;
     int split = 1;
   } vc[4];  // [0] ordered (kVcOrdered), [1] split (kVcSplit); experimental: [2] split4, [3] wgather windows
+  struct Sell {  // k_sell layout, built on first use (option "kernel" = SELL)
+    bool built = false;
+    uint64_t* d_off = nullptr;
+    uint32_t *d_width = nullptr, *d_row = nullptr, *d_len = nullptr, *d_col = nullptr, *d_hubs = nullptr;
+    uint64_t* d_vals = nullptr;
+    uint32_t nslices = 0, nhubs = 0;
+    uint64_t padding = 0;
+  } sell;
   int vcache_dma = 0;    // option "vcache_dma": LDS-DMA x loader (experimental)
   int vcache_xlane = 0;  // option "vcache_xlane": cross-lane run continuation (experimental)
   void *d_x = nullptr, *d_y = nullptr;
@@ -99,6 +107,12 @@ static void release(hipspmv_t* h) {
   for (auto& v : h->vc) {
     void* vp[] = {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial};
     for (void* p : vp)
+      if (p) (void)hipFree(p);
+  }
+  {
+    auto& q = h->sell;
+    void* sp[] = {q.d_off, q.d_width, q.d_row, q.d_len, q.d_col, q.d_hubs, q.d_vals};
+    for (void* p : sp)
       if (p) (void)hipFree(p);
   }
   for (hipEvent_t e : h->ev)
@@ -152,6 +166,41 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
       h->device_bytes += 8ull * v.split * a.rows;
     }
   }
+  return HIPSPMV_OK;
+}
+
+// The SELL layout is built from the device CSR copy (the host CSR is gone
+// after create), once, when the kernel is first selected.
+static int build_sell_layout(hipspmv_t* h) {
+  auto& q = h->sell;
+  if (q.built) return HIPSPMV_OK;
+  DeviceGuard g(h->device);
+  HostCSR a;
+  a.rows = h->rows;
+  a.cols = h->cols;
+  a.nnz = h->nnz;
+  a.rowptr.resize((size_t)h->rows + 1);
+  a.colind.resize(h->nnz);
+  a.vals.resize(h->nnz);
+  HIP_TRY(hipMemcpy(a.rowptr.data(), h->d_rowptr, 4ull * (h->rows + 1), hipMemcpyDeviceToHost));
+  if (h->nnz) {
+    HIP_TRY(hipMemcpy(a.colind.data(), h->d_colind, 4ull * h->nnz, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(a.vals.data(), h->d_vals, 8ull * h->nnz, hipMemcpyDeviceToHost));
+  }
+  SellLayout L;
+  build_sell(a, L);
+  int st;
+  if ((st = dev_upload(&q.d_off, L.off.data(), L.off.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&q.d_width, L.width.data(), L.width.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&q.d_row, L.row.data(), L.row.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&q.d_len, L.len.data(), L.len.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&q.d_col, L.col.data(), L.col.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&q.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&q.d_hubs, L.hubs.data(), L.hubs.size(), h->device_bytes))) return st;
+  q.nslices = L.nslices;
+  q.nhubs = L.nhubs;
+  q.padding = L.padding;
+  q.built = true;
   return HIPSPMV_OK;
 }
 
@@ -211,6 +260,8 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
       return h->vc[3].ok ? HIPSPMV_KERNEL_WGATHER : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_LANE:
       return HIPSPMV_KERNEL_CSR_LANE;
+    case HIPSPMV_KERNEL_SELL:  // ordered: valid in both modes
+      return h->sell.built ? HIPSPMV_KERNEL_SELL : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_VECTOR:
       return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_AUTO:
@@ -229,9 +280,16 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
 }
 
 static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in, void* d_y_out, int beta,
-                  hipStream_t s) {
+                  hipStream_t s, int mode) {
   hipError_t e = hipSuccess;
-  if (kernel == HIPSPMV_KERNEL_VCACHE || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ||
+  if (mode == HIPSPMV_MODE_AUTO) mode = h->mode_opt;
+  if (kernel == HIPSPMV_KERNEL_SELL) {
+    const auto& q = h->sell;
+    SellArgs a{q.d_off,     q.d_width, q.d_row,     q.d_len, q.d_col, q.d_vals,  q.d_hubs,
+               h->d_rowptr, h->d_colind, h->d_vals, d_x,     d_y_in,  d_y_out,   q.nslices,
+               q.nhubs,     beta,      mode == HIPSPMV_MODE_ORDERED ? 1 : 0};
+    e = launch_sell(h->dtype, a, s);
+  } else if (kernel == HIPSPMV_KERNEL_VCACHE || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ||
       kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
     const int k = kernel == HIPSPMV_KERNEL_VCACHE ? 0 : kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1 : 2;
     const auto& v = h->vc[k];
@@ -303,7 +361,14 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   if (!h || !key) return HIPSPMV_ERR_INVALID_ARG;
   const std::string k(key);
   if (k == "kernel") {
-    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_WGATHER) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_SELL) return HIPSPMV_ERR_INVALID_ARG;
+    if (value == HIPSPMV_KERNEL_SELL) {
+      try {
+        if (int st = build_sell_layout(h)) return st;
+      } catch (const std::bad_alloc&) {
+        return HIPSPMV_ERR_OOM;
+      }
+    }
     h->kernel_opt = (int)value;
   } else if (k == "vcache_dma") {
     h->vcache_dma = value ? 1 : 0;
@@ -341,7 +406,7 @@ int hipspmv_exec(hipspmv_t* h, const void* x, void* y, int beta, int mode) {
     HIP_TRY(hipMemcpyAsync(h->d_x, x, bx, hipMemcpyHostToDevice, s));
     if (beta) HIP_TRY(hipMemcpyAsync(h->d_y, y, by, hipMemcpyHostToDevice, s));
     HIP_TRY(hipEventRecord(h->ev[1], s));
-    int st = launch(h, kernel, h->d_x, h->d_y, h->d_y, beta, s);
+    int st = launch(h, kernel, h->d_x, h->d_y, h->d_y, beta, s, mode);
     if (st) return st;
     HIP_TRY(hipEventRecord(h->ev[2], s));
     HIP_TRY(hipMemcpyAsync(y, h->d_y, by, hipMemcpyDeviceToHost, s));
@@ -369,7 +434,7 @@ int hipspmv_exec_device(hipspmv_t* h, const void* d_x, const void* d_y_in, void*
   DeviceGuard g(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the default stream
   if (h->timing) HIP_TRY(hipEventRecord(h->ev[1], s));
-  int st = launch(h, kernel, d_x, beta ? d_y_in : d_y_out, d_y_out, beta, s);
+  int st = launch(h, kernel, d_x, beta ? d_y_in : d_y_out, d_y_out, beta, s, mode);
   if (st) return st;
   if (h->timing) {
     HIP_TRY(hipEventRecord(h->ev[2], s));
@@ -415,6 +480,9 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "wgather_eligible") *out = h->vc[3].ok;
   else if (k == "wgather_windows") *out = h->vc[3].npanels;
   else if (k == "vcache_split4_x_bytes") *out = h->vc[2].ok ? 8ull * h->vc[2].nblocks * h->cols : 0;
+  else if (k == "sell_slices") *out = h->sell.nslices;
+  else if (k == "sell_hubs") *out = h->sell.nhubs;
+  else if (k == "sell_padding") *out = h->sell.padding;
   else if (k == "row_groups") *out = h->ngroups;
   else if (k == "max_row_len") *out = h->max_row_len;
   else if (k == "empty_rows") *out = h->empty_rows;
@@ -432,6 +500,7 @@ const char* hipspmv_kernel_name(hipspmv_t* h, int mode) {
     case HIPSPMV_KERNEL_WGATHER: return "wgather";
     case HIPSPMV_KERNEL_CSR_LANE: return "csr_lane";
     case HIPSPMV_KERNEL_CSR_VECTOR: return "csr_vector";
+    case HIPSPMV_KERNEL_SELL: return "sell";
     default: return "unsupported";
   }
 }

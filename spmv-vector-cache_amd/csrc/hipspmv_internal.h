@@ -43,6 +43,19 @@ constexpr uint32_t kVcMore = 1u << 31;  // next entry continues this entry's row
 constexpr int kCvGroupNnz = 256;  // max nnz of a multi-row group (4 per lane)
 constexpr int kCvGroupRows = 64;  // max rows of a multi-row group (1 per lane)
 
+// ---- k_sell geometry ---------------------------------------
+// SELL-C-sigma: rows sorted by length (descending, stable) inside windows of
+// kSellSigma rows, cut into slices of kSellRows rows, one wave per slice: lane
+// l owns rows l, l+64, l+128, l+192 of the slice (four independent sequential
+// sums per lane); entry k of sub-slice j, lane l at off + (4k + j)*64 + l.
+// Rows longer than kSellHub entries are "hub" rows: one wave each, reading
+// the CSR copy (ordered: one sequential chain; fast: lane partials + a fixed
+// shuffle tree).
+constexpr int kSellRows = 256;
+constexpr uint32_t kSellSigma = 65536;
+constexpr uint32_t kSellHub = 256;
+constexpr uint32_t kSellNoRow = 0xFFFFFFFFu;
+
 struct HostCSR {
   uint32_t rows = 0, cols = 0, nnz = 0;
   std::vector<uint32_t> rowptr, colind;
@@ -60,6 +73,18 @@ struct VcacheLayout {
   uint32_t max_seg = 0;
 };
 
+struct SellLayout {
+  uint32_t nslices = 0, nhubs = 0;
+  std::vector<uint64_t> off;    // nslices + 1: first entry of each slice
+  std::vector<uint32_t> width;  // nslices: longest row of the slice
+  std::vector<uint32_t> row;    // nslices * kSellRows: row id (kSellNoRow past the window's rows)
+  std::vector<uint32_t> len;    // nslices * kSellRows: row length (0 for kSellNoRow)
+  std::vector<uint32_t> col;    // off[nslices] entries; padding: column 0
+  std::vector<uint64_t> vals;   // padding: 0 (never added: k < len selects)
+  std::vector<uint32_t> hubs;   // hub rows, longest first
+  uint64_t padding = 0;         // padded entries (off[nslices] - nnz of the slices)
+};
+
 // CSC (SparseMatrix layout) -> CSR, stable, masking bits 30-31 of the row ids.
 // Returns a HIPSPMV_* status; fills `why` on validation failure.
 int csc_to_csr(const uint32_t* colptr, const uint32_t* rowind, const void* vals, uint32_t rows, uint32_t cols,
@@ -69,6 +94,7 @@ int copy_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, u
 
 bool vcache_eligible(const HostCSR& a, const VcGeom& g);
 void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out);
+void build_sell(const HostCSR& a, SellLayout& out);
 // Row groups for csr_vector: group g covers rows [groups[g], groups[g+1]).
 void build_row_groups(const HostCSR& a, std::vector<uint32_t>& groups);
 

@@ -36,7 +36,27 @@ struct CsrArgs {
   int beta;
 };
 
+struct SellArgs {
+  const uint64_t* off;    // [nslices + 1]
+  const uint32_t* width;  // [nslices]
+  const uint32_t* row;    // [nslices * 256]
+  const uint32_t* len;    // [nslices * 256]
+  const uint32_t* col;    // padded entries
+  const void* vals;
+  const uint32_t* hubs;   // [nhubs] rows read from the CSR copy
+  const uint32_t* rowptr;
+  const uint32_t* colind;
+  const void* csr_vals;
+  const void* x;
+  const void* y_in;
+  void* y_out;
+  uint32_t nslices, nhubs;
+  int beta;
+  int exact;  // 1: hub rows summed in one sequential chain (ORDERED f64)
+};
+
 hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);
+hipError_t launch_sell(int dtype, const SellArgs& a, hipStream_t s);
 hipError_t launch_wgather(int dtype, const VcacheArgs& a, hipStream_t s);
 hipError_t launch_csr_lane(int dtype, const CsrArgs& a, hipStream_t s);
 hipError_t launch_csr_vector(int dtype, const CsrArgs& a, hipStream_t s);

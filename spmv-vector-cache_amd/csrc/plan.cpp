@@ -164,6 +164,64 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
   }
 }
 
+// SELL-C-sigma layout for k_sell (hipspmv_internal.h): within each window of
+// kSellSigma rows the rows of at most kSellHub entries are ordered by length,
+// longest first (ties by row id), and cut into slices of kSellRows; each
+// row's entries keep their CSR order (ascending column = SoftwareSpMV's
+// order), so the lane that owns a row adds them exactly as the reference does.
+void build_sell(const HostCSR& a, SellLayout& out) {
+  out = SellLayout{};
+  std::vector<uint32_t> hubs, order;
+  out.off.push_back(0);
+  for (uint32_t w0 = 0; w0 < a.rows; w0 += kSellSigma) {
+    const uint32_t w1 = std::min<uint64_t>((uint64_t)w0 + kSellSigma, a.rows);
+    order.clear();
+    for (uint32_t r = w0; r < w1; ++r) {
+      if (a.rowptr[r + 1] - a.rowptr[r] > kSellHub)
+        hubs.push_back(r);
+      else
+        order.push_back(r);
+    }
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t p, uint32_t q) {
+      return a.rowptr[p + 1] - a.rowptr[p] > a.rowptr[q + 1] - a.rowptr[q];
+    });
+    for (size_t s0 = 0; s0 < order.size(); s0 += kSellRows) {
+      const size_t s1 = std::min(order.size(), s0 + kSellRows);
+      const uint32_t width = a.rowptr[order[s0] + 1] - a.rowptr[order[s0]];  // longest first
+      const uint64_t base = out.off.back();
+      out.width.push_back(width);
+      out.off.push_back(base + (uint64_t)width * kSellRows);
+      out.col.resize(out.off.back(), 0u);
+      out.vals.resize(out.off.back(), 0u);
+      for (size_t i = 0; i < (size_t)kSellRows; ++i) {
+        const uint32_t j = (uint32_t)(i / 64), l = (uint32_t)(i % 64);
+        if (s0 + i >= s1) {
+          out.row.push_back(kSellNoRow);
+          out.len.push_back(0);
+          continue;
+        }
+        const uint32_t r = order[s0 + i], e0 = a.rowptr[r], n = a.rowptr[r + 1] - e0;
+        out.row.push_back(r);
+        out.len.push_back(n);
+        for (uint32_t k = 0; k < n; ++k) {
+          const uint64_t d = base + ((uint64_t)k * 4 + j) * 64 + l;
+          out.col[d] = a.colind[e0 + k];
+          out.vals[d] = a.vals[e0 + k];
+        }
+      }
+    }
+  }
+  std::stable_sort(hubs.begin(), hubs.end(), [&](uint32_t p, uint32_t q) {
+    return a.rowptr[p + 1] - a.rowptr[p] > a.rowptr[q + 1] - a.rowptr[q];
+  });
+  uint64_t hub_nnz = 0;
+  for (uint32_t r : hubs) hub_nnz += a.rowptr[r + 1] - a.rowptr[r];
+  out.padding = out.off.back() - (a.nnz - hub_nnz);
+  out.hubs = std::move(hubs);
+  out.nhubs = (uint32_t)out.hubs.size();
+  out.nslices = (uint32_t)out.width.size();
+}
+
 // Greedy row groups: consecutive rows while the group stays within
 // kCvGroupNnz nonzeros and kCvGroupRows rows; a longer row is a group alone.
 void build_row_groups(const HostCSR& a, std::vector<uint32_t>& groups) {

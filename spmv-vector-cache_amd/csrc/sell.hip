@@ -1,0 +1,244 @@
+// k_sell: SELL-C-sigma SpMV for gfx950 -- one lane per row, ORDERED for any
+// matrix.
+//
+// The vector-cache kernels need x to be streamed through LDS by every row
+// block, which pays only while the matrix is dense enough per x element
+// (choose_kernel); k_csr_lane, the ordered fallback, reads each row's entries
+// with per-lane strides (no coalescing).  Here every row is still summed by
+// ONE lane in ascending column order (SoftwareSpMV.cpp:59-64: products
+// rounded, then added in order), but the entries are stored slice-major, so
+// the 64 lanes of a wave read 64 consecutive 4-B column ids and 64
+// consecutive 8-B values per step:
+//
+//   slice s: 256 rows (lane l owns rows l, l+64, l+128, l+192 -- four
+//            independent chains per lane), width = its longest row; entry k
+//            of sub-slice j, lane l at off[s] + (4k + j)*64 + l.
+//   rows sorted by length inside windows of kSellSigma rows, so a slice's
+//   rows have similar lengths (little padding); padded steps are loaded
+//   (column 0, value 0: branch-free, coalesced) but never added.
+//   hub rows (> kSellHub entries) -- one wave each over the CSR copy:
+//   entries loaded 256 at a time two stages ahead; ORDERED f64 sums the
+//   products in one sequential chain through v_readlane (the order is the
+//   contract); FAST / u64 keeps four lane partials and a fixed xor-shuffle
+//   tree (deterministic).
+//
+// Bytes per launch: 12 B per entry (padding included) + 8 B per slice row
+// (row id, length) + 8 B per row of y written; x gathered from L2/MALL.
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "hipspmv_internal.h"
+#include "kernels.h"
+
+namespace hipspmv {
+namespace {
+
+constexpr int kHubG = 4;                    // chunks of 64 entries per hub pipeline stage
+constexpr uint32_t kHubStage = 64 * kHubG;  // entries per stage
+
+template <typename T>
+__device__ __forceinline__ T nt(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+
+// v as held by lane l (l wave-uniform)
+template <typename T>
+__device__ __forceinline__ T lane_value(T v, uint32_t l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, (int)l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), (int)l);
+  return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+}
+
+template <typename T>
+__device__ __forceinline__ T xor_shuffle(T v, int m) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)u, m);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(u >> 32), m);
+  return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+}
+
+// One hub row r (n > kSellHub entries, so n >= kHubStage + 1), the whole wave.
+template <typename T, bool EXACT>
+__device__ __forceinline__ void hub_row(const SellArgs& a, uint32_t r, int lane) {
+#pragma clang fp contract(off)
+  const T* __restrict__ vals = static_cast<const T*>(a.csr_vals);
+  const T* __restrict__ x = static_cast<const T*>(a.x);
+  const uint32_t base = a.rowptr[r], n = a.rowptr[r + 1] - base;
+  // entries of the stage starting at g0, indices clamped into the row (the
+  // clamped copies are loaded but never consumed)
+  auto load = [&](uint32_t g0, uint32_t* c, T* v) {
+#pragma unroll
+    for (int j = 0; j < kHubG; ++j) {
+      const uint32_t e = min(g0 + (uint32_t)(j * 64 + lane), n - 1);
+      c[j] = nt(a.colind + base + e);
+      v[j] = nt(vals + base + e);
+    }
+  };
+  uint32_t cA[kHubG];
+  T vA[kHubG], p[kHubG], xs[kHubG];
+  load(0, cA, vA);
+#pragma unroll
+  for (int j = 0; j < kHubG; ++j) xs[j] = x[cA[j]];
+#pragma unroll
+  for (int j = 0; j < kHubG; ++j) p[j] = vA[j] * xs[j];  // stage 0 products (rounded)
+  load(kHubStage, cA, vA);                              // stage 1 entries
+  T acc = EXACT && a.beta ? static_cast<const T*>(a.y_in)[r] : T(0);  // the chain starts from y_in
+  T part[kHubG];
+#pragma unroll
+  for (int j = 0; j < kHubG; ++j) part[j] = T(0);
+  for (uint32_t g0 = 0; g0 < n; g0 += kHubStage) {
+    // gathers of the next stage and entries of the one after, in flight
+    // while this stage's products are summed
+#pragma unroll
+    for (int j = 0; j < kHubG; ++j) xs[j] = x[cA[j]];
+    uint32_t cB[kHubG];
+    T vB[kHubG];
+    load(g0 + 2 * kHubStage, cB, vB);
+    const uint32_t m = min(kHubStage, n - g0);
+    if (EXACT) {
+      if (m == kHubStage) {
+#pragma unroll
+        for (int j = 0; j < kHubG; ++j) {
+#pragma unroll
+          for (int l = 0; l < 64; ++l) acc = acc + lane_value(p[j], (uint32_t)l);
+        }
+      } else {  // the row's last stage
+#pragma unroll
+        for (int j = 0; j < kHubG; ++j) {
+          const uint32_t mj = m > (uint32_t)j * 64 ? min(64u, m - (uint32_t)j * 64) : 0u;
+          for (uint32_t l = 0; l < mj; ++l) acc = acc + lane_value(p[j], l);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kHubG; ++j)
+        if (g0 + (uint32_t)(j * 64 + lane) < n) part[j] = part[j] + p[j];
+    }
+#pragma unroll
+    for (int j = 0; j < kHubG; ++j) {
+      p[j] = vA[j] * xs[j];
+      cA[j] = cB[j];
+      vA[j] = vB[j];
+    }
+  }
+  if (EXACT) {
+    if (lane == 0) static_cast<T*>(a.y_out)[r] = acc;
+  } else {
+    T s = (part[0] + part[1]) + (part[2] + part[3]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s = s + xor_shuffle(s, d);  // every lane: the same total
+    if (lane == 0) static_cast<T*>(a.y_out)[r] = a.beta ? static_cast<const T*>(a.y_in)[r] + s : s;
+  }
+}
+
+// One slice s: lane `lane` sums rows row[s][j*64 + lane], j = 0..3.
+template <typename T>
+__device__ __forceinline__ void slice_rows(const SellArgs& a, uint32_t s, int lane) {
+#pragma clang fp contract(off)
+  const T* __restrict__ x = static_cast<const T*>(a.x);
+  const uint64_t off = a.off[s];
+  const uint32_t width = a.width[s];
+  uint32_t r[4], n[4];
+  T acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const size_t i = (size_t)s * kSellRows + j * 64 + lane;
+    r[j] = a.row[i];
+    n[j] = a.len[i];
+    acc[j] = a.beta && r[j] != kSellNoRow ? static_cast<const T*>(a.y_in)[r[j]] : T(0);
+  }
+  const uint32_t* __restrict__ c = a.col + off + lane;
+  const T* __restrict__ v = static_cast<const T*>(a.vals) + off + lane;
+  // Software pipeline over pairs of steps (8 entries per lane), two register
+  // buffers A/B: gathers of one pair are issued, then the entries of the
+  // pair after it, then the products wait for the gathers only (vmcnt counts
+  // in issue order, so the younger entry loads stay in flight).  Clamped
+  // indices keep every prefetch inside the slice.
+  auto load2 = [&](uint32_t k0, uint32_t* cc, T* vv) {
+    const size_t i0 = (size_t)k0 * 4 * 64;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      cc[q] = nt(c + i0 + q * 64);
+      vv[q] = nt(v + i0 + q * 64);
+    }
+    // compiler-only barriers (emit nothing): without a possible memory write
+    // after these loads, InstCombine folds a loop-carried load into one load
+    // at the loop header (the prefetch is lost); the scheduling barrier keeps
+    // the machine scheduler from interleaving the three groups (gathers, next
+    // entries, products), which would put a wait for a young load in front
+    // of older work
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto add2 = [&](uint32_t k0, const T* xx, const T* vv) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int j = q & 3;
+      const T t = madd(acc[j], vv[q], xx[q]);
+      acc[j] = k0 + (q >> 2) < n[j] ? t : acc[j];
+    }
+  };
+  auto gather2 = [&](const uint32_t* cc, T* xx) {
+    __builtin_amdgcn_sched_barrier(0);  // after the previous products
+#pragma unroll
+    for (int q = 0; q < 8; ++q) xx[q] = x[cc[q]];
+    asm volatile("" ::: "memory");  // the gathers issue before the next entry loads
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  uint32_t k = 0;
+  if (width >= 4) {
+    uint32_t cA[8], cB[8];
+    T vA[8], vB[8], xx[8];
+    load2(0, cA, vA);
+    for (; k + 4 <= width; k += 4) {
+      gather2(cA, xx);
+      load2(k + 2, cB, vB);
+      add2(k, xx, vA);
+      gather2(cB, xx);
+      load2(min(k + 4, width - 2), cA, vA);
+      add2(k + 2, xx, vB);
+    }
+  }
+  for (; k < width; ++k) {  // the last 0-3 steps
+    const size_t i0 = (size_t)k * 4 * 64;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const T t = madd(acc[j], nt(v + i0 + j * 64), x[nt(c + i0 + j * 64)]);
+      acc[j] = k < n[j] ? t : acc[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (r[j] != kSellNoRow) static_cast<T*>(a.y_out)[r[j]] = acc[j];
+}
+
+// Waves [0, nhubs) take the hub rows (longest first), the rest one slice each.
+template <typename T, bool EXACT>
+__global__ __launch_bounds__(256) void k_sell(const SellArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t w = blockIdx.x * 4 + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w < a.nhubs) {
+    hub_row<T, EXACT>(a, a.hubs[w], lane);
+    return;
+  }
+  const uint32_t s = w - a.nhubs;
+  if (s < a.nslices) slice_rows<T>(a, s, lane);
+}
+
+template <typename T, bool EXACT>
+hipError_t launch(const SellArgs& a, hipStream_t s) {
+  const uint64_t waves = (uint64_t)a.nhubs + a.nslices;
+  if (waves == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_sell<T, EXACT>), dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_sell(int dtype, const SellArgs& a, hipStream_t s) {
+  if (dtype == HIPSPMV_U64) return launch<uint64_t, false>(a, s);  // integer sums: order-free
+  return a.exact ? launch<double, true>(a, s) : launch<double, false>(a, s);
+}
+
+}  // namespace hipspmv

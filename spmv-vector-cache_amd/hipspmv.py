@@ -33,9 +33,10 @@ F64, U64 = 0, 1
 MODE_AUTO, MODE_ORDERED, MODE_FAST = 0, 1, 2
 KERNEL_AUTO, KERNEL_VCACHE, KERNEL_CSR_LANE, KERNEL_CSR_VECTOR, KERNEL_VCACHE_SPLIT = 0, 1, 2, 3, 4
 KERNEL_VCACHE_SPLIT4, KERNEL_WGATHER = 5, 6  # experimental: never chosen by AUTO
+KERNEL_SELL = 7  # SELL-C-sigma lane per row; selectable, not chosen by AUTO yet
 KERNELS = {"auto": KERNEL_AUTO, "vcache": KERNEL_VCACHE, "csr_lane": KERNEL_CSR_LANE,
            "csr_vector": KERNEL_CSR_VECTOR, "vcache_split": KERNEL_VCACHE_SPLIT,
-           "vcache_split4": KERNEL_VCACHE_SPLIT4, "wgather": KERNEL_WGATHER}
+           "vcache_split4": KERNEL_VCACHE_SPLIT4, "wgather": KERNEL_WGATHER, "sell": KERNEL_SELL}
 STATUS = {0: "ok", 1: "invalid argument", 2: "invalid matrix", 3: "HIP error", 4: "out of memory",
           5: "unsupported", 6: "no device", 7: "unknown key"}
 

@@ -32,6 +32,8 @@ for s in $STEPS; do
     ablate) step ablate 600 ./spmv-vector-cache_amd/lib/vc_ablate ;;
     sweep) step sweep 600 python spmv-vector-cache_amd/tools/kernel_sweep.py ;;
     sweepx) HIPSPMV_EXPERIMENTAL=1 step sweep_exp 900 python spmv-vector-cache_amd/tools/kernel_sweep.py ;;
+    sweeprmat) step sweep_rmat 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --rmat 20 ;;
+    sweepwide) step sweep_wide 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 21 --log2-cols 24 ;;
     c4) step bench_c4 900 python bench.py --workload c4 --steps 20 --warmup 5 ;;
     c5) step bench_c5 900 python bench.py --workload c5 --steps 20 --warmup 5 ;;
     c4wg) HIPSPMV_EXPERIMENTAL=1 step bench_c4_wgather 900 python bench.py --workload c4 --scale 24 --kernel wgather --mode ordered --steps 10 --warmup 3 --no-secondary ;;

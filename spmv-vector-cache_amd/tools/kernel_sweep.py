@@ -35,7 +35,7 @@ s = torch.cuda.current_stream()
 O, F = hs.MODE_ORDERED, hs.MODE_FAST
 # (label, kernel, mode, options); the experimental ones need HIPSPMV_EXPERIMENTAL=1 at create
 cands = [("vcache", "vcache", O, {}), ("csr_lane", "csr_lane", O, {}), ("vcache_split", "vcache_split", F, {}),
-         ("csr_vector", "csr_vector", F, {})]
+         ("csr_vector", "csr_vector", F, {}), ("sell", "sell", O, {}), ("sell fast", "sell", F, {})]
 if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
     cands += [("vcache xl1", "vcache", O, {"vcache_xlane": 1}), ("vcache xl2", "vcache", O, {"vcache_xlane": 2}),
               ("vcache dma", "vcache", O, {"vcache_dma": 1}),

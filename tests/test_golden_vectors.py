@@ -99,7 +99,7 @@ def test_product_vector_generator_matches_numpy():
 
 
 # ------------------------------------------------------------------ GPU
-ORDERED = ["vcache", "csr_lane"]
+ORDERED = ["vcache", "csr_lane", "sell"]
 
 
 @pytest.mark.gpu
@@ -144,7 +144,7 @@ def test_gpu_synthetic_vectors_ordered(gpu, name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kernel,mode", [("auto", hs.MODE_ORDERED), ("vcache_split", hs.MODE_FAST),
-                                         ("vcache", hs.MODE_ORDERED)])
+                                         ("vcache", hs.MODE_ORDERED), ("sell", hs.MODE_FAST)])
 def test_gpu_row_partition_bit_identical(gpu, kernel, mode):
     """Row shards (the multi-GPU layout) give bit-identical rows to one
     unpartitioned run: no arithmetic depends on where a shard starts."""

@@ -38,7 +38,7 @@ def test_multi_ordered_matches_oracle(gpu, name, ndev, beta):
 
 
 @pytest.mark.parametrize("kernel,mode", [("vcache_split", hs.MODE_FAST), ("csr_vector", hs.MODE_FAST),
-                                         ("vcache", hs.MODE_ORDERED)])
+                                         ("vcache", hs.MODE_ORDERED), ("sell", hs.MODE_ORDERED)])
 def test_multi_equals_single_device(gpu, kernel, mode):
     n = 1 << 17
     rowptr, colind, vals = hs.gen_stripe_csr(0, n, 1 << 20, 32)

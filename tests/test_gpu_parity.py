@@ -16,7 +16,7 @@ import oracle
 
 pytestmark = pytest.mark.gpu
 
-ORDERED_KERNELS = ["vcache", "csr_lane"]
+ORDERED_KERNELS = ["vcache", "csr_lane", "sell"]
 
 
 def _fast_bound(rowptr_len, absprod, yin):
@@ -58,7 +58,7 @@ def _check(name, rows, cols, colptr, rowind, vals, x, kernel, beta, mode=hs.MODE
 
 
 @pytest.mark.parametrize("name", fx.ALL_FIXTURES)
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
 @pytest.mark.parametrize("beta", [0, 1])
 def test_fixtures(gpu, name, kernel, beta):
     rows, cols, colptr, rowind, vals = fx.load(name)
@@ -94,7 +94,7 @@ def _random_csc(rows, cols, density, rng, dtype=np.float64, empty_rows=True, lon
 
 
 @pytest.mark.parametrize("shape", [(1, 1), (1, 300), (300, 1), (257, 1000), (5000, 333), (3000, 20000)])
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
 def test_random_ragged(gpu, shape, kernel):
     rng = np.random.default_rng(shape[0] * 31 + shape[1])
     rows, cols = shape
@@ -106,7 +106,7 @@ def test_random_ragged(gpu, shape, kernel):
         _check(f"rand{shape}", rows, cols, colptr, rowind, vals, x, kernel, beta, mode)
 
 
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
 def test_random_u64_wraparound(gpu, kernel):
     rng = np.random.default_rng(5)
     rows, cols = 4000, 9000
@@ -285,7 +285,7 @@ def test_experimental_vcache_variants(gpu, kernel, dma, xlane):
 # ---- analogues of the backend known-answer test (chisel/tests/TestSpMVBackend.scala:122-178):
 # write-out mode (rows come back unchanged: y_in -> y_out with nothing to add) and the stream
 # sums sumUpTo(64) = 2080 carried by the nonzero-value stream and by the input-vector stream.
-@pytest.mark.parametrize("kernel", ["auto", "vcache", "csr_lane", "csr_vector", "vcache_split"])
+@pytest.mark.parametrize("kernel", ["auto", "vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
 def test_backend_kat_writeout_empty_matrix(gpu, kernel):
     rows = cols = 64
     colptr = np.zeros(cols + 1, np.uint32)
@@ -307,7 +307,7 @@ def test_backend_kat_writeout_empty_matrix(gpu, kernel):
         assert not y0.any()
 
 
-@pytest.mark.parametrize("kernel", ["auto", "vcache", "csr_lane", "csr_vector", "vcache_split"])
+@pytest.mark.parametrize("kernel", ["auto", "vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
 def test_backend_kat_stream_sums(gpu, kernel):
     n = 64
     # value stream i+1 in one row, x = 1: y0 = sumUpTo(64)
@@ -336,3 +336,40 @@ def test_integration_example_program(gpu):
     lines = [l for l in out.stdout.splitlines() if l.startswith("HIPSpMV")]
     assert len(lines) == 2 and all("diffFromGolden=0" in l for l in lines), out.stdout
     assert "devices=1" in lines[0] and "devices=3" in lines[1]
+
+
+# ---- k_sell (csrc/sell.hip): SELL-C-sigma lane per row, hub rows one wave each.
+# Its layout and index arithmetic are replayed on the CPU by tests/test_sell_sim.py.
+def test_sell_rmat_hubs_ordered_and_fast(gpu):
+    rowptr, colind, vals = hs.gen_rmat_csr(15)
+    n = 1 << 15
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    h.set_kernel("sell")
+    assert h.kernel_name(hs.MODE_ORDERED) == "sell" and h.stat("sell_hubs") > 0
+    colptr, rowind, cvals = oracle.csr2csc(n, n, rowptr, colind, vals)
+    x = hs.gen_vector(n, 3)
+    lens = np.diff(rowptr.astype(np.int64))
+    absprod = np.bincount(np.repeat(np.arange(n), lens), weights=np.abs(vals * x[colind]), minlength=n)
+    for beta in (0, 1):
+        y0 = np.random.default_rng(beta).uniform(-1, 1, n)
+        y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else None), rows=n)
+        y = h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_ORDERED)
+        assert y.tobytes() == y_ref.tobytes(), beta
+        yf = [h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST) for _ in range(2)]
+        assert yf[0].tobytes() == yf[1].tobytes()  # deterministic
+        bound = _fast_bound(lens + 1, absprod, y0 if beta else np.zeros(n))
+        assert np.all(np.abs(yf[0] - y_ref) <= bound), beta
+    h.close()
+
+
+def test_sell_c3_full_size_ordered(gpu):
+    n = 1 << 20
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+    colptr, rowind, cvals = oracle.csr2csc(n, n, rowptr, colind, vals)
+    x = hs.gen_vector(n, 3)
+    y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=n)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    h.set_kernel("sell")
+    assert h.stat("sell_padding") == 0 and h.stat("sell_hubs") == 0
+    assert h.exec(x, beta=0, mode=hs.MODE_ORDERED).tobytes() == y_ref.tobytes()
+    h.close()
