@@ -103,7 +103,8 @@ int main(int argc, char** argv) {
       kernel = k == "vcache" ? HIPSPMV_KERNEL_VCACHE
                : k == "vcache_split" ? HIPSPMV_KERNEL_VCACHE_SPLIT
                : k == "csr_lane" ? HIPSPMV_KERNEL_CSR_LANE
-               : k == "csr_vector" ? HIPSPMV_KERNEL_CSR_VECTOR : HIPSPMV_KERNEL_AUTO;
+               : k == "csr_vector" ? HIPSPMV_KERNEL_CSR_VECTOR
+               : k == "sell" ? HIPSPMV_KERNEL_SELL : HIPSPMV_KERNEL_AUTO;
     } else if (a == "--reps") reps = std::atoi(next().c_str());
     else if (a == "--cms") { cms = std::atoi(next().c_str()) != 0; haveCms = true; }
     else if (a == "--confs") {

@@ -373,3 +373,19 @@ def test_sell_c3_full_size_ordered(gpu):
     assert h.stat("sell_padding") == 0 and h.stat("sell_hubs") == 0
     assert h.exec(x, beta=0, mode=hs.MODE_ORDERED).tobytes() == y_ref.tobytes()
     h.close()
+
+
+def test_plugin_surface_spmvbench_sell(gpu):
+    # the plugin pipeline with the SELL kernel register, one device and three
+    import subprocess
+    names = fx.ALL_FIXTURES
+    out = subprocess.run([f"{hs.LIB_DIR}/spmvbench", "--dir", fx.MATRICES, "--confs", "hip,hip3", "--cms", "1",
+                          "--kernel", "sell", *names], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = out.stdout.splitlines()
+    hdr = next(l for l in lines if l.startswith("diffFromGolden,"))
+    keys = hdr.rstrip(",").split(",")
+    recs = [dict(zip(keys, l.rstrip(",").split(","))) for l in lines if l[:1].isdigit()]
+    assert len(recs) == 2 * len(names)
+    for r in recs:
+        assert r["diffFromGolden"] == "0" and r["error"] == "0" and r["kernel"] == "7", r
