@@ -228,6 +228,27 @@ def main():
         torch.cuda.synchronize()
         bcast_us = (time.perf_counter() - tb) / reps * 1e6
     yd = torch.empty(rows, dtype=torch.float64, device=dev)
+    # Square, strong-scaled matrices (C4/C5): when y feeds the next x (power
+    # iteration), the exchange is an allgather of the y slices into every
+    # rank's x; slices are padded to the longest for the
+    # collective.  Timed outside the step, like the broadcast.
+    gather_us = None
+    if dist is not None and a.workload in ("c4", "c5"):
+        rmax_t = torch.tensor([rows], dtype=torch.int64, device=dev)
+        dist.all_reduce(rmax_t, op=dist.ReduceOp.MAX)
+        rmax = int(rmax_t.item())
+        ys = torch.zeros(rmax, dtype=torch.float64, device=dev)
+        xg = torch.empty(rmax * world, dtype=torch.float64, device=dev)
+        for _ in range(3):
+            dist.all_gather_into_tensor(xg, ys)
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg = time.perf_counter()
+        for _ in range(10):
+            dist.all_gather_into_tensor(xg, ys)
+        torch.cuda.synchronize()
+        gather_us = (time.perf_counter() - tg) / 10 * 1e6
+        del ys, xg
     stream = torch.cuda.current_stream(dev)
 
     def timed(mode: int):
@@ -400,6 +421,10 @@ def main():
             "end_to_end": None if bcast_us is None else {
                 "value": round(total_flops / (ms_per_step * 1e-3 + bcast_us * 1e-6) / 1e9, 2), "unit": "GFLOP/s",
                 "ms_per_step": round(ms_per_step + bcast_us * 1e-3, 5), "includes": "one RCCL x broadcast per step"},
+            "y_allgather_us": None if gather_us is None else round(gather_us, 2),
+            "iterative": None if gather_us is None else {
+                "value": round(total_flops / (ms_per_step * 1e-3 + gather_us * 1e-6) / 1e9, 2), "unit": "GFLOP/s",
+                "includes": "SpMV + RCCL allgather of the y slices into the next x (power iteration)"},
             "pcie_us": {"x_h2d": round(h2d_us, 2), "y_d2h": round(d2h_us, 2),
                         "note": "host-buffer path legs (hipspmv_exec), not in value"},
             "rank_kernel_us": [round(v * 1e3, 3) for v in rank_kern_ms],

@@ -180,6 +180,7 @@ def test_bench_strong_workloads_gloo(workload, scale):
     out = res[0]
     assert res[1] is None and out["n_gpus"] == 2 and out["scaling"] == "strong"
     assert len(out["rank_kernel_us"]) == 2
+    assert out["y_allgather_us"] > 0 and out["iterative"]["value"] <= out["value"]
     # the two shards together are the whole matrix
     if workload == "c4":
         assert out["config"]["nnz_total"] == 32 << scale and out["config"]["rows_per_gpu"] == 1 << (scale - 1)
