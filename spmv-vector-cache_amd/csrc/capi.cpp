@@ -189,14 +189,23 @@ static int build_sell_layout(hipspmv_t* h) {
   }
   SellLayout L;
   build_sell(a, L);
+  const uint64_t bytes0 = h->device_bytes;
+  auto fail = [&](int st) {  // a later attempt starts from nothing
+    void* sp[] = {q.d_off, q.d_width, q.d_row, q.d_len, q.d_col, q.d_hubs, q.d_vals};
+    for (void* p : sp)
+      if (p) (void)hipFree(p);
+    q = hipspmv_handle::Sell{};
+    h->device_bytes = bytes0;
+    return st;
+  };
   int st;
-  if ((st = dev_upload(&q.d_off, L.off.data(), L.off.size(), h->device_bytes))) return st;
-  if ((st = dev_upload(&q.d_width, L.width.data(), L.width.size(), h->device_bytes))) return st;
-  if ((st = dev_upload(&q.d_row, L.row.data(), L.row.size(), h->device_bytes))) return st;
-  if ((st = dev_upload(&q.d_len, L.len.data(), L.len.size(), h->device_bytes))) return st;
-  if ((st = dev_upload(&q.d_col, L.col.data(), L.col.size(), h->device_bytes))) return st;
-  if ((st = dev_upload(&q.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return st;
-  if ((st = dev_upload(&q.d_hubs, L.hubs.data(), L.hubs.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&q.d_off, L.off.data(), L.off.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&q.d_width, L.width.data(), L.width.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&q.d_row, L.row.data(), L.row.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&q.d_len, L.len.data(), L.len.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&q.d_col, L.col.data(), L.col.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&q.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&q.d_hubs, L.hubs.data(), L.hubs.size(), h->device_bytes))) return fail(st);
   q.nslices = L.nslices;
   q.nhubs = L.nhubs;
   q.padding = L.padding;
