@@ -1,0 +1,83 @@
+"""BASELINE.json's two largest single-GPU configurations at full size:
+C4 (2^24 x 2^24 stripe, 32 nnz/row, 537 M nonzeros) and C5 (R-MAT scale 24,
+263 M nonzeros, longest row 238,554 entries).  The CPU oracle would need
+minutes and ~20 GB per run at these sizes, so the checks are size-independent:
+a sample of rows (first, last, the longest, 2,000 random) is recomputed
+sequentially in Python floats -- products rounded, then added in ascending
+column order, exactly SoftwareSpMV's arithmetic (SoftwareSpMV.cpp:59-64) --
+and ORDERED results must match those rows bit for bit, FAST results the
+per-row bound of include/hipspmv.h; runs are deterministic.  Exercises the
+64-bit entry offsets of every kernel and the hub-row path of k_sell."""
+import numpy as np
+import pytest
+
+import hipspmv as hs
+
+pytestmark = pytest.mark.gpu
+
+
+def _sample(rowptr, n, k=2000):
+    lens = np.diff(rowptr.astype(np.int64))
+    rows = np.concatenate([[0, 1, n - 1, int(np.argmax(lens))], np.random.default_rng(7).integers(0, n, k)])
+    return np.unique(rows)
+
+
+def _sequential(rowptr, colind, vals, x, rows):
+    want, absprod = [], []
+    for r in rows:
+        acc, ap = 0.0, 0.0
+        for e in range(int(rowptr[r]), int(rowptr[r + 1])):
+            p = float(vals[e]) * float(x[colind[e]])
+            acc = acc + p
+            ap = ap + abs(p)
+        want.append(acc)
+        absprod.append(ap)
+    return np.array(want), np.array(absprod)
+
+
+def _check(h, x, rows, want, absprod, lens, kernel, mode):
+    if kernel != "auto":
+        h.set_kernel(kernel)
+    y1 = h.exec(x, beta=0, mode=mode)
+    y2 = h.exec(x, beta=0, mode=mode)
+    assert y1.tobytes() == y2.tobytes(), (kernel, mode)  # deterministic
+    got = y1[rows]
+    if mode == hs.MODE_ORDERED:
+        bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
+        assert bad.size == 0, (kernel, h.kernel_name(mode), rows[bad[:5]])
+    else:
+        bound = 2.0 * np.maximum(lens[rows], 1) * 2.0 ** -53 * absprod + 1e-300
+        assert np.all(np.abs(got - want) <= bound), (kernel, h.kernel_name(mode))
+    return h.kernel_name(mode)
+
+
+def _case(gen):
+    n, rowptr, colind, vals = gen()
+    x = hs.gen_vector(n, 3)
+    rows = _sample(rowptr, n)
+    want, absprod = _sequential(rowptr, colind, vals, x, rows)
+    lens = np.diff(rowptr.astype(np.int64))
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    return h, x, rows, want, absprod, lens
+
+
+@pytest.fixture(scope="module")
+def c4(gpu):
+    case = _case(lambda: (1 << 24, *hs.gen_stripe_csr(0, 1 << 24, 1 << 24, 32)))
+    yield case
+    case[0].close()
+
+
+@pytest.fixture(scope="module")
+def c5(gpu):
+    case = _case(lambda: (1 << 24, *hs.gen_rmat_csr(24)))
+    yield case
+    case[0].close()
+
+
+@pytest.mark.parametrize("kernel,mode", [("auto", hs.MODE_ORDERED), ("auto", hs.MODE_FAST),
+                                         ("sell", hs.MODE_ORDERED), ("sell", hs.MODE_FAST)])
+@pytest.mark.parametrize("which", ["c4", "c5"])
+def test_full_size_sampled_rows(request, which, kernel, mode):
+    h, x, rows, want, absprod, lens = request.getfixturevalue(which)
+    _check(h, x, rows, want, absprod, lens, kernel, mode)
