@@ -83,8 +83,9 @@ struct hipspmv_handle {
     bool built = false;
     uint64_t* d_off = nullptr;
     uint32_t *d_width = nullptr, *d_row = nullptr, *d_len = nullptr, *d_col = nullptr, *d_hubs = nullptr;
-    uint64_t* d_vals = nullptr;
-    uint32_t nslices = 0, nhubs = 0;
+    uint32_t *d_pieces = nullptr, *d_tickets = nullptr;
+    uint64_t *d_vals = nullptr, *d_partial = nullptr;
+    uint32_t nslices = 0, nhubs = 0, npieces = 0;
     uint64_t padding = 0;
   } sell;
   int vcache_dma = 0;    // option "vcache_dma": LDS-DMA x loader (experimental)
@@ -111,7 +112,8 @@ static void release(hipspmv_t* h) {
   }
   {
     auto& q = h->sell;
-    void* sp[] = {q.d_off, q.d_width, q.d_row, q.d_len, q.d_col, q.d_hubs, q.d_vals};
+    void* sp[] = {q.d_off, q.d_width, q.d_row, q.d_len, q.d_col, q.d_hubs, q.d_vals, q.d_pieces, q.d_tickets,
+                  q.d_partial};
     for (void* p : sp)
       if (p) (void)hipFree(p);
   }
@@ -191,7 +193,8 @@ static int build_sell_layout(hipspmv_t* h) {
   build_sell(a, L);
   const uint64_t bytes0 = h->device_bytes;
   auto fail = [&](int st) {  // a later attempt starts from nothing
-    void* sp[] = {q.d_off, q.d_width, q.d_row, q.d_len, q.d_col, q.d_hubs, q.d_vals};
+    void* sp[] = {q.d_off, q.d_width, q.d_row, q.d_len, q.d_col, q.d_hubs, q.d_vals, q.d_pieces, q.d_tickets,
+                  q.d_partial};
     for (void* p : sp)
       if (p) (void)hipFree(p);
     q = hipspmv_handle::Sell{};
@@ -206,6 +209,14 @@ static int build_sell_layout(hipspmv_t* h) {
   if ((st = dev_upload(&q.d_col, L.col.data(), L.col.size(), h->device_bytes))) return fail(st);
   if ((st = dev_upload(&q.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return fail(st);
   if ((st = dev_upload(&q.d_hubs, L.hubs.data(), L.hubs.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&q.d_pieces, L.pieces.data(), L.pieces.size(), h->device_bytes))) return fail(st);
+  {
+    const std::vector<uint32_t> zeros(L.ntickets, 0u);  // tickets self-reset after each launch
+    if ((st = dev_upload(&q.d_tickets, zeros.data(), zeros.size(), h->device_bytes))) return fail(st);
+    const std::vector<uint64_t> none(L.npieces, 0u);
+    if ((st = dev_upload(&q.d_partial, none.data(), none.size(), h->device_bytes))) return fail(st);
+  }
+  q.npieces = L.npieces;
   q.nslices = L.nslices;
   q.nhubs = L.nhubs;
   q.padding = L.padding;
@@ -294,9 +305,10 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   if (mode == HIPSPMV_MODE_AUTO) mode = h->mode_opt;
   if (kernel == HIPSPMV_KERNEL_SELL) {
     const auto& q = h->sell;
-    SellArgs a{q.d_off,     q.d_width, q.d_row,     q.d_len, q.d_col, q.d_vals,  q.d_hubs,
-               h->d_rowptr, h->d_colind, h->d_vals, d_x,     d_y_in,  d_y_out,   q.nslices,
-               q.nhubs,     beta,      mode == HIPSPMV_MODE_ORDERED ? 1 : 0};
+    SellArgs a{q.d_off,     q.d_width,   q.d_row,     q.d_len, q.d_col,  q.d_vals,
+               q.d_hubs,    h->d_rowptr, h->d_colind, h->d_vals, d_x,    d_y_in,
+               d_y_out,     q.nslices,   q.nhubs,     beta,    mode == HIPSPMV_MODE_ORDERED ? 1 : 0,
+               q.d_pieces,  q.npieces,   q.d_partial, q.d_tickets};
     e = launch_sell(h->dtype, a, s);
   } else if (kernel == HIPSPMV_KERNEL_VCACHE || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ||
       kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
@@ -491,6 +503,7 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "vcache_split4_x_bytes") *out = h->vc[2].ok ? 8ull * h->vc[2].nblocks * h->cols : 0;
   else if (k == "sell_slices") *out = h->sell.nslices;
   else if (k == "sell_hubs") *out = h->sell.nhubs;
+  else if (k == "sell_hub_pieces") *out = h->sell.npieces;
   else if (k == "sell_padding") *out = h->sell.padding;
   else if (k == "row_groups") *out = h->ngroups;
   else if (k == "max_row_len") *out = h->max_row_len;

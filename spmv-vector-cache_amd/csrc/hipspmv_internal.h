@@ -55,6 +55,13 @@ constexpr int kSellRows = 256;
 constexpr uint32_t kSellSigma = 65536;
 constexpr uint32_t kSellHub = 256;
 constexpr uint32_t kSellNoRow = 0xFFFFFFFFu;
+// FAST / u64: a hub row is cut into pieces of at most kSellPiece entries, one
+// wave each; the wave that finishes a row's last piece (ticket) adds the
+// piece partials in piece order (deterministic).  Piece record, 8 x u32:
+// row, first entry (within the row), entries, piece index, pieces of the row,
+// ticket index, 0, 0.
+constexpr uint32_t kSellPiece = 4096;
+constexpr int kSellPieceWords = 8;
 
 struct HostCSR {
   uint32_t rows = 0, cols = 0, nnz = 0;
@@ -81,7 +88,9 @@ struct SellLayout {
   std::vector<uint32_t> len;    // nslices * kSellRows: row length (0 for kSellNoRow)
   std::vector<uint32_t> col;    // off[nslices] entries; padding: column 0
   std::vector<uint64_t> vals;   // padding: 0 (never added: k < len selects)
-  std::vector<uint32_t> hubs;   // hub rows, longest first
+  std::vector<uint32_t> hubs;   // hub rows, longest first (ORDERED: one wave each)
+  std::vector<uint32_t> pieces; // FAST: kSellPieceWords per piece, pieces of a row contiguous
+  uint32_t npieces = 0, ntickets = 0;
   uint64_t padding = 0;         // padded entries (off[nslices] - nnz of the slices)
 };
 

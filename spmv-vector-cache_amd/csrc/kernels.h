@@ -53,6 +53,10 @@ struct SellArgs {
   uint32_t nslices, nhubs;
   int beta;
   int exact;  // 1: hub rows summed in one sequential chain (ORDERED f64)
+  const uint32_t* pieces = nullptr;  // exact == 0: hub-row pieces (kSellPieceWords each)
+  uint32_t npieces = 0;
+  void* partial = nullptr;      // [npieces] piece partials
+  uint32_t* tickets = nullptr;  // per split row, zero between launches
 };
 
 hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);

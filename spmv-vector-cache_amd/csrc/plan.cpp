@@ -217,6 +217,17 @@ void build_sell(const HostCSR& a, SellLayout& out) {
   uint64_t hub_nnz = 0;
   for (uint32_t r : hubs) hub_nnz += a.rowptr[r + 1] - a.rowptr[r];
   out.padding = out.off.back() - (a.nnz - hub_nnz);
+  for (uint32_t r : hubs) {  // FAST pieces: near-equal cuts of at most kSellPiece entries
+    const uint32_t n = a.rowptr[r + 1] - a.rowptr[r];
+    const uint32_t np = (n + kSellPiece - 1) / kSellPiece;
+    const uint32_t ticket = np > 1 ? out.ntickets++ : 0u;
+    for (uint32_t p = 0; p < np; ++p) {
+      const uint32_t b = (uint32_t)((uint64_t)n * p / np), e = (uint32_t)((uint64_t)n * (p + 1) / np);
+      const uint32_t rec[kSellPieceWords] = {r, b, e - b, p, np, ticket, 0u, 0u};
+      out.pieces.insert(out.pieces.end(), rec, rec + kSellPieceWords);
+    }
+  }
+  out.npieces = (uint32_t)(out.pieces.size() / kSellPieceWords);
   out.hubs = std::move(hubs);
   out.nhubs = (uint32_t)out.hubs.size();
   out.nslices = (uint32_t)out.width.size();

@@ -16,11 +16,13 @@
 //   rows sorted by length inside windows of kSellSigma rows, so a slice's
 //   rows have similar lengths (little padding); padded steps are loaded
 //   (column 0, value 0: branch-free, coalesced) but never added.
-//   hub rows (> kSellHub entries) -- one wave each over the CSR copy:
-//   entries loaded 256 at a time two stages ahead; ORDERED f64 sums the
-//   products in one sequential chain through v_readlane (the order is the
-//   contract); FAST / u64 keeps four lane partials and a fixed xor-shuffle
-//   tree (deterministic).
+//   hub rows (> kSellHub entries) -- over the CSR copy, entries loaded 256
+//   at a time two stages ahead: ORDERED f64 gives each hub row one wave that
+//   sums the products in one sequential chain through v_readlane (the order
+//   is the contract); FAST / u64 cuts hub rows into pieces of <= 4096
+//   entries, one wave each (four lane partials + a fixed xor tree), and the
+//   last piece to finish adds the piece partials in piece order
+//   (deterministic).
 //
 // Bytes per launch: 12 B per entry (padding included) + 8 B per slice row
 // (row id, length) + 8 B per row of y written; x gathered from L2/MALL.
@@ -58,14 +60,16 @@ __device__ __forceinline__ T xor_shuffle(T v, int m) {
   return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
 }
 
-// One hub row r (n > kSellHub entries, so n >= kHubStage + 1), the whole wave.
+// The n >= 1 entries [base, base + n) of one row, the whole wave.  EXACT: the
+// products added one after another to `acc` (the row's sequential chain; the
+// result is wave-uniform).  Otherwise: four lane partials, then a fixed xor
+// tree (every lane returns the same total; `acc` unused).
 template <typename T, bool EXACT>
-__device__ __forceinline__ void hub_row(const SellArgs& a, uint32_t r, int lane) {
+__device__ __forceinline__ T hub_entries(const SellArgs& a, uint32_t base, uint32_t n, T acc, int lane) {
 #pragma clang fp contract(off)
   const T* __restrict__ vals = static_cast<const T*>(a.csr_vals);
   const T* __restrict__ x = static_cast<const T*>(a.x);
-  const uint32_t base = a.rowptr[r], n = a.rowptr[r + 1] - base;
-  // entries of the stage starting at g0, indices clamped into the row (the
+  // entries of the stage starting at g0, indices clamped into the range (the
   // clamped copies are loaded but never consumed)
   auto load = [&](uint32_t g0, uint32_t* c, T* v) {
 #pragma unroll
@@ -83,7 +87,6 @@ __device__ __forceinline__ void hub_row(const SellArgs& a, uint32_t r, int lane)
 #pragma unroll
   for (int j = 0; j < kHubG; ++j) p[j] = vA[j] * xs[j];  // stage 0 products (rounded)
   load(kHubStage, cA, vA);                              // stage 1 entries
-  T acc = EXACT && a.beta ? static_cast<const T*>(a.y_in)[r] : T(0);  // the chain starts from y_in
   T part[kHubG];
 #pragma unroll
   for (int j = 0; j < kHubG; ++j) part[j] = T(0);
@@ -103,7 +106,7 @@ __device__ __forceinline__ void hub_row(const SellArgs& a, uint32_t r, int lane)
 #pragma unroll
           for (int l = 0; l < 64; ++l) acc = acc + lane_value(p[j], (uint32_t)l);
         }
-      } else {  // the row's last stage
+      } else {  // the last stage
 #pragma unroll
         for (int j = 0; j < kHubG; ++j) {
           const uint32_t mj = m > (uint32_t)j * 64 ? min(64u, m - (uint32_t)j * 64) : 0u;
@@ -122,14 +125,50 @@ __device__ __forceinline__ void hub_row(const SellArgs& a, uint32_t r, int lane)
       vA[j] = vB[j];
     }
   }
-  if (EXACT) {
-    if (lane == 0) static_cast<T*>(a.y_out)[r] = acc;
-  } else {
-    T s = (part[0] + part[1]) + (part[2] + part[3]);
+  if (EXACT) return acc;
+  T s = (part[0] + part[1]) + (part[2] + part[3]);
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) s = s + xor_shuffle(s, d);  // every lane: the same total
-    if (lane == 0) static_cast<T*>(a.y_out)[r] = a.beta ? static_cast<const T*>(a.y_in)[r] + s : s;
+  for (int d = 32; d >= 1; d >>= 1) s = s + xor_shuffle(s, d);  // every lane: the same total
+  return s;
+}
+
+// ORDERED f64: hub row r in one wave, one chain from y_in (or +0.0).
+template <typename T>
+__device__ __forceinline__ void hub_row_exact(const SellArgs& a, uint32_t r, int lane) {
+  const uint32_t base = a.rowptr[r], n = a.rowptr[r + 1] - base;
+  const T acc0 = a.beta ? static_cast<const T*>(a.y_in)[r] : T(0);
+  const T acc = hub_entries<T, true>(a, base, n, acc0, lane);
+  if (lane == 0) static_cast<T*>(a.y_out)[r] = acc;
+}
+
+// FAST / u64: one piece of a hub row.  A row in several pieces is finished by
+// the wave whose ticket add returns np - 1: it adds the piece partials in
+// piece order.  Hand-off as in k_vcache's split combine (MI355X_MICROARCH.md,
+// "Valid forms" row 1): agent-scope (sc1) store of the partial, vmcnt(0),
+// agent-scope ticket add; the last arriver reads the partials with
+// agent-scope loads and resets the ticket for the next launch.
+template <typename T>
+__device__ __forceinline__ void hub_piece(const SellArgs& a, uint32_t pid, int lane) {
+#pragma clang fp contract(off)
+  const uint32_t* pc = a.pieces + (size_t)pid * kSellPieceWords;
+  const uint32_t r = pc[0], begin = pc[1], n = pc[2], idx = pc[3], np = pc[4], tk = pc[5];
+  const T s = hub_entries<T, false>(a, a.rowptr[r] + begin, n, T(0), lane);
+  if (lane != 0) return;
+  T* y = static_cast<T*>(a.y_out);
+  if (np == 1) {
+    y[r] = a.beta ? static_cast<const T*>(a.y_in)[r] + s : s;
+    return;
   }
+  uint64_t* parts = static_cast<uint64_t*>(a.partial) + (pid - idx);
+  __hip_atomic_store(parts + idx, __builtin_bit_cast(uint64_t, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint32_t old = __hip_atomic_fetch_add(a.tickets + tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old != np - 1) return;
+  __hip_atomic_store(a.tickets + tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  T t = __builtin_bit_cast(T, __hip_atomic_load(parts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (uint32_t q = 1; q < np; ++q)
+    t = t + __builtin_bit_cast(T, __hip_atomic_load(parts + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  y[r] = a.beta ? static_cast<const T*>(a.y_in)[r] + t : t;
 }
 
 // One slice s: lane `lane` sums rows row[s][j*64 + lane], j = 0..3.
@@ -213,22 +252,27 @@ __device__ __forceinline__ void slice_rows(const SellArgs& a, uint32_t s, int la
     if (r[j] != kSellNoRow) static_cast<T*>(a.y_out)[r[j]] = acc[j];
 }
 
-// Waves [0, nhubs) take the hub rows (longest first), the rest one slice each.
+// Waves [0, H) take the hub work -- EXACT: the hub rows (longest first), one
+// wave each; otherwise the hub-row pieces -- and the rest one slice each.
 template <typename T, bool EXACT>
 __global__ __launch_bounds__(256) void k_sell(const SellArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t w = blockIdx.x * 4 + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (w < a.nhubs) {
-    hub_row<T, EXACT>(a, a.hubs[w], lane);
+  const uint32_t H = EXACT ? a.nhubs : a.npieces;
+  if (w < H) {
+    if (EXACT)
+      hub_row_exact<T>(a, a.hubs[w], lane);
+    else
+      hub_piece<T>(a, w, lane);
     return;
   }
-  const uint32_t s = w - a.nhubs;
+  const uint32_t s = w - H;
   if (s < a.nslices) slice_rows<T>(a, s, lane);
 }
 
 template <typename T, bool EXACT>
 hipError_t launch(const SellArgs& a, hipStream_t s) {
-  const uint64_t waves = (uint64_t)a.nhubs + a.nslices;
+  const uint64_t waves = (uint64_t)(EXACT ? a.nhubs : a.npieces) + a.nslices;
   if (waves == 0) return hipSuccess;
   hipLaunchKernelGGL((k_sell<T, EXACT>), dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
   return hipGetLastError();

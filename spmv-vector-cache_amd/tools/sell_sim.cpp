@@ -49,32 +49,27 @@ static std::vector<T> replay(const HostCSR& a, const SellLayout& L, const std::v
   std::vector<T> y(a.rows, T(0));
   writes.assign(a.rows, 0);
   auto xv = [&](uint32_t c) { return at(x, c, "x gather"); };
-  // hub waves
-  for (uint32_t w = 0; w < L.nhubs; ++w) {
-    const uint32_t r = at(L.hubs, w, "hubs");
-    const uint32_t base = at(a.rowptr, r, "rowptr"), n = at(a.rowptr, (uint64_t)r + 1, "rowptr") - base;
-    if (n <= kSellHub) violation("hub row too short", n, kSellHub);
+  // the hub-entry routine (hub_entries): EXACT chain from acc, or lane
+  // partials + xor tree; loads at the kernel's clamped indices
+  auto hub_entries = [&](uint32_t base, uint32_t n, T acc, bool chain) -> T {
     const uint32_t S = 256;
     auto entry = [&](uint32_t g0, int j, int lane, uint32_t& c, T& v) {
       const uint32_t e = std::min<uint32_t>(g0 + j * 64 + lane, n - 1);
       c = at(a.colind, (uint64_t)base + e, "hub colind");
       v = bits<T>(at(a.vals, (uint64_t)base + e, "hub vals"));
     };
-    // loads the kernel issues beyond the products it consumes (prologue
-    // stage 1 and the stage two ahead) -- bounds only
-    T acc = exact && beta ? yin[r] : T(0);
     std::vector<std::array<T, 4>> part(64, {T(0), T(0), T(0), T(0)});
     for (uint32_t g0 = 0; g0 < n; g0 += S) {
       for (int lane = 0; lane < 64; ++lane)
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 4; ++j) {  // prefetches: entries two stages ahead, gathers one ahead
           uint32_t c;
           T v;
-          entry(g0 + 2 * S, j, lane, c, v);  // prefetch (clamped)
+          entry(g0 + 2 * S, j, lane, c, v);
           entry(g0 + S, j, lane, c, v);
-          (void)xv(c);                       // next stage's gather
+          (void)xv(c);
         }
       const uint32_t m = std::min(S, n - g0);
-      if (exact) {
+      if (chain) {
         for (uint32_t i = 0; i < m; ++i) {
           uint32_t c;
           T v;
@@ -93,21 +88,58 @@ static std::vector<T> replay(const HostCSR& a, const SellLayout& L, const std::v
           }
       }
     }
-    if (exact) {
-      y[r] = acc;
-    } else {
-      std::array<T, 64> s;
-      for (int l = 0; l < 64; ++l) s[l] = (part[l][0] + part[l][1]) + (part[l][2] + part[l][3]);
-      for (int d = 32; d >= 1; d >>= 1) {
-        std::array<T, 64> t;
-        for (int l = 0; l < 64; ++l) t[l] = s[l] + s[l ^ d];
-        s = t;
-      }
-      for (int l = 1; l < 64; ++l)
-        if (std::memcmp(&s[l], &s[0], 8)) violation("xor tree lanes disagree", l, 64);
-      y[r] = beta ? yin[r] + s[0] : s[0];
+    if (chain) return acc;
+    std::array<T, 64> s;
+    for (int l = 0; l < 64; ++l) s[l] = (part[l][0] + part[l][1]) + (part[l][2] + part[l][3]);
+    for (int d = 32; d >= 1; d >>= 1) {
+      std::array<T, 64> t;
+      for (int l = 0; l < 64; ++l) t[l] = s[l] + s[l ^ d];
+      s = t;
     }
-    writes[r]++;
+    for (int l = 1; l < 64; ++l)
+      if (std::memcmp(&s[l], &s[0], 8)) violation("xor tree lanes disagree", l, 64);
+    return s[0];
+  };
+  if (exact) {  // hub rows, one wave each
+    for (uint32_t w = 0; w < L.nhubs; ++w) {
+      const uint32_t r = at(L.hubs, w, "hubs");
+      const uint32_t base = at(a.rowptr, r, "rowptr"), n = at(a.rowptr, (uint64_t)r + 1, "rowptr") - base;
+      if (n <= kSellHub) violation("hub row too short", n, kSellHub);
+      y[r] = hub_entries(base, n, beta ? yin[r] : T(0), true);
+      writes[r]++;
+    }
+  } else {  // hub pieces; a row's pieces contiguous, combined in piece order
+    std::vector<T> partial(L.npieces);
+    std::vector<uint32_t> covered(a.rows, 0);
+    for (uint32_t pid = 0; pid < L.npieces; ++pid) {
+      const uint64_t w0 = (uint64_t)pid * kSellPieceWords;
+      const uint32_t r = at(L.pieces, w0, "pieces"), begin = at(L.pieces, w0 + 1, "pieces"),
+                     n = at(L.pieces, w0 + 2, "pieces"), idx = at(L.pieces, w0 + 3, "pieces"),
+                     np = at(L.pieces, w0 + 4, "pieces"), tk = at(L.pieces, w0 + 5, "pieces");
+      if (r >= a.rows || n == 0 || n > kSellPiece || idx >= np || pid < idx ||
+          (np > 1 && tk >= L.ntickets)) {
+        violation("piece record", pid, L.npieces);
+        continue;
+      }
+      const uint32_t rb = a.rowptr[r], rn = a.rowptr[r + 1] - rb;
+      if (begin != covered[r] || begin + n > rn) violation("piece range", begin, rn);
+      covered[r] = begin + n;
+      const T s = hub_entries(rb + begin, n, T(0), false);
+      if (np == 1) {
+        y[r] = beta ? yin[r] + s : s;
+        writes[r]++;
+        continue;
+      }
+      partial[pid] = s;
+      if (idx == np - 1) {  // the combine reads every piece of the row in order, whoever arrives last
+        T t = partial[pid - idx];
+        for (uint32_t q = 1; q < np; ++q) t = t + partial[pid - idx + q];
+        y[r] = beta ? yin[r] + t : t;
+        writes[r]++;
+      }
+    }
+    for (uint32_t r : L.hubs)
+      if (covered[r] != a.rowptr[r + 1] - a.rowptr[r]) violation("hub row not covered by its pieces", r, a.rows);
   }
   // slice waves
   for (uint32_t s = 0; s < L.nslices; ++s) {
@@ -264,6 +296,12 @@ int main(int argc, char** argv) {
   {  // all rows empty; one row; one column
     cases.push_back({"empty 1000", from_lens(std::vector<uint32_t>(1000, 0), 17, 1)});
     cases.push_back({"single row 1x4000 (hub)", from_lens(std::vector<uint32_t>(1, 3000), 4000, 2)});
+    // hub rows in several FAST pieces (combine in piece order)
+    std::vector<uint32_t> lens(700, 3);
+    lens[0] = 20000;  // 5 pieces
+    lens[333] = 4097; // 2 pieces, the smallest split
+    lens[699] = 8192; // 2 full pieces
+    cases.push_back({"split hubs 700x30000", from_lens(lens, 30000, 4)});
     cases.push_back({"single column 300x1", from_lens(std::vector<uint32_t>(300, 1), 1, 3)});
   }
   int failures = 0;
@@ -305,10 +343,10 @@ int main(int argc, char** argv) {
         for (int w : writes) miswritten += w != 1;
         const bool ok = bad == 0 && miswritten == 0 && g_violations == 0;
         failures += !ok;
-        std::printf("%-26s %s beta=%d slices=%u hubs=%u padding=%llu: %s (%zu rows off, %zu rows not written once, "
+        std::printf("%-26s %s beta=%d slices=%u hubs=%u pieces=%u padding=%llu: %s (%zu rows off, %zu rows not written once, "
                     "%d violations)\n",
                     cs.name.c_str(), mode == 0 ? "f64-ordered" : mode == 1 ? "f64-fast" : "u64", beta, L.nslices,
-                    L.nhubs, (unsigned long long)L.padding, ok ? "ok" : "FAIL", bad, miswritten, g_violations);
+                    L.nhubs, L.npieces, (unsigned long long)L.padding, ok ? "ok" : "FAIL", bad, miswritten, g_violations);
       }
     }
   }

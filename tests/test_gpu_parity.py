@@ -389,3 +389,41 @@ def test_plugin_surface_spmvbench_sell(gpu):
     assert len(recs) == 2 * len(names)
     for r in recs:
         assert r["diffFromGolden"] == "0" and r["error"] == "0" and r["kernel"] == "7", r
+
+
+def test_sell_split_hub_rows_fast(gpu):
+    # FAST hub rows over 4096 entries are cut into pieces whose partials the
+    # last-finishing piece adds in piece order; tickets reset themselves, so
+    # repeated launches must give identical bits
+    rng = np.random.default_rng(21)
+    rows, cols = 700, 30000
+    lens = np.full(rows, 3)
+    lens[[0, 333, 699]] = [20000, 4097, 8192]
+    rowptr = np.zeros(rows + 1, np.uint32)
+    rowptr[1:] = np.cumsum(lens)
+    colind = np.concatenate([np.sort(rng.choice(cols, n, replace=False)) for n in lens]).astype(np.uint32)
+    vals = rng.uniform(-1, 1, colind.size)
+    x = rng.uniform(-1, 1, cols)
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+    h.set_kernel("sell")
+    assert h.stat("sell_hubs") == 3 and h.stat("sell_hub_pieces") == 9
+    colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+    absprod = np.bincount(np.repeat(np.arange(rows), lens), weights=np.abs(vals * x[colind]), minlength=rows)
+    for beta in (0, 1):
+        y0 = rng.uniform(-1, 1, rows)
+        y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else None), rows=rows)
+        ys = [h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST) for _ in range(3)]
+        assert ys[0].tobytes() == ys[1].tobytes() == ys[2].tobytes()
+        assert np.all(np.abs(ys[0] - y_ref) <= _fast_bound(lens + 1, absprod, y0 if beta else np.zeros(rows)))
+        assert h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_ORDERED).tobytes() == y_ref.tobytes()
+    # u64: pieces and combine are exact mod 2^64
+    vu = rng.integers(0, 2**64, colind.size, dtype=np.uint64)
+    xu = rng.integers(0, 2**64, cols, dtype=np.uint64)
+    hu = hs.Handle.from_csr(rowptr, colind, vu, rows, cols)
+    hu.set_kernel("sell")
+    cp, ri, cv = oracle.csr2csc(rows, cols, rowptr, colind, vu)
+    want = oracle.spmv_csc(cp, ri, cv, xu, rows=rows)
+    for _ in range(2):
+        assert hu.exec(xu, beta=0, mode=hs.MODE_FAST).tobytes() == want.tobytes()
+    h.close()
+    hu.close()

@@ -22,7 +22,8 @@ def _run(target, *args):
 
 def test_sell_replay():
     lines = _run("sell_sim")
-    assert len(lines) == 7 * 2 * 3
+    assert len(lines) == 8 * 2 * 3
+    assert any(l.startswith("split hubs") for l in lines)  # rows in several FAST pieces
     assert any("hubs=0" not in l for l in lines)  # the hub path is exercised
 
 
