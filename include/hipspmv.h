@@ -129,7 +129,8 @@ int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void 
  * "vcache_split_units" "vcache_split_rows_per_block" "vcache_x_bytes"
  * "vcache_split_x_bytes" (x bytes one launch streams into LDS)
  * "vcache_split4_eligible" "vcache_split4_x_bytes" "wgather_eligible"
- * "wgather_windows" "row_groups"
+ * "wgather_windows" "row_groups" "sell_slices" "sell_hubs" "sell_hub_pieces"
+ * "sell_padding" (SELL layout, 0 until the sell kernel is selected)
  * "max_row_len" "empty_rows" "execs". */
 int hipspmv_stat(hipspmv_t *h, const char *key, uint64_t *out);
 
