@@ -190,6 +190,9 @@ class Handle:
         else:
             raise TypeError("values must be float64 or uint64")
         vals = np.ascontiguousarray(vals)
+        if ptr.size != (rows if csr else cols) + 1 or vals.size != ind.size:
+            raise ValueError(f"{'rowptr' if csr else 'colptr'} needs {(rows if csr else cols) + 1} entries "
+                             f"(got {ptr.size}) and one value per index (got {vals.size} for {ind.size})")
         self.rows, self.cols, self.nnz = int(rows), int(cols), int(ind.size)
         self.device = device
         h = C.c_void_p()
@@ -222,7 +225,8 @@ class Handle:
         x = np.ascontiguousarray(x, dtype=npdt)
         if y is None:
             y = np.zeros(self.rows, dtype=npdt)
-        assert x.size == self.cols and y.size == self.rows and y.dtype == npdt and y.flags.c_contiguous
+        if x.size != self.cols or y.size != self.rows or y.dtype != npdt or not y.flags.c_contiguous:
+            raise ValueError(f"x needs {self.cols} and y {self.rows} contiguous {np.dtype(npdt).name} elements")
         _check(self._lib.hipspmv_exec(self._h, x.ctypes.data, y.ctypes.data, beta, mode), "hipspmv_exec")
         return y
 
@@ -231,6 +235,18 @@ class Handle:
         s = stream
         if s is not None and hasattr(s, "cuda_stream"):
             s = s.cuda_stream
+        # the C ABI takes raw pointers: a short or strided tensor would be read
+        # past its end on the device, so shapes are checked here
+        for name, t, n in (("x", x, self.cols), ("y_out", y_out, self.rows), ("y_in", y_in, self.rows)):
+            if t is None:
+                continue
+            if hasattr(t, "is_contiguous"):
+                ok = (t.numel() == n and t.is_contiguous() and t.element_size() == 8 and t.is_cuda
+                      and t.device.index == self.device)
+            else:
+                ok = False
+            if not ok:
+                raise ValueError(f"{name}: needs a contiguous 8-byte tensor of {n} elements on cuda:{self.device}")
         yin = _ptr(y_in) if y_in is not None else None
         _check(self._lib.hipspmv_exec_device(self._h, _ptr(x), yin, _ptr(y_out), beta, mode, s),
                "hipspmv_exec_device")
@@ -281,6 +297,8 @@ class MultiHandle:
         lib = load_hipspmv()
         self._keep = [np.ascontiguousarray(colptr, dtype=np.uint32), np.ascontiguousarray(rowind, dtype=np.uint32),
                       np.ascontiguousarray(vals)]
+        if self._keep[0].size != cols + 1 or self._keep[2].size != self._keep[1].size:
+            raise ValueError("colptr needs cols + 1 entries and one value per row index")
         self.dtype = self._keep[2].dtype
         self.rows, self.cols = rows, cols
         devs = (C.c_int * len(devices))(*devices)
@@ -299,6 +317,8 @@ class MultiHandle:
     def exec(self, x: np.ndarray, y: np.ndarray | None = None, beta: int = 0, mode: int = MODE_ORDERED):
         x = np.ascontiguousarray(x, dtype=self.dtype)
         y = np.zeros(self.rows, dtype=self.dtype) if y is None else np.ascontiguousarray(y, dtype=self.dtype)
+        if x.size != self.cols or y.size != self.rows:
+            raise ValueError(f"x needs {self.cols} and y {self.rows} elements")
         _check(load_hipspmv().hipspmv_multi_exec(self._h, _ptr(x), _ptr(y), beta, mode), "multi_exec")
         return y
 

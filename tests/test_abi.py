@@ -62,3 +62,14 @@ def test_integration_example_builds():
     import subprocess
     out = subprocess.run([os.path.join(hs.LIB_DIR, "plugin_example")], capture_output=True, text=True, timeout=60)
     assert out.returncode == 2 and "usage" in out.stderr
+
+
+def test_wrapper_rejects_mismatched_arrays():
+    # raw pointers cross the ABI, so the wrapper checks lengths before calling it
+    import numpy as np
+    import pytest
+    import hipspmv as hs
+    with pytest.raises(ValueError):
+        hs.Handle.from_csc(np.zeros(3, np.uint32), np.zeros(0, np.uint32), np.zeros(0), 4, 4)  # colptr short
+    with pytest.raises(ValueError):
+        hs.Handle.from_csr(np.array([0, 1], np.uint32), np.zeros(1, np.uint32), np.zeros(2), 1, 4)  # vals long

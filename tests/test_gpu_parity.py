@@ -427,3 +427,16 @@ def test_sell_split_hub_rows_fast(gpu):
         assert hu.exec(xu, beta=0, mode=hs.MODE_FAST).tobytes() == want.tobytes()
     h.close()
     hu.close()
+
+
+def test_exec_device_rejects_bad_tensors(gpu):
+    import torch
+    rows, cols, colptr, rowind, vals = fx.load("circuit204")
+    h = hs.Handle.from_csc(colptr, rowind, vals, rows, cols)
+    x = torch.zeros(cols, dtype=torch.float64, device=gpu)
+    y = torch.empty(rows, dtype=torch.float64, device=gpu)
+    for bad_x, bad_y in ((x[:-1], y), (x, y[:-1]), (x, torch.empty(2 * rows, dtype=torch.float64, device=gpu)[::2]),
+                         (x.cpu(), y), (x.float(), y)):
+        with pytest.raises(ValueError):
+            h.exec_device(bad_x, bad_y, beta=0, mode=hs.MODE_ORDERED)
+    h.close()
