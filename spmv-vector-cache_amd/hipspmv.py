@@ -299,6 +299,8 @@ class MultiHandle:
                       np.ascontiguousarray(vals)]
         if self._keep[0].size != cols + 1 or self._keep[2].size != self._keep[1].size:
             raise ValueError("colptr needs cols + 1 entries and one value per row index")
+        if self._keep[2].dtype not in (np.float64, np.uint64):
+            raise TypeError("values must be float64 or uint64")
         self.dtype = self._keep[2].dtype
         self.rows, self.cols = rows, cols
         devs = (C.c_int * len(devices))(*devices)
