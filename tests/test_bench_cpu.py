@@ -199,3 +199,12 @@ def test_bench_multi_rank_gloo():
     assert out["config"]["parallelism"].startswith("row-partition x2")
     # value is the whole-job rate: both ranks' flops over the max step time
     assert abs(out["value"] - 2 * 2 * out["config"]["nnz_per_gpu"] / (out["ms_per_step"] * 1e-3) / 1e9) < 0.02 * out["value"]
+
+
+def test_bench_four_ranks_gloo():
+    # more ranks than the GPU tests can use: rank r owns rows [r*2^10, (r+1)*2^10)
+    res = _multi_rank([], world=4)
+    out = res[0]
+    assert all(res[r] is None for r in (1, 2, 3))
+    assert out["n_gpus"] == 4 and len(out["rank_kernel_us"]) == 4
+    assert out["config"]["nnz_total"] == 4 * out["config"]["nnz_per_gpu"]
