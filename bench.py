@@ -70,9 +70,11 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true", help="skip timing the other mode")
-    p.add_argument("--vcache-xlane", type=int, default=0, choices=[0, 1, 2],
+    p.add_argument("--vcache-xlane", type=int, default=0, choices=[0, 1, 2, 3],
                    help="experimental vcache option (include/hipspmv.h); not the default path")
     p.add_argument("--vcache-dma", type=int, default=0, choices=[0, 1], help="experimental LDS-DMA x loader")
+    p.add_argument("--vcache-map", type=int, default=0, choices=[0, 1],
+                   help="experimental XCD-aware placement of vcache_split4's column parts")
     p.add_argument("--traffic-csv", default=None,
                    help="rocprofv3 --pmc counter CSV (FETCH_SIZE, WRITE_SIZE) of this workload, for roofline.traffic")
     return p.parse_args()
@@ -205,7 +207,8 @@ def main():
     h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols, device=local)
     if a.kernel != "auto":
         h.set_kernel(a.kernel)
-    if a.vcache_xlane or a.vcache_dma:
+    if a.vcache_xlane or a.vcache_dma or a.vcache_map:
+        h.set_option("vcache_map", a.vcache_map)
         h.set_option("vcache_xlane", a.vcache_xlane)
         h.set_option("vcache_dma", a.vcache_dma)
     setup_s = time.perf_counter() - t0
@@ -329,7 +332,7 @@ def main():
     ksub = "k_vcache" if "vcache" in kname else "k_" + kname
     if a.traffic_csv and os.path.exists(a.traffic_csv):
         traffic, traffic_src = traffic_from_csv(a.traffic_csv, ksub), a.traffic_csv
-    elif kname in PMC_PROFILES and not (a.vcache_xlane or a.vcache_dma) and a.workload == "c3" and \
+    elif kname in PMC_PROFILES and not (a.vcache_xlane or a.vcache_dma or a.vcache_map) and a.workload == "c3" and \
             (rows, cols, k) == (1 << 20, 1 << 20, 32):
         import glob
         d = os.path.join(REPO, PMC_PROFILES[kname])
@@ -401,8 +404,8 @@ def main():
                        "rows_per_gpu": rows, "cols": cols, "nnz_per_gpu": nnz,
                        "nnz_total": int(nnz_t.item()), "kernel": kname,
                        "mode": a.mode, "parallelism": f"row-partition x{world}, x broadcast (RCCL) before timing",
-                       **({"vcache_xlane": a.vcache_xlane, "vcache_dma": a.vcache_dma}
-                          if a.vcache_xlane or a.vcache_dma else {})},
+                       **({"vcache_xlane": a.vcache_xlane, "vcache_dma": a.vcache_dma, "vcache_map": a.vcache_map}
+                          if a.vcache_xlane or a.vcache_dma or a.vcache_map else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic),

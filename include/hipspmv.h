@@ -104,7 +104,9 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
  * reloads; 2 = that plus step loops padded to the unroll and register rings
  * loaded by inline asm with explicit vmcnt waits; 3 = cross-lane and padded
  * loops with the compiler's own waits -- 2 and 3 keep the DE-deep entry
- * prefetch in flight across the loop header; experimental). */
+ * prefetch in flight across the loop header; experimental), "vcache_map"
+ * (1 = VCACHE_SPLIT4 places column part h on XCDs 2h and 2h+1, so each XCD's
+ * L2 serves a quarter of x; experimental). */
 int hipspmv_set_option(hipspmv_t *h, const char *key, int64_t value);
 
 /* Replaces HardwareSpMV::exec()'s reset -> init -> regular -> write sequence

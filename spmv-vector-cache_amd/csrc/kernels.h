@@ -22,6 +22,7 @@ struct VcacheArgs {
   uint32_t panel = 0; // the layout's panel width: checked against the kernel's
   int xlane = 0;      // cross-lane run continuation (experimental, option "vcache_xlane")
   uint32_t max_seg = 0;  // longest segment of the layout (xlane needs it in the register window)
+  int map = 0;           // split 4: XCD-aware unit placement (experimental, option "vcache_map")
 };
 
 struct CsrArgs {

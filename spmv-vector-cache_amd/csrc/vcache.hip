@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include "device_common.h"
+#include "vc_map.h"
 #include "hipspmv_internal.h"
 #include "kernels.h"
 
@@ -76,13 +77,9 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   const int t = threadIdx.x;
   const bool loader = __builtin_amdgcn_readfirstlane(t >> 6) < WL;  // wave-uniform role
   uint32_t b = blockIdx.x, h = 0;
-  if (SPLIT == 2 && MAP == 1 && nblocks % 4 == 0) {
-    // dispatch slot i -> XCD group i % 8: groups 0-3 take column half 0,
-    // groups 4-7 half 1, so one XCD's L2 serves one half of x (speed only)
-    const uint32_t grp = blockIdx.x % 8;
-    h = grp / 4;
-    b = (blockIdx.x / 8) * 4 + grp % 4;
-  } else if (SPLIT > 1) {  // unit i -> (b, h): the parts of a block are 8 dispatch slots apart
+  if (MAP == 1 && SPLIT > 1 && vc_map1_applies<SPLIT>(nblocks)) {
+    vc_unit_map1<SPLIT>(blockIdx.x, b, h);  // XCD-aware placement (csrc/vc_map.h)
+  } else if (SPLIT > 1) {  // unit i -> (b, h): the parts of a block are 8 dispatch slots apart (vc_unit_map0)
     const uint32_t g = blockIdx.x / (8 * SPLIT), rem = blockIdx.x % (8 * SPLIT);
     const uint32_t nbg = min(8u, nblocks - g * 8);
     h = rem / nbg;
@@ -411,24 +408,24 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   }
 }
 
-template <typename T, int SPLIT, int LD, int CX = 0>
+template <typename T, int SPLIT, int LD, int CX = 0, int MAP = 0>
 static void launch_one(const VcacheArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_vcache<T, SPLIT, VcCfg<SPLIT>::WL, VcCfg<SPLIT>::DE, VcCfg<SPLIT>::EPT, 0, 0, false, LD, CX>),
+  hipLaunchKernelGGL((k_vcache<T, SPLIT, VcCfg<SPLIT>::WL, VcCfg<SPLIT>::DE, VcCfg<SPLIT>::EPT, 0, MAP, false, LD, CX>),
                      dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s, a.seg, a.code, (const T*)a.vals,
                      (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets, a.rows, a.cols,
                      a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta);
 }
 
-template <typename T, int SPLIT>
+template <typename T, int SPLIT, int MAP = 0>
 static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
   if (cx == 0) {
-    ld == 1 ? launch_one<T, SPLIT, 1, 0>(a, s) : launch_one<T, SPLIT, 0, 0>(a, s);
+    ld == 1 ? launch_one<T, SPLIT, 1, 0, MAP>(a, s) : launch_one<T, SPLIT, 0, 0, MAP>(a, s);
   } else if (cx == 1) {
-    ld == 1 ? launch_one<T, SPLIT, 1, 1>(a, s) : launch_one<T, SPLIT, 0, 1>(a, s);
+    ld == 1 ? launch_one<T, SPLIT, 1, 1, MAP>(a, s) : launch_one<T, SPLIT, 0, 1, MAP>(a, s);
   } else if (cx == 2) {
-    ld == 1 ? launch_one<T, SPLIT, 1, 2>(a, s) : launch_one<T, SPLIT, 2, 2>(a, s);
+    ld == 1 ? launch_one<T, SPLIT, 1, 2, MAP>(a, s) : launch_one<T, SPLIT, 2, 2, MAP>(a, s);
   } else {
-    ld == 1 ? launch_one<T, SPLIT, 1, 3>(a, s) : launch_one<T, SPLIT, 0, 3>(a, s);
+    ld == 1 ? launch_one<T, SPLIT, 1, 3, MAP>(a, s) : launch_one<T, SPLIT, 0, 3, MAP>(a, s);
   }
 }
 
@@ -457,6 +454,8 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
     dispatch<T, 1>(a, s, ld, cx);
   else if (a.split == 2)
     dispatch<T, 2>(a, s, ld, cx);
+  else if (a.map)  // experimental: XCD-aware placement of the four column parts
+    dispatch<T, 4, 1>(a, s, ld, cx);
   else
     dispatch<T, 4>(a, s, ld, cx);
   return hipGetLastError();

@@ -46,14 +46,17 @@ if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
               ("vcache xl3", "vcache", O, {"vcache_xlane": 3}), ("split xl3", "vcache_split", F, {"vcache_xlane": 3}),
               ("split4", "vcache_split4", F, {}), ("split4 xl2", "vcache_split4", F, {"vcache_xlane": 2}),
               ("split4 dma xl2", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 2}),
-              ("wgather", "wgather", O, {}), ("wgather xl2", "wgather", O, {"vcache_xlane": 2})]
+              ("wgather", "wgather", O, {}), ("wgather xl2", "wgather", O, {"vcache_xlane": 2}),
+              ("split4 map", "vcache_split4", F, {"vcache_map": 1}),
+              ("split4 map xl3", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 3}),
+              ("split4 map xl2", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 2})]
 ref = None
 res, check = {}, {}
 for rnd in range(a.rounds):  # interleaved rounds in one process (methodology rule 24)
     for label, kname, mode, opts in cands:
         try:
             h.set_kernel(kname)
-            for k in ("vcache_dma", "vcache_xlane"):
+            for k in ("vcache_dma", "vcache_xlane", "vcache_map"):
                 h.set_option(k, opts.get(k, 0))
             h.exec_device(x, y, beta=0, mode=mode, stream=s)
         except hs.HipSpMVError:

@@ -25,6 +25,7 @@
 
 #include "../host/Synthetic.h"
 #include "hipspmv_internal.h"
+#include "vc_map.h"
 
 using namespace hipspmv;
 
@@ -335,6 +336,35 @@ static HostCSR random_csr(uint32_t rows, uint32_t cols, double density, uint64_t
   return A;
 }
 
+// Slot -> unit mappings (csrc/vc_map.h): bijections onto the units, and
+// MAP 1 keeps each column part on its own XCDs.
+template <int SPLIT>
+static int check_maps() {
+  int bad = 0;
+  for (uint32_t nb = 1; nb <= 300; ++nb) {
+    for (int map = 0; map < 2; ++map) {
+      if (map == 1 && !vc_map1_applies<SPLIT>(nb)) continue;
+      std::vector<int> seen((size_t)nb * SPLIT, 0);
+      for (uint32_t slot = 0; slot < nb * SPLIT; ++slot) {
+        uint32_t b = 0, h = 0;
+        if (map)
+          vc_unit_map1<SPLIT>(slot, b, h);
+        else
+          vc_unit_map0<SPLIT>(slot, nb, b, h);
+        if (b >= nb || h >= (uint32_t)SPLIT) {
+          ++bad;
+          continue;
+        }
+        seen[(size_t)b * SPLIT + h]++;
+        if (map && h != (slot % 8) / (8 / SPLIT)) ++bad;  // part h on XCDs of group h
+      }
+      for (int c : seen) bad += c != 1;
+    }
+  }
+  std::printf("unit mappings split=%d: %s\n", SPLIT, bad ? "FAIL" : "ok");
+  return bad != 0;
+}
+
 int main(int argc, char** argv) {
   // cases: stripe C3-like (scaled), random ragged, odd cols, a long row
   struct Case {
@@ -420,7 +450,7 @@ int main(int argc, char** argv) {
                       {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 0, 16, 2},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0, 16, 2},
                       {kWgWindow.rows, kWgWindow.panel, 0, 4, 4, 1, 2, kWgWindow.colbits, 2}};
-  int failures = 0;
+  int failures = check_maps<1>() + check_maps<2>() + check_maps<4>();
   for (auto& cs : cases) {
     // host-side planning beside the replay: CSC -> CSR (csc_to_csr, the
     // hipspmv_create path) reproduces the case's CSR exactly, and the
