@@ -2,6 +2,7 @@
 // device layouts each kernel reads.
 #include <algorithm>
 #include <cstring>
+#include <thread>
 
 #include "hipspmv.h"
 #include "hipspmv_internal.h"
@@ -171,46 +172,59 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
 // order), so the lane that owns a row adds them exactly as the reference does.
 void build_sell(const HostCSR& a, SellLayout& out) {
   out = SellLayout{};
-  std::vector<uint32_t> hubs, order;
-  out.off.push_back(0);
-  for (uint32_t w0 = 0; w0 < a.rows; w0 += kSellSigma) {
-    const uint32_t w1 = std::min<uint64_t>((uint64_t)w0 + kSellSigma, a.rows);
-    order.clear();
-    for (uint32_t r = w0; r < w1; ++r) {
-      if (a.rowptr[r + 1] - a.rowptr[r] > kSellHub)
-        hubs.push_back(r);
-      else
-        order.push_back(r);
+  auto len = [&](uint32_t r) { return a.rowptr[r + 1] - a.rowptr[r]; };
+  const uint32_t nwin = (uint32_t)(((uint64_t)a.rows + kSellSigma - 1) / kSellSigma);
+  // the windows are independent: sorted in parallel, laid out at offsets
+  // from a serial prefix sum, filled in parallel -- the same bytes as a
+  // serial build
+  const unsigned nthr = std::max(1u, std::min({std::thread::hardware_concurrency(), 16u, nwin}));
+  auto parallel = [&](auto&& fn) {
+    std::vector<std::thread> ts;
+    for (unsigned t = 0; t < nthr; ++t)
+      ts.emplace_back([&, t] {
+        for (uint32_t w = t; w < nwin; w += nthr) fn(w);
+      });
+    for (auto& th : ts) th.join();
+  };
+  std::vector<std::vector<uint32_t>> order(nwin), whubs(nwin);
+  parallel([&](uint32_t w) {
+    const uint32_t w0 = w * kSellSigma, w1 = (uint32_t)std::min<uint64_t>((uint64_t)w0 + kSellSigma, a.rows);
+    for (uint32_t r = w0; r < w1; ++r) (len(r) > kSellHub ? whubs[w] : order[w]).push_back(r);
+    std::stable_sort(order[w].begin(), order[w].end(), [&](uint32_t p, uint32_t q) { return len(p) > len(q); });
+  });
+  std::vector<uint32_t> first_slice(nwin + 1, 0);
+  for (uint32_t w = 0; w < nwin; ++w)
+    first_slice[w + 1] = first_slice[w] + (uint32_t)((order[w].size() + kSellRows - 1) / kSellRows);
+  const uint32_t nslices = first_slice[nwin];
+  out.width.resize(nslices);
+  out.off.resize((size_t)nslices + 1);
+  out.off[0] = 0;
+  for (uint32_t w = 0; w < nwin; ++w)
+    for (uint32_t s = first_slice[w]; s < first_slice[w + 1]; ++s) {
+      out.width[s] = len(order[w][(size_t)(s - first_slice[w]) * kSellRows]);  // longest first
+      out.off[s + 1] = out.off[s] + (uint64_t)out.width[s] * kSellRows;
     }
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t p, uint32_t q) {
-      return a.rowptr[p + 1] - a.rowptr[p] > a.rowptr[q + 1] - a.rowptr[q];
-    });
-    for (size_t s0 = 0; s0 < order.size(); s0 += kSellRows) {
-      const size_t s1 = std::min(order.size(), s0 + kSellRows);
-      const uint32_t width = a.rowptr[order[s0] + 1] - a.rowptr[order[s0]];  // longest first
-      const uint64_t base = out.off.back();
-      out.width.push_back(width);
-      out.off.push_back(base + (uint64_t)width * kSellRows);
-      out.col.resize(out.off.back(), 0u);
-      out.vals.resize(out.off.back(), 0u);
-      for (size_t i = 0; i < (size_t)kSellRows; ++i) {
-        const uint32_t j = (uint32_t)(i / 64), l = (uint32_t)(i % 64);
-        if (s0 + i >= s1) {
-          out.row.push_back(kSellNoRow);
-          out.len.push_back(0);
-          continue;
-        }
-        const uint32_t r = order[s0 + i], e0 = a.rowptr[r], n = a.rowptr[r + 1] - e0;
-        out.row.push_back(r);
-        out.len.push_back(n);
-        for (uint32_t k = 0; k < n; ++k) {
-          const uint64_t d = base + ((uint64_t)k * 4 + j) * 64 + l;
-          out.col[d] = a.colind[e0 + k];
-          out.vals[d] = a.vals[e0 + k];
-        }
+  out.col.assign(out.off[nslices], 0u);
+  out.vals.assign(out.off[nslices], 0u);
+  out.row.assign((size_t)nslices * kSellRows, kSellNoRow);
+  out.len.assign((size_t)nslices * kSellRows, 0u);
+  parallel([&](uint32_t w) {
+    const auto& ord = order[w];
+    for (size_t i = 0; i < ord.size(); ++i) {
+      const uint32_t s = first_slice[w] + (uint32_t)(i / kSellRows), q = (uint32_t)(i % kSellRows);
+      const uint32_t j = q / 64, l = q % 64;
+      const uint32_t r = ord[i], e0 = a.rowptr[r], n = len(r);
+      out.row[(size_t)s * kSellRows + q] = r;
+      out.len[(size_t)s * kSellRows + q] = n;
+      for (uint32_t k = 0; k < n; ++k) {
+        const uint64_t d = out.off[s] + ((uint64_t)k * 4 + j) * 64 + l;
+        out.col[d] = a.colind[e0 + k];
+        out.vals[d] = a.vals[e0 + k];
       }
     }
-  }
+  });
+  std::vector<uint32_t> hubs;
+  for (auto& v : whubs) hubs.insert(hubs.end(), v.begin(), v.end());
   std::stable_sort(hubs.begin(), hubs.end(), [&](uint32_t p, uint32_t q) {
     return a.rowptr[p + 1] - a.rowptr[p] > a.rowptr[q + 1] - a.rowptr[q];
   });
@@ -230,7 +244,7 @@ void build_sell(const HostCSR& a, SellLayout& out) {
   out.npieces = (uint32_t)(out.pieces.size() / kSellPieceWords);
   out.hubs = std::move(hubs);
   out.nhubs = (uint32_t)out.hubs.size();
-  out.nslices = (uint32_t)out.width.size();
+  out.nslices = nslices;
 }
 
 // Greedy row groups: consecutive rows while the group stays within
