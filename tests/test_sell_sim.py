@@ -17,6 +17,7 @@ def _run(target, *args):
     lines = [l for l in out.stdout.splitlines() if "beta=" in l]
     assert lines and all(": ok" in l for l in lines), out.stdout
     assert "VIOLATION" not in out.stderr and "runtime error" not in out.stderr
+    assert "ThreadSanitizer" not in out.stderr
     return lines
 
 
@@ -29,3 +30,9 @@ def test_sell_replay():
 
 def test_sell_replay_under_sanitizers():
     _run("sell_sim_san", "small")
+
+
+def test_sell_layout_build_threads_race_free():
+    # build_sell fills its windows from several threads (csrc/plan.cpp)
+    lines = _run("sell_sim_tsan", "small")
+    assert lines
