@@ -56,8 +56,8 @@ MODES = {"ordered": hs.MODE_ORDERED, "fast": hs.MODE_FAST}
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--kernel", default="auto", choices=list(hs.KERNELS))
     p.add_argument("--mode", default="fast", choices=list(MODES))
     p.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"])
