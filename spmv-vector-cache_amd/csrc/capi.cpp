@@ -389,6 +389,9 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
         if (int st = build_sell_layout(h)) return st;
       } catch (const std::bad_alloc&) {
         return HIPSPMV_ERR_OOM;
+      } catch (...) {  // e.g. std::system_error from the layout builder's threads
+        g_last_error = "sell layout build failed";
+        return HIPSPMV_ERR_HIP;
       }
     }
     h->kernel_opt = (int)value;
@@ -445,8 +448,11 @@ int hipspmv_exec(hipspmv_t* h, const void* x, void* y, int beta, int mode) {
     h->d2h_ns = (uint64_t)(ms * 1e6);
     h->pending = false;
     return HIPSPMV_OK;
-  } catch (...) {
+  } catch (const std::bad_alloc&) {
     return HIPSPMV_ERR_OOM;
+  } catch (...) {
+    set_last_error("unexpected C++ exception");
+    return HIPSPMV_ERR_HIP;
   }
 }
 
@@ -540,8 +546,11 @@ int hipspmv_prep_stats(const uint32_t* colptr, const uint32_t* rowind, uint32_t 
                        int device, hipspmv_prep_stats_t* out) {
   try {
     return prep_stats(colptr, rowind, rows, cols, nnz, device, out);
-  } catch (...) {
+  } catch (const std::bad_alloc&) {
     return HIPSPMV_ERR_OOM;
+  } catch (...) {
+    set_last_error("unexpected C++ exception");
+    return HIPSPMV_ERR_HIP;
   }
 }
 
@@ -549,8 +558,11 @@ int hipspmv_mark_row_starts(const uint32_t* rowind, uint32_t* rowind_out, uint32
                             int shift, int device, uint64_t* kernel_ns) {
   try {
     return mark_row_starts(rowind, rowind_out, rows, nnz, reverse, shift, device, kernel_ns);
-  } catch (...) {
+  } catch (const std::bad_alloc&) {
     return HIPSPMV_ERR_OOM;
+  } catch (...) {
+    set_last_error("unexpected C++ exception");
+    return HIPSPMV_ERR_HIP;
   }
 }
 

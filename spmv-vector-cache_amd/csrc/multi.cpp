@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -310,8 +311,11 @@ int hipspmv_multi_set_option(hipspmv_multi_t* m, const char* key, int64_t value)
 int hipspmv_multi_exec(hipspmv_multi_t* m, const void* x, void* y, int beta, int mode) {
   try {
     return multi_exec(m, x, y, beta, mode);
-  } catch (...) {
+  } catch (const std::bad_alloc&) {
     return HIPSPMV_ERR_OOM;
+  } catch (...) {
+    set_last_error("unexpected C++ exception");
+    return HIPSPMV_ERR_HIP;
   }
 }
 
