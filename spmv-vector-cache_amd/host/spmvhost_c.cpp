@@ -79,7 +79,7 @@ void spmvhost_partition_rows(const uint32_t* rowptr, uint32_t rows, uint32_t par
 // Loads <dir>/<name>; copies into caller arrays when they are non-null, and
 // always reports the dimensions.  Returns 0 on success.
 int spmvhost_load_matrix(const char* dir, const char* name, uint32_t* dims /*rows, cols, nz, is_u64*/,
-                         uint32_t* colptr, uint32_t* rowind, uint64_t* vals) {
+                         uint32_t* colptr, uint32_t* rowind, uint64_t* vals) try {
   SparseMatrix* A = loadSparseMatrix(dir, name);
   if (!A) return 1;
   dims[0] = A->getRows();
@@ -91,6 +91,8 @@ int spmvhost_load_matrix(const char* dir, const char* name, uint32_t* dims /*row
   if (vals) std::memcpy(vals, A->getNzData(), 8ull * A->getNz());
   delete A;
   return 0;
+} catch (...) {  // nothing throws across the C boundary
+  return 3;
 }
 
 // Row-length histogram (matrixutils.py:116-126, MatrixOps.h): writes up to
@@ -134,7 +136,7 @@ void spmvhost_permute_longest_row_first(uint32_t rows, uint32_t cols, uint32_t n
 // the job of matrices/matrixutils.py:187-260 and :108-113; with permute, rows
 // are reordered longest first before writing (:149-158).  Returns 0 on success.
 int spmvhost_convert_mtx(const char* mtx_path, const char* outdir, const char* name, int write_golden,
-                         int permute) {
+                         int permute) try {
   SparseMatrix* A = loadMatrixMarket(mtx_path);
   if (!A) return 1;
   if (permute) {
@@ -146,6 +148,8 @@ int spmvhost_convert_mtx(const char* mtx_path, const char* outdir, const char* n
   if (ok && write_golden) ok = writeGolden(A, std::string(outdir) + "/" + name + "/golden.bin");
   delete A;
   return ok ? 0 : 2;
+} catch (...) {
+  return 3;
 }
 
 }  // extern "C"
