@@ -60,7 +60,7 @@ def disasm(tmp_path_factory):
 
 
 def test_kernels_present(disasm):
-    for k in ("k_vcache", "k_csr_lane", "k_csr_vector"):
+    for k in ("k_vcache", "k_csr_lane", "k_csr_vector", "k_sell", "k_wgather", "k_first_last", "k_alive_blocks"):
         assert k in disasm, k
 
 
