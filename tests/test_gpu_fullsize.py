@@ -36,8 +36,7 @@ def _sequential(rowptr, colind, vals, x, rows):
 
 
 def _check(h, x, rows, want, absprod, lens, kernel, mode):
-    if kernel != "auto":
-        h.set_kernel(kernel)
+    h.set_kernel(kernel)  # the handle is shared by the module's tests: always (re)select
     y1 = h.exec(x, beta=0, mode=mode)
     y2 = h.exec(x, beta=0, mode=mode)
     assert y1.tobytes() == y2.tobytes(), (kernel, mode)  # deterministic
