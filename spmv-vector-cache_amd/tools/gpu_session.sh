@@ -24,9 +24,9 @@ for s in $STEPS; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchfast) step bench_fast 600 python bench.py --mode fast --no-cpu-baseline ;;
-    prof) export TMPDIR=/tmp; step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
-    pmc) export TMPDIR=/tmp; step pmc 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
-         step pmc2 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    prof) export TMPDIR=/tmp; step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-rocprof ;;
+    pmc) export TMPDIR=/tmp; step pmc 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-rocprof &&
+         step pmc2 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-rocprof ;;
     micro) step micro 300 ./spmv-vector-cache_amd/tools/microbench ;;
     exp) HIPSPMV_EXPERIMENTAL=1 step pytest_exp 600 python -m pytest tests/test_gpu_parity.py -m gpu -q -x -p no:cacheprovider -k experimental ;;
     ablate) step ablate 600 ./spmv-vector-cache_amd/lib/vc_ablate ;;

@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 2
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc; mkdir -p $OUT
-ARGS=${BENCH_ARGS:-"--kernel vcache_split --mode fast --steps 10 --warmup 3 --no-cpu-baseline"}
+ARGS=${BENCH_ARGS:-"--kernel vcache_split --mode fast --steps 10 --warmup 3 --no-cpu-baseline --no-rocprof"}
 GROUPS_DEFAULT="FETCH_SIZE WRITE_SIZE TCC_HIT_sum,TCC_MISS_sum SQ_INSTS_LDS,SQ_LDS_BANK_CONFLICT,SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY"
 read -r -a GROUPS_ARR <<< "${PMC_GROUPS:-$GROUPS_DEFAULT}"
 i=0

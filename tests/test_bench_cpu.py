@@ -78,6 +78,8 @@ def _patch(monkeypatch):
     real_device = torch.device
     monkeypatch.setattr(bench.torch, "device", lambda *a, **k: real_device("cpu"))
     monkeypatch.setattr(bench, "COPY_BYTES", 1 << 20)
+    # the profiler leg starts a child bench on the GPU: its plumbing has its own test below
+    monkeypatch.setattr(bench, "rocprof_leg", lambda a: {"kernel": "hipspmv::k_fake", "calls": 3, "avg_us": 1.0})
     return bench
 
 
@@ -116,6 +118,58 @@ def test_bench_json_contract_single(monkeypatch):
     # the stand-in computes the ordered result, so both legs must pass their parity checks
     assert out["parity"].startswith("within FAST bound")
     assert out["secondary"]["mode"] == "ordered" and out["secondary"]["parity"] == "bit-exact vs oracle"
+    rp = out["rocprof"]
+    assert rp["kernel"] == "hipspmv::k_fake" and rp["event_kernel_us"] == rf["kernel_us"]
+    assert abs(rp["event_over_rocprof"] - rf["kernel_us"] / 1.0) < 1e-3
+
+
+FAKE_ROCPROF = """#!/usr/bin/env python3
+import os, sys
+args = sys.argv[1:]
+assert args[:2] == ["--kernel-trace", "--stats"], args
+sep = args.index("--")
+prog = args[sep + 1:]
+# the program itself follows "--" (no env/sh/launcher hop), in child mode
+assert os.path.basename(prog[0]).startswith("python") and prog[1].endswith("bench.py"), prog
+assert "--rocprof-child" in prog and "--no-cpu-baseline" in prog, prog
+d = args[args.index("-d") + 1]
+os.makedirs(os.path.join(d, "host", "123"), exist_ok=True)
+with open(os.path.join(d, "host", "123", "run_kernel_stats.csv"), "w") as f:
+    f.write('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\\n')
+    f.write('"void hipspmv::k_vcache<double, 2>(int)",106,15264000,144000.0,99.0,139000,149000,1700.0\\n')
+    f.write('"__amd_rocclr_copyBuffer",15,50282,3352.1,0.5,2601,4440,657.3\\n')
+"""
+
+
+def test_rocprof_leg_plumbing(tmp_path, monkeypatch):
+    """The profiler leg: rocprofv3 with --kernel-trace --stats only, the bench
+    itself right after "--" in child mode, and the dominant hipspmv kernel read
+    back from kernel_stats.csv (a fake rocprofv3 here; no GPU is touched)."""
+    import argparse
+    import shutil
+    sys.path.insert(0, REPO)
+    import bench
+    fake = tmp_path / "rocprofv3"
+    fake.write_text(FAKE_ROCPROF)
+    fake.chmod(0o755)
+    monkeypatch.setattr(shutil, "which", lambda name: str(fake) if name == "rocprofv3" else None)
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    a = argparse.Namespace(steps=200, workload="c3", scale=24, log2_rows=20, log2_cols=20, nnz_per_row=32,
+                           kernel="auto", mode="fast", vcache_xlane=0, vcache_dma=0, vcache_map=0,
+                           rocprof_timeout=60.0)
+    s = bench.rocprof_leg(a)
+    assert "error" not in s, s
+    assert s["kernel"].startswith("void hipspmv::k_vcache") and s["calls"] == 106
+    assert s["avg_us"] == 144.0 and s["min_us"] == 139.0 and s["max_us"] == 149.0
+    assert s["csv"].endswith("run_kernel_stats.csv") and s["tool"] == "rocprofv3 --kernel-trace --stats"
+
+
+def test_kernel_stats_summary_committed_profile():
+    """The parser on the committed round-1 table (kernel_stats.csv layout)."""
+    sys.path.insert(0, REPO)
+    import bench
+    s = bench.kernel_stats_summary(os.path.join(REPO, "profiles", "r01", "kernel_stats_from_pmc.csv"))
+    assert "k_vcache<double, 2" in s["kernel"] and s["calls"] == 65 and abs(s["avg_us"] - 144.814) < 1e-3
 
 
 def _rank_main(rank, world, store_path, q, extra=()):
