@@ -13,8 +13,11 @@
  * reference ships (matrices/{i64,i1k,i64k,row64k,circuit204}/golden.bin, made
  * by matrices/matrixutils.py:108-113), and the u64 semiring against the
  * known-answer tests of chisel/tests/TestSpMVFrontend.scala:121-143,148-182
- * (see tests/test_oracle.py).  The reference C++ itself is not buildable here:
+ * (see tests/test_oracle.py).  The reference's SpMV loop is not buildable here:
  * software/timer.c needs the ARM-only Xilinx BSP (XScuTimer, software/bsp_lib).
+ * software/SparseMatrix.cpp is: `make ref` compiles it into _ref/, and
+ * tests/test_oracle_ref.py checks the CMS / maxAlive / maxColSpan /
+ * clearRowMarkings restatements below against it bit for bit.
  */
 #ifndef SPMV_ORACLE_H_
 #define SPMV_ORACLE_H_
