@@ -84,7 +84,7 @@ def parse():
                    help="rocprofv3 --pmc counter CSV (FETCH_SIZE, WRITE_SIZE) of this workload, for roofline.traffic")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the rocprofv3 --kernel-trace --stats leg (N=1 only; runs before this process uses the GPU)")
-    p.add_argument("--rocprof-timeout", type=float, default=420.0)
+    p.add_argument("--rocprof-timeout", type=float, default=300.0)
     p.add_argument("--rocprof-child", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -206,12 +206,17 @@ def rocprof_leg(a):
     t = time.perf_counter()
     with open(os.path.join(outdir, "child.log"), "w") as log:
         p = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT, env=env, start_new_session=True, cwd=REPO)
-        try:
-            rc = p.wait(timeout=a.rocprof_timeout)
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGKILL)
-            p.wait()
-            return {"error": f"timed out after {a.rocprof_timeout:.0f} s"}
+        rc = None
+        while rc is None:  # a progress line every 20 s, so a watchdog never sees a silent run
+            try:
+                rc = p.wait(timeout=max(0.1, min(20.0, a.rocprof_timeout - (time.perf_counter() - t))))
+            except subprocess.TimeoutExpired:
+                waited = time.perf_counter() - t
+                if waited >= a.rocprof_timeout:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait()
+                    return {"error": f"timed out after {a.rocprof_timeout:.0f} s"}
+                print(f"[bench] rocprof leg running ({waited:.0f} s)", file=sys.stderr, flush=True)
     print(f"[bench] rocprof leg done: rc={rc} in {time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
     files = sorted(glob.glob(os.path.join(outdir, "**", "*kernel_stats.csv"), recursive=True))
     if rc != 0 or not files:

@@ -164,6 +164,24 @@ def test_rocprof_leg_plumbing(tmp_path, monkeypatch):
     assert s["csv"].endswith("run_kernel_stats.csv") and s["tool"] == "rocprofv3 --kernel-trace --stats"
 
 
+def test_rocprof_leg_timeout_kills_child(tmp_path, monkeypatch):
+    import argparse
+    import shutil
+    sys.path.insert(0, REPO)
+    import bench
+    fake = tmp_path / "rocprofv3"
+    fake.write_text("#!/bin/sh\nsleep 60\n")
+    fake.chmod(0o755)
+    monkeypatch.setattr(shutil, "which", lambda name: str(fake) if name == "rocprofv3" else None)
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    a = argparse.Namespace(steps=5, workload="c3", scale=24, log2_rows=20, log2_cols=20, nnz_per_row=32,
+                           kernel="auto", mode="fast", vcache_xlane=0, vcache_dma=0, vcache_map=0,
+                           rocprof_timeout=1.0)
+    t = time.perf_counter()
+    s = bench.rocprof_leg(a)
+    assert "timed out" in s["error"] and time.perf_counter() - t < 10
+
+
 def test_kernel_stats_summary_committed_profile():
     """The parser on the committed round-1 table (kernel_stats.csv layout)."""
     sys.path.insert(0, REPO)
