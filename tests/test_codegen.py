@@ -54,7 +54,9 @@ def disasm(tmp_path_factory):
             continue
         out = subprocess.run([_tool("llvm-objdump"), "-d", "-t", str(co)], check=True, capture_output=True,
                              text=True).stdout
-        texts.append(out)
+        notes = subprocess.run([_tool("llvm-readelf"), "--notes", str(co)], check=True, capture_output=True,
+                               text=True).stdout
+        texts.append(out + "\n" + notes)
     assert texts, "no gfx950 code object in libhipspmv.so"
     return "\n".join(texts)
 
@@ -72,3 +74,37 @@ def test_no_f64_fma(disasm):
 
 def test_no_mfma(disasm):
     assert "v_mfma" not in disasm
+
+
+def _kernel_notes(disasm):
+    """(name, fields) for every kernel in the code-object metadata notes."""
+    import re
+    out = []
+    for blk in re.split(r"\n\s+- \.agpr_count", disasm)[1:]:
+        f = dict(re.findall(r"\.([a-z_]+):\s+(\S+)", blk))
+        if "name" in f and "group_segment_fixed_size" in f:
+            out.append((f["name"], f))
+    return out
+
+
+def test_kernel_resources_within_gfx950_limits(disasm):
+    """Every kernel launches as compiled: LDS within the CU's 160 KiB, no
+    scratch and no spills, and enough VGPRs free for its largest workgroup to
+    be resident on one CU (4 SIMDs, 512 VGPRs per lane each)."""
+    ks = _kernel_notes(disasm)
+    assert len(ks) >= 20, len(ks)
+    for name, f in ks:
+        assert int(f["group_segment_fixed_size"]) <= 160 * 1024, name
+        assert int(f["private_segment_fixed_size"]) == 0, name
+        assert int(f["vgpr_spill_count"]) == 0 and int(f["sgpr_spill_count"]) == 0, name
+        assert f.get("uses_dynamic_stack", "false") == "false", name
+        waves_per_simd = -(-int(f["max_flat_workgroup_size"]) // 64 // 4)
+        alloc = -(-(int(f["vgpr_count"]) + int(f.get("agpr_count", 0) or 0)) // 8) * 8
+        assert alloc * waves_per_simd <= 512, (name, alloc, waves_per_simd)
+
+
+def test_no_scalar_stores(disasm):
+    """No writes through the scalar data cache (a hard rule of the GPU pool)."""
+    for op in ("s_store_dword", "s_buffer_store_dword", "s_scratch_store", "s_dcache_wb", "s_dcache_discard",
+               "s_atomic_", "s_buffer_atomic_"):
+        assert op not in disasm, op
