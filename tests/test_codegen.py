@@ -108,3 +108,21 @@ def test_no_scalar_stores(disasm):
     for op in ("s_store_dword", "s_buffer_store_dword", "s_scratch_store", "s_dcache_wb", "s_dcache_discard",
                "s_atomic_", "s_buffer_atomic_"):
         assert op not in disasm, op
+
+
+def test_product_kernels_are_the_gpu_validated_machine_code():
+    """The kernels AUTO selects (vcache ordered + split, csr_lane, csr_vector;
+    f64 and u64) compile to exactly the instructions of the build that passed
+    the round-1 GPU session (tests/golden/validated_isa.json, commit 2552e52):
+    the round-end bench and the validated GPU tests run that machine code."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(PKG, "tools"))
+    import kernel_isa
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "validated_isa.json")))
+    now = kernel_isa.fingerprints(os.path.join(LIBDIR, "libhipspmv.so"))
+    base = {n[:n.index(">(") + 1] if ">(" in n else n: v for n, v in now.items()}
+    assert len(ref["kernels"]) == 8
+    for k in ref["kernels"]:
+        assert k["current"] in base, k["current"]
+        assert base[k["current"]]["sha256"] == k["sha256"], f"{k['current']} differs from the validated build"
