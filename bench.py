@@ -166,16 +166,18 @@ def kernel_stats_summary(path: str):
     best = None
     with open(path) as f:
         for row in csv.DictReader(f):
-            name = row.get("Name", "")
+            row = {k.strip().lower().replace("_", ""): v for k, v in row.items() if k}
+            name = row.get("name") or row.get("kernelname") or ""
             if "hipspmv::" not in name:
                 continue
-            if best is None or float(row["TotalDurationNs"]) > float(best["TotalDurationNs"]):
+            row["name"] = name
+            if best is None or float(row["totaldurationns"]) > float(best["totaldurationns"]):
                 best = row
     if best is None:
         return None
-    return {"kernel": best["Name"], "calls": int(float(best["Calls"])),
-            "avg_us": round(float(best["AverageNs"]) / 1e3, 3), "min_us": round(float(best["MinNs"]) / 1e3, 3),
-            "max_us": round(float(best["MaxNs"]) / 1e3, 3), "stddev_us": round(float(best["StdDev"]) / 1e3, 3)}
+    us = lambda k: round(float(best[k]) / 1e3, 3) if best.get(k) not in (None, "") else None  # noqa: E731
+    return {"kernel": best["name"], "calls": int(float(best["calls"])), "avg_us": us("averagens"),
+            "min_us": us("minns"), "max_us": us("maxns"), "stddev_us": us("stddev")}
 
 
 def rocprof_leg(a):
@@ -223,7 +225,9 @@ def rocprof_leg(a):
         return {"error": f"rocprofv3 rc={rc}, {len(files)} kernel_stats.csv files"}
     s = kernel_stats_summary(files[0])
     if s is None:
-        return {"error": "no hipspmv kernel in kernel_stats.csv"}
+        with open(files[0]) as f:
+            head = f.readline().strip()
+        return {"error": f"no hipspmv kernel in {os.path.relpath(files[0], REPO)} (header: {head[:200]})"}
     s["tool"] = "rocprofv3 --kernel-trace --stats"
     s["launches"] = f"{min(a.steps, 100)} timed + 5 warmup + {min(a.steps, 100) + 1} per-launch, headline mode"
     s["csv"] = os.path.relpath(files[0], REPO)
