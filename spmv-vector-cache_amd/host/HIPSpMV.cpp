@@ -149,9 +149,9 @@ unsigned int HIPSpMV::statInt(std::string name) {
   if (name == "cmstime") return (unsigned int)(prepStats().cms_ns / 1000);
   if (name == "maxAliveTime") return (unsigned int)(prepStats().max_alive_ns / 1000);
   if (name == "maxColSpanTime") return (unsigned int)(prepStats().max_col_span_ns / 1000);
-  if (name == "thresColPtr") return m_thres_colPtr;
-  if (name == "thresRowInd") return m_thres_rowInd;
-  if (name == "thresNZData") return m_thres_nzData;
-  if (name == "thresInputVec") return m_thres_inpVec;
+  if (name == "thresColPtr") return m_thres.colPtr;
+  if (name == "thresRowInd") return m_thres.rowInd;
+  if (name == "thresNZData") return m_thres.nzData;
+  if (name == "thresInputVec") return m_thres.inpVec;
   return HardwareSpMV::statInt(name);
 }

@@ -13,8 +13,11 @@ class HWSpMVFactory {
   HWSpMVFactory();
   virtual ~HWSpMVFactory();
 
-  // nullptr (and a message on stdout) for an unrecognised signature.
+  // The backend whose signature is the first 32-bit word at aBase, as a new
+  // object the caller deletes; nullptr (and a message on stdout) for an
+  // unrecognised signature, where the reference asserts.
   static HardwareSpMV* make(uintptr_t aBase, uintptr_t aReset, SparseMatrix* A, SpMVData* x, SpMVData* y);
+  // The backend's short name for the CSV's accType column ("HIPSpMV").
   static std::string name(uintptr_t aBase);
 };
 

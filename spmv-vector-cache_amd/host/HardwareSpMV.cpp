@@ -9,12 +9,7 @@
 HardwareSpMV::HardwareSpMV(uintptr_t aBase, uintptr_t aReset, SparseMatrix* A, SpMVData* x, SpMVData* y)
     : SpMV(A, x, y),
       m_accelBase(reinterpret_cast<volatile uint32_t*>(aBase)),
-      m_resetBase(reinterpret_cast<volatile uint32_t*>(aReset)),
-      m_diffFromGolden(1),
-      m_thres_colPtr(128),
-      m_thres_rowInd(128),
-      m_thres_nzData(128),
-      m_thres_inpVec(128) {}
+      m_resetBase(reinterpret_cast<volatile uint32_t*>(aReset)) {}
 
 HardwareSpMV::~HardwareSpMV() {}
 
@@ -47,10 +42,7 @@ void HardwareSpMV::write() {}
 void HardwareSpMV::regular() {}
 
 void HardwareSpMV::setThresholds(unsigned int colPtr, unsigned int rowInd, unsigned int nzData, unsigned int inpVec) {
-  m_thres_colPtr = colPtr;
-  m_thres_rowInd = rowInd;
-  m_thres_nzData = nzData;
-  m_thres_inpVec = inpVec;
+  m_thres = Thresholds{colPtr, rowInd, nzData, inpVec};
 }
 
 void HardwareSpMV::setupRegs() { setThresholdRegisters(); }

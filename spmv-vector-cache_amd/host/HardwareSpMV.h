@@ -16,33 +16,42 @@
 
 class HardwareSpMV : public SpMV {
  public:
+  // aBase: the backend's register block (word 0 = signature); aReset: its
+  // reset word.  Neither is owned.
   HardwareSpMV(uintptr_t aBase, uintptr_t aReset, SparseMatrix* A, SpMVData* x, SpMVData* y);
   virtual ~HardwareSpMV();
 
+  // Pulse the reset word; marks the result as not yet compared.
   void resetAccelerator();
   // memcmp of y against a golden vector; statInt("diffFromGolden") == 0 iff
   // bit-identical (HardwareSpMV.cpp:37-39).
   void compareGolden(SpMVData* golden);
 
+  // "diffFromGolden", "rows", "cols", "nz" (HardwareSpMV.cpp:41-61)
   virtual unsigned int statInt(std::string name);
   virtual std::vector<std::string> statKeys();
 
+  // Stream-FIFO throttle thresholds of the FPGA backends (default 128 each);
+  // a backend without FIFOs keeps them as statistics only.
   virtual void setThresholds(unsigned int colPtr, unsigned int rowInd, unsigned int nzData, unsigned int inpVec);
 
  protected:
-  volatile uint32_t* m_accelBase;
-  volatile uint32_t* m_resetBase;
-  int m_diffFromGolden;
-  unsigned int m_thres_colPtr;
-  unsigned int m_thres_rowInd;
-  unsigned int m_thres_nzData;
-  unsigned int m_thres_inpVec;
+  struct Thresholds {
+    uint32_t colPtr = 128, rowInd = 128, nzData = 128, inpVec = 128;
+  };
+  volatile uint32_t* m_accelBase;  // register block (signature at word 0)
+  volatile uint32_t* m_resetBase;  // reset word
+  int m_diffFromGolden = 1;        // memcmp result; 1 until compareGolden runs
+  Thresholds m_thres;
 
-  virtual void init();
-  virtual void write();
-  virtual void regular();
-  virtual void setThresholdRegisters() = 0;
+  // exec() phases of a backend, in the order HardwareSpMVNewCache.cpp:78-88
+  // calls them: setupRegs (program the matrix), init, regular (the SpMV),
+  // write (y back to the caller).
   virtual void setupRegs();
+  virtual void init();
+  virtual void regular();
+  virtual void write();
+  virtual void setThresholdRegisters() = 0;
 };
 
 #endif

@@ -34,7 +34,7 @@ SoftwareSpMV::SoftwareSpMV(SparseMatrix* A, SpMVData* x, SpMVData* y) : SpMV(A, 
   }
   const bool u64 = A->getDataType() == SPMV_U64;
   if (!x) {
-    m_allocX = true;
+    m_ownX = true;
     m_x = new SpMVData[A->getCols()];
     for (unsigned int i = 0; i < A->getCols(); ++i) {
       if (u64) {
@@ -46,15 +46,15 @@ SoftwareSpMV::SoftwareSpMV(SparseMatrix* A, SpMVData* x, SpMVData* y) : SpMV(A, 
     }
   }
   if (!y) {
-    m_allocY = true;
+    m_ownY = true;
     m_y = new SpMVData[A->getRows()];
     std::memset(m_y, 0, sizeof(SpMVData) * A->getRows());  // +0.0 and integer 0 share the bit pattern
   }
 }
 
 SoftwareSpMV::~SoftwareSpMV() {
-  if (m_allocX) delete[] m_x;
-  if (m_allocY) delete[] m_y;
+  if (m_ownX) delete[] m_x;
+  if (m_ownY) delete[] m_y;
 }
 
 bool SoftwareSpMV::exec() {
@@ -65,7 +65,7 @@ bool SoftwareSpMV::exec() {
                           reinterpret_cast<const uint64_t*>(m_x), reinterpret_cast<uint64_t*>(m_y));
   else
     csc_scatter<double>(m_A->getCols(), m_A->getIndPtrs(), m_A->getInds(), m_A->getNzData(), m_x, m_y);
-  m_execTime = micros_since(t0);
+  m_stats.spmvUs = micros_since(t0);
   return true;
 }
 
@@ -74,15 +74,15 @@ bool SoftwareSpMV::exec() {
 void SoftwareSpMV::measurePreprocessingTimes() {
   const unsigned int keep = ~((1u << 31) | (1u << 30));
   auto t0 = Clock::now();
-  m_maxColSpan = m_A->maxColSpan();
-  m_maxColSpanTime = micros_since(t0);
+  m_stats.maxColSpan = m_A->maxColSpan();
+  m_stats.maxColSpanUs = micros_since(t0);
   t0 = Clock::now();
-  m_maxAlive = m_A->maxAlive();
-  m_maxAliveTime = micros_since(t0);
+  m_stats.maxAlive = m_A->maxAlive();
+  m_stats.maxAliveUs = micros_since(t0);
   m_A->clearRowMarkings(keep);
   t0 = Clock::now();
   m_A->markRowStarts();
-  m_cmsTime = micros_since(t0);
+  m_stats.cmsUs = micros_since(t0);
   m_A->clearRowMarkings(keep);
 }
 
@@ -94,11 +94,11 @@ unsigned int SoftwareSpMV::statInt(std::string name) {
   if (name == "rows") return m_A->getRows();
   if (name == "cols") return m_A->getCols();
   if (name == "nz") return m_A->getNz();
-  if (name == "spmvtime") return m_execTime;
-  if (name == "cmstime") return m_cmsTime;
-  if (name == "maxAliveTime") return m_maxAliveTime;
-  if (name == "maxColSpanTime") return m_maxColSpanTime;
-  if (name == "maxAlive") return m_maxAlive;
-  if (name == "maxColSpan") return m_maxColSpan;
+  if (name == "spmvtime") return m_stats.spmvUs;
+  if (name == "cmstime") return m_stats.cmsUs;
+  if (name == "maxAliveTime") return m_stats.maxAliveUs;
+  if (name == "maxColSpanTime") return m_stats.maxColSpanUs;
+  if (name == "maxAlive") return m_stats.maxAlive;
+  if (name == "maxColSpan") return m_stats.maxColSpan;
   return 0;
 }

@@ -11,25 +11,29 @@
 class SoftwareSpMV : public SpMV {
  public:
   // x == nullptr: an all-ones x is allocated; y == nullptr: an all-zero y
-  // (SoftwareSpMV.cpp:23-39).
+  // (SoftwareSpMV.cpp:23-39).  Vectors passed in are not owned.
   SoftwareSpMV(SparseMatrix* A, SpMVData* x = 0, SpMVData* y = 0);
   virtual ~SoftwareSpMV();
 
+  // Times maxColSpan, maxAlive and CMS marking of A (SoftwareSpMV.cpp:72-95);
+  // A's row ids are left unmarked afterwards.
   void measurePreprocessingTimes();
 
+  // y += A*x in column order; true (the reference's return value)
   virtual bool exec();
 
+  // "rows", "cols", "nz", "spmvtime", "cmstime", "maxAliveTime",
+  // "maxColSpanTime", "maxAlive", "maxColSpan"; times in microseconds
   virtual unsigned int statInt(std::string name);
   virtual std::vector<std::string> statKeys();
 
  protected:
-  bool m_allocX = false, m_allocY = false;
-  unsigned int m_execTime = 0;
-  unsigned int m_cmsTime = 0;
-  unsigned int m_maxAliveTime = 0;
-  unsigned int m_maxColSpanTime = 0;
-  unsigned int m_maxAlive = 0;
-  unsigned int m_maxColSpan = 0;
+  struct Stats {
+    unsigned int spmvUs = 0, cmsUs = 0, maxAliveUs = 0, maxColSpanUs = 0;
+    unsigned int maxAlive = 0, maxColSpan = 0;
+  };
+  bool m_ownX = false, m_ownY = false;  // vectors allocated by the constructor
+  Stats m_stats;
 };
 
 #endif
