@@ -170,9 +170,19 @@ int hipspmv_prep_stats(const uint32_t *colptr, const uint32_t *rowind, uint32_t 
 int hipspmv_mark_row_starts(const uint32_t *rowind, uint32_t *rowind_out, uint32_t rows, uint32_t nnz, int reverse,
                             int shift, int device, uint64_t *kernel_ns);
 
+/* Row partitions: a block of rows handed to its own handle (a shard) gives
+ * rows bit-identical to the unpartitioned matrix in every mode and kernel
+ * when the block starts at a multiple of HIPSPMV_SHARD_ALIGN rows and runs
+ * the same kernel (the FAST csr_vector kernel groups rows within aligned
+ * 64-row windows; every other kernel is position-independent; ORDERED is
+ * kernel-independent, FAST AUTO may choose by shard shape).  hipspmv_multi_create and the host
+ * partition helpers cut at such rows. */
+#define HIPSPMV_SHARD_ALIGN 64
+
 /* ---- several devices of one process ---------------------------------------
  * One matrix row-partitioned over ndev devices (rows cut into contiguous,
- * nnz-balanced blocks; block i on devices[i]): the single-host-thread
+ * nnz-balanced blocks starting at multiples of HIPSPMV_SHARD_ALIGN; block i
+ * on devices[i]): the single-host-thread
  * multi-GPU form of SURVEY.md §8(b)/(e), for HIPSpMV (register num_devices)
  * and C callers.  exec copies x to devices[0], broadcasts it device to device
  * (RCCL ncclBroadcast over xGMI when the ids are distinct, peer copies when an

@@ -4,7 +4,8 @@
 // hipspmv_t per shard) plus the HIP runtime and RCCL.
 //
 //   create: CSC -> CSR once, rows cut into ndev contiguous nnz-balanced
-//           blocks, block i uploaded to devices[i].
+//           blocks starting at multiples of HIPSPMV_SHARD_ALIGN rows, block i
+//           uploaded to devices[i].
 //   exec:   x host -> devices[0]; broadcast devices[0] -> all others (RCCL
 //           ncclBroadcast over xGMI, one communicator per device, from one
 //           thread in an ncclGroupStart/End; with repeated device ids, where
@@ -150,7 +151,11 @@ static int multi_create(const uint32_t* colptr, const uint32_t* rowind, const vo
     const uint64_t target = (uint64_t)nnz * p / ndev;
     const uint32_t r = (uint32_t)(std::lower_bound(a.rowptr.begin(), a.rowptr.end(), (uint32_t)target) -
                                   a.rowptr.begin());
-    bounds[p] = std::max(std::min(r, rows), bounds[p - 1]);
+    // blocks start at multiples of HIPSPMV_SHARD_ALIGN (the nearer one), so
+    // every kernel gives the single-device bits (include/hipspmv.h)
+    const uint32_t A = HIPSPMV_SHARD_ALIGN, lo = std::min(r, rows) / A * A;
+    const uint32_t snap = std::min(rows, std::min(r, rows) - lo <= A / 2 ? lo : lo + A);
+    bounds[p] = std::max(snap, bounds[p - 1]);
   }
   bounds[ndev] = rows;
   auto* m = new hipspmv_multi;

@@ -249,14 +249,21 @@ void build_sell(const HostCSR& a, SellLayout& out) {
 
 // Greedy row groups: consecutive rows while the group stays within
 // kCvGroupNnz nonzeros and kCvGroupRows rows; a longer row is a group alone.
+// No group crosses a multiple of HIPSPMV_SHARD_ALIGN rows, so the groups of a
+// shard that starts at such a row are exactly the unpartitioned matrix's
+// groups there, and csr_vector's reduction order -- and so its FAST-mode
+// bits -- does not depend on the partition.
 void build_row_groups(const HostCSR& a, std::vector<uint32_t>& groups) {
+  static_assert(kCvGroupRows <= HIPSPMV_SHARD_ALIGN && HIPSPMV_SHARD_ALIGN % kCvGroupRows == 0,
+                "a group fits an aligned window");
   groups.clear();
   uint32_t r = 0;
   while (r < a.rows) {
     groups.push_back(r);
     const uint32_t start = a.rowptr[r];
     uint32_t n = 0;
-    while (r < a.rows && n < (uint32_t)kCvGroupRows && a.rowptr[r + 1] - start <= (uint32_t)kCvGroupNnz) {
+    while (r < a.rows && n < (uint32_t)kCvGroupRows && a.rowptr[r + 1] - start <= (uint32_t)kCvGroupNnz &&
+           (n == 0 || r % HIPSPMV_SHARD_ALIGN != 0)) {
       ++r;
       ++n;
     }

@@ -1,5 +1,7 @@
 #include "Synthetic.h"
 
+#include "hipspmv.h"
+
 #include <algorithm>
 #include <cstdlib>
 #include <numeric>
@@ -183,14 +185,22 @@ uint64_t genRmatCSR(uint32_t scale, uint32_t edgeFactor, uint64_t seed, double a
   return genRmatCSRRows(scale, edgeFactor, seed, a, b, c, 0, (uint32_t)(1ull << scale), rowptr, colind, vals);
 }
 
+// Interior bounds move to the nearer multiple of HIPSPMV_SHARD_ALIGN rows
+// (include/hipspmv.h): shards cut there compute every row with the
+// unpartitioned matrix's bits in every kernel.
+static uint32_t snapShardStart(uint32_t r, uint32_t rows) {
+  const uint32_t a = HIPSPMV_SHARD_ALIGN, lo = std::min(r, rows) / a * a;
+  return std::min(rows, std::min(r, rows) - lo <= a / 2 ? lo : lo + a);
+}
+
 void partitionRows(const uint32_t* rowptr, uint32_t rows, uint32_t parts, uint32_t* bounds) {
   const uint64_t nnz = rowptr[rows];
   bounds[0] = 0;
   for (uint32_t p = 1; p < parts; ++p) {
     const uint64_t target = nnz * p / parts;
-    // first row whose start reaches the target, but never before the previous bound
+    // first row whose start reaches the target, snapped, never before the previous bound
     uint32_t r = (uint32_t)(std::lower_bound(rowptr, rowptr + rows + 1, (uint32_t)target) - rowptr);
-    bounds[p] = std::max(std::min(r, rows), bounds[p - 1]);
+    bounds[p] = std::max(snapShardStart(r, rows), bounds[p - 1]);
   }
   bounds[parts] = rows;
 }
@@ -204,7 +214,7 @@ void partitionRowCounts(const uint32_t* counts, uint32_t rows, uint32_t parts, u
   for (uint32_t p = 1; p < parts; ++p) {
     const uint64_t target = total * p / parts;
     while (r < rows && acc < target) acc += counts[r++];
-    bounds[p] = r;
+    bounds[p] = std::max(snapShardStart(r, rows), bounds[p - 1]);
   }
   bounds[parts] = rows;
 }

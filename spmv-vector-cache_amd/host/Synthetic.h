@@ -42,10 +42,11 @@ void genRmatRowCounts(uint32_t scale, uint32_t edgeFactor, uint64_t seed, double
                       uint32_t* counts);
 
 // nnz-balanced contiguous row partition: bounds[0..parts], bounds[0] = 0,
-// bounds[parts] = rows, each part holding about nnz/parts nonzeros.
+// bounds[parts] = rows, each part holding about nnz/parts nonzeros; interior
+// bounds are multiples of HIPSPMV_SHARD_ALIGN (64) rows, the nearer one.
 void partitionRows(const uint32_t* rowptr, uint32_t rows, uint32_t parts, uint32_t* bounds);
 // Same from per-row counts: bounds[p] = first row whose prefix count reaches
-// total*p/parts.
+// total*p/parts, snapped the same way.
 void partitionRowCounts(const uint32_t* counts, uint32_t rows, uint32_t parts, uint32_t* bounds);
 
 // Worker threads of the host generators: $SPMV_THREADS, else

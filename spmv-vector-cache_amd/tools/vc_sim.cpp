@@ -475,10 +475,35 @@ int main(int argc, char** argv) {
       std::vector<uint32_t> groups;
       build_row_groups(A, groups);
       bool tiles = groups.size() >= 2 && groups.front() == 0 && groups.back() == A.rows;
-      for (size_t i = 1; i < groups.size(); ++i) tiles = tiles && groups[i - 1] < groups[i];
-      failures += !(same && tiles);
-      std::printf("%-28s csc_to_csr %s, row groups %s\n", cs.name.c_str(), same ? "ok" : "FAIL",
-                  tiles ? "ok" : "FAIL");
+      for (size_t i = 1; i < groups.size(); ++i) {
+        tiles = tiles && groups[i - 1] < groups[i];
+        tiles = tiles && groups[i] - groups[i - 1] <= (uint32_t)kCvGroupRows;
+        tiles = tiles && (groups[i - 1] / HIPSPMV_SHARD_ALIGN == (groups[i] - 1) / HIPSPMV_SHARD_ALIGN);
+      }
+      // a shard cut at multiples of HIPSPMV_SHARD_ALIGN has exactly the
+      // unpartitioned matrix's groups over its rows (csr_vector bits do not
+      // depend on the partition)
+      bool shards = true;
+      const uint32_t AL = HIPSPMV_SHARD_ALIGN;
+      const uint32_t cuts[] = {0, A.rows / 3 / AL * AL, 2 * (A.rows / 3) / AL * AL, A.rows};
+      for (int k = 0; k < 3; ++k) {
+        const uint32_t s0 = cuts[k], s1 = cuts[k + 1];
+        if (s1 <= s0) continue;
+        HostCSR S;
+        S.rows = s1 - s0;
+        S.cols = A.cols;
+        S.nnz = A.rowptr[s1] - A.rowptr[s0];
+        S.rowptr.resize(S.rows + 1);
+        for (uint32_t r = 0; r <= S.rows; ++r) S.rowptr[r] = A.rowptr[s0 + r] - A.rowptr[s0];
+        std::vector<uint32_t> sg, want;
+        build_row_groups(S, sg);
+        for (uint32_t g : groups)
+          if (g >= s0 && g <= s1) want.push_back(g - s0);
+        shards = shards && sg == want;
+      }
+      failures += !(same && tiles && shards);
+      std::printf("%-28s csc_to_csr %s, row groups %s, shard groups %s\n", cs.name.c_str(), same ? "ok" : "FAIL",
+                  tiles ? "ok" : "FAIL", shards ? "ok" : "FAIL");
     }
     std::vector<double> x(cs.A.cols), yin(cs.A.rows);
     for (uint32_t i = 0; i < cs.A.cols; ++i) x[i] = uniform11(splitmix64_at(3, i));

@@ -168,3 +168,37 @@ def test_gpu_row_partition_bit_identical(gpu, kernel, mode):
             ys = sh.exec(x, beta=0, mode=mode)
             sh.close()
             assert ys.tobytes() == y[r0:r1].tobytes(), (parts, p, kernel)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel,mode", [("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST),
+                                         ("csr_lane", hs.MODE_ORDERED), ("auto", hs.MODE_ORDERED)])
+def test_gpu_row_partition_bit_identical_skewed(gpu, kernel, mode):
+    """The same on R-MAT rows of very different lengths, where csr_vector's row
+    groups differ from row to row: shards cut at multiples of
+    HIPSPMV_SHARD_ALIGN (what partition_rows returns) keep the FAST bits of a
+    given kernel.  (AUTO may pick a different FAST kernel for a smaller shard;
+    in ORDERED mode every kernel gives the same bits.)"""
+    n = 1 << 16
+    rowptr, colind, vals = hs.gen_rmat_csr(16)
+    x = hs.gen_vector(n, 3)
+    whole = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    if kernel != "auto":
+        whole.set_kernel(kernel)
+    y = whole.exec(x, beta=0, mode=mode)
+    whole.close()
+    for parts in (2, 3, 5):
+        bounds = hs.partition_rows(rowptr, parts)
+        assert all(int(b) % 64 == 0 for b in bounds[1:-1])
+        for p in range(parts):
+            r0, r1 = int(bounds[p]), int(bounds[p + 1])
+            if r1 == r0:
+                continue
+            e0, e1 = int(rowptr[r0]), int(rowptr[r1])
+            sh = hs.Handle.from_csr((rowptr[r0:r1 + 1] - rowptr[r0]).astype(np.uint32), colind[e0:e1],
+                                    vals[e0:e1], r1 - r0, n)
+            if kernel != "auto":
+                sh.set_kernel(kernel)
+            ys = sh.exec(x, beta=0, mode=mode)
+            sh.close()
+            assert ys.tobytes() == y[r0:r1].tobytes(), (parts, p, kernel)

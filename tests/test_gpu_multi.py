@@ -57,6 +57,25 @@ def test_multi_equals_single_device(gpu, kernel, mode):
     m.close()
 
 
+@pytest.mark.parametrize("kernel", ["csr_vector", "sell"])
+def test_multi_equals_single_device_skewed_fast(gpu, kernel):
+    # R-MAT rows: block starts are multiples of HIPSPMV_SHARD_ALIGN, so even
+    # csr_vector's FAST reduction order matches the single device bit for bit
+    n = 1 << 15
+    rowptr, colind, vals = hs.gen_rmat_csr(15)
+    colptr, rowind, cvals = oracle.csr2csc(n, n, rowptr, colind, vals)
+    x = hs.gen_vector(n, 3)
+    one = hs.Handle.from_csc(colptr, rowind, cvals, n, n)
+    one.set_kernel(kernel)
+    y1 = one.exec(x, beta=0, mode=hs.MODE_FAST)
+    one.close()
+    m = hs.MultiHandle(colptr, rowind, cvals, n, n, _devices(3))
+    assert all(m.stat(f"shard{i}_row0") % 64 == 0 for i in range(3))
+    m.set_kernel(kernel)
+    assert m.exec(x, beta=0, mode=hs.MODE_FAST).tobytes() == y1.tobytes()
+    m.close()
+
+
 def test_multi_more_devices_than_rows(gpu):
     rows, cols, colptr, rowind, vals = fx.load("i64")
     m = hs.MultiHandle(colptr, rowind, vals, rows, cols, _devices(5))

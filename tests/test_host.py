@@ -102,9 +102,12 @@ def test_partition_rows_balanced(parts):
     rowptr, colind, vals = hs.gen_rmat_csr(12, 16, seed=4)
     b = hs.partition_rows(rowptr, parts).astype(np.int64)
     assert b[0] == 0 and b[-1] == rowptr.size - 1 and np.all(np.diff(b) >= 0)
+    assert np.all(b[1:-1] % 64 == 0)  # shard starts at multiples of HIPSPMV_SHARD_ALIGN
     nnz = rowptr[b[1:]].astype(np.int64) - rowptr[b[:-1]].astype(np.int64)
     assert nnz.sum() == colind.size
-    assert nnz.max() <= colind.size / parts + np.diff(rowptr.astype(np.int64)).max() + 1
+    lens = np.diff(rowptr.astype(np.int64))
+    slack = np.sort(lens)[-33:].sum()  # the snap moves a cut by at most 32 rows each way
+    assert nnz.max() <= colind.size / parts + 2 * slack + 1
 
 
 def test_product_csr2csc_equals_oracle():
@@ -125,6 +128,7 @@ def test_rmat_row_ranges_concatenate_to_the_whole_matrix():
     for parts in (1, 3, 8):
         b = hs.partition_row_counts(counts, parts)
         assert b[0] == 0 and b[-1] == 1 << scale and np.all(np.diff(b.astype(np.int64)) >= 0)
+        assert np.all(b[1:-1] % 64 == 0)
         for p in range(parts):
             r0, r1 = int(b[p]), int(b[p + 1])
             rp, ci, v = hs.gen_rmat_rows(scale, r0, r1, 16, 4)
