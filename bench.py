@@ -288,7 +288,9 @@ def main():
         scaling = "weak"
     elif a.workload == "c4":
         n = 1 << a.scale
-        row0, row1 = n * rank // world, n * (rank + 1) // world
+        # equal blocks, cut at multiples of HIPSPMV_SHARD_ALIGN (include/hipspmv.h)
+        cut = lambda r: n if r >= world else (n * r // world) // hs.SHARD_ALIGN * hs.SHARD_ALIGN  # noqa: E731
+        row0, row1 = cut(rank), cut(rank + 1)
         rows, cols = row1 - row0, n
         rowptr, colind, vals = hs.gen_stripe_csr(row0, rows, cols, k, 1, 2)
         workload = f"C4 stripe-uniform CSR {n}x{n}, {k} nnz/row, {world} equal row blocks"

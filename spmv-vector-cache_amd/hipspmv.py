@@ -34,6 +34,7 @@ MODE_AUTO, MODE_ORDERED, MODE_FAST = 0, 1, 2
 KERNEL_AUTO, KERNEL_VCACHE, KERNEL_CSR_LANE, KERNEL_CSR_VECTOR, KERNEL_VCACHE_SPLIT = 0, 1, 2, 3, 4
 KERNEL_VCACHE_SPLIT4, KERNEL_WGATHER = 5, 6  # experimental: never chosen by AUTO
 KERNEL_SELL = 7  # SELL-C-sigma lane per row; selectable, not chosen by AUTO yet
+SHARD_ALIGN = 64  # HIPSPMV_SHARD_ALIGN: row shards starting at multiples keep every kernel's bits
 KERNELS = {"auto": KERNEL_AUTO, "vcache": KERNEL_VCACHE, "csr_lane": KERNEL_CSR_LANE,
            "csr_vector": KERNEL_CSR_VECTOR, "vcache_split": KERNEL_VCACHE_SPLIT,
            "vcache_split4": KERNEL_VCACHE_SPLIT4, "wgather": KERNEL_WGATHER, "sell": KERNEL_SELL}

@@ -73,3 +73,16 @@ def test_wrapper_rejects_mismatched_arrays():
         hs.Handle.from_csc(np.zeros(3, np.uint32), np.zeros(0, np.uint32), np.zeros(0), 4, 4)  # colptr short
     with pytest.raises(ValueError):
         hs.Handle.from_csr(np.array([0, 1], np.uint32), np.zeros(1, np.uint32), np.zeros(2), 1, 4)  # vals long
+
+
+def test_python_constants_match_header():
+    """The binding's enums and HIPSPMV_SHARD_ALIGN are the header's #defines."""
+    import re
+    text = open(hs.HEADER).read()
+    d = {k: int(v) for k, v in re.findall(r"#define (HIPSPMV_[A-Z0-9_]+) (\d+)", text)}
+    assert d["HIPSPMV_SHARD_ALIGN"] == hs.SHARD_ALIGN
+    assert (d["HIPSPMV_F64"], d["HIPSPMV_U64"]) == (hs.F64, hs.U64)
+    assert (d["HIPSPMV_MODE_AUTO"], d["HIPSPMV_MODE_ORDERED"], d["HIPSPMV_MODE_FAST"]) == \
+        (hs.MODE_AUTO, hs.MODE_ORDERED, hs.MODE_FAST)
+    for name, v in hs.KERNELS.items():
+        assert d["HIPSPMV_KERNEL_" + name.upper()] == v, name
