@@ -132,6 +132,38 @@ void spmvhost_permute_longest_row_first(uint32_t rows, uint32_t cols, uint32_t n
   delete A;
 }
 
+// SparseMatrix's preprocessing helpers (host/SparseMatrix.cpp, the statistics
+// SoftwareSpMV::measurePreprocessingTimes reports) on caller CSC arrays, in
+// place on inds like the reference; tests/test_oracle_ref.py checks them
+// against the reference's own SparseMatrix.cpp.
+void spmvhost_mark_row_starts(uint32_t rows, uint32_t cols, uint32_t nz, uint32_t* colptr, uint32_t* inds,
+                              int reverse, int shift) {
+  SparseMatrix* A = SparseMatrix::fromArrays(rows, cols, nz, colptr, inds, nullptr);
+  A->markRowStarts(reverse != 0, shift);
+  delete A;
+}
+
+uint32_t spmvhost_max_alive(uint32_t rows, uint32_t cols, uint32_t nz, uint32_t* colptr, uint32_t* inds) {
+  SparseMatrix* A = SparseMatrix::fromArrays(rows, cols, nz, colptr, inds, nullptr);
+  const uint32_t v = A->maxAlive();
+  delete A;
+  return v;
+}
+
+uint32_t spmvhost_max_col_span(uint32_t rows, uint32_t cols, uint32_t nz, uint32_t* colptr, uint32_t* inds) {
+  SparseMatrix* A = SparseMatrix::fromArrays(rows, cols, nz, colptr, inds, nullptr);
+  const uint32_t v = A->maxColSpan();
+  delete A;
+  return v;
+}
+
+void spmvhost_clear_row_markings(uint32_t rows, uint32_t cols, uint32_t nz, uint32_t* colptr, uint32_t* inds,
+                                 uint32_t mask) {
+  SparseMatrix* A = SparseMatrix::fromArrays(rows, cols, nz, colptr, inds, nullptr);
+  A->clearRowMarkings(mask);
+  delete A;
+}
+
 // Matrix Market -> reference .bin files (+ golden.bin) under <outdir>/<name>/,
 // the job of matrices/matrixutils.py:187-260 and :108-113; with permute, rows
 // are reordered longest first before writing (:149-158).  Returns 0 on success.

@@ -3,8 +3,10 @@
 oracle/_ref/libref_sparsematrix.so is the reference's own
 software/SparseMatrix.cpp compiled unmodified where it lies (oracle/Makefile
 target `ref`, harness oracle/ref_harness.cpp).  markRowStarts, maxAlive,
-maxColSpan and clearRowMarkings of the oracle (oracle/oracle.c) must give the
-reference's exact results -- marked index arrays bit for bit, the two
+maxColSpan and clearRowMarkings of the oracle (oracle/oracle.c) and of the
+product's host library (host/SparseMatrix.cpp via libspmvhost.so, the
+statistics SoftwareSpMV and spmvbench report) must give the reference's exact
+results -- marked index arrays bit for bit, the two
 statistics equal -- on every fixture and on random matrices.  The GPU scans
 (csrc/prep.hip, tests/test_gpu_prep.py) are checked against the oracle, so
 this closes the chain to the reference for those statistics.
@@ -30,6 +32,23 @@ LIB = os.path.join(REPO, "oracle", "_ref", "libref_sparsematrix.so")
 pytestmark = pytest.mark.skipif(not os.path.exists(REF_SRC), reason="reference tree absent (GPU box)")
 
 _u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+
+
+@pytest.fixture(scope="module")
+def host():
+    """The product's own SparseMatrix helpers (libspmvhost.so, host/SparseMatrix.cpp)."""
+    import hipspmv as hs
+    lib = hs.load_host()
+    args = [C.c_uint32, C.c_uint32, C.c_uint32, _u32p, _u32p]
+    lib.spmvhost_mark_row_starts.argtypes = args + [C.c_int, C.c_int]
+    lib.spmvhost_mark_row_starts.restype = None
+    lib.spmvhost_max_alive.argtypes = args
+    lib.spmvhost_max_alive.restype = C.c_uint32
+    lib.spmvhost_max_col_span.argtypes = args
+    lib.spmvhost_max_col_span.restype = C.c_uint32
+    lib.spmvhost_clear_row_markings.argtypes = args + [C.c_uint32]
+    lib.spmvhost_clear_row_markings.restype = None
+    return lib
 
 
 @pytest.fixture(scope="module")
@@ -79,20 +98,30 @@ def _ref_call(ref, fn, case, inds, *extra):
 
 @pytest.mark.parametrize("case", _cases())
 @pytest.mark.parametrize("reverse,shift", [(False, 31), (True, 30), (False, 30), (True, 31), (False, 29)])
-def test_mark_row_starts_matches_reference(ref, case, reverse, shift):
+def test_mark_row_starts_matches_reference(ref, host, case, reverse, shift):
     rows, cols, colptr, rowind = case
     want = rowind.copy()
     _ref_call(ref, "ref_mark_row_starts", case, want, int(reverse), shift)
     got = oracle.mark_row_starts(rowind, rows, reverse=reverse, shift=shift)
     assert got.tobytes() == want.tobytes()
+    prod = rowind.copy()
+    _ref_call(host, "spmvhost_mark_row_starts", case, prod, int(reverse), shift)
+    assert prod.tobytes() == want.tobytes()
 
 
 @pytest.mark.parametrize("case", _cases())
-def test_max_alive_and_col_span_match_reference(ref, case):
+def test_max_alive_and_col_span_match_reference(ref, host, case):
     rows, cols, colptr, rowind = case
     ref_inds = rowind.copy()
-    assert oracle.max_col_span(colptr, rowind) == _ref_call(ref, "ref_max_col_span", case, rowind.copy())
+    span = _ref_call(ref, "ref_max_col_span", case, rowind.copy())
+    assert oracle.max_col_span(colptr, rowind) == span
+    assert _ref_call(host, "spmvhost_max_col_span", case, rowind.copy()) == span
     want = _ref_call(ref, "ref_max_alive", case, ref_inds)
+    prod = rowind.copy()
+    assert _ref_call(host, "spmvhost_max_alive", case, prod) == want
+    assert prod.tobytes() == ref_inds.tobytes()  # the product leaves the reference's marks
+    _ref_call(host, "spmvhost_clear_row_markings", case, prod, 0x3FFFFFFF)
+    assert prod.tobytes() == rowind.tobytes()
     mine = rowind.copy()
     got = int(oracle.lib().oracle_max_alive(rows, mine.size, mine))
     assert got == want
