@@ -180,6 +180,27 @@ def kernel_stats_summary(path: str):
             "min_us": us("minns"), "max_us": us("maxns"), "stddev_us": us("stddev")}
 
 
+def kernel_provenance(kname: str, dtype: str = "double"):
+    """Machine-code fingerprint of the timed kernel (tools/kernel_isa.py over
+    the libhipspmv.so this run loaded) and whether it equals the build that
+    passed the round-1 GPU session (tests/golden/validated_isa.json)."""
+    sys.path.insert(0, os.path.join(REPO, "spmv-vector-cache_amd", "tools"))
+    import kernel_isa
+    want = {"vcache": f"void hipspmv::k_vcache<{dtype}, 1, 8, 4, 3, 0, 0, false, 0, 0>",
+            "vcache_split": f"void hipspmv::k_vcache<{dtype}, 2, 6, 4, 3, 0, 0, false, 0, 0>",
+            "csr_lane": f"void hipspmv::k_csr_lane<{dtype}>", "csr_vector": f"void hipspmv::k_csr_vector<{dtype}>"}
+    if kname not in want:
+        return {"kernel": kname, "note": "not one of the round-1 validated kernels"}
+    fps = kernel_isa.fingerprints(os.path.join(hs.LIB_DIR, "libhipspmv.so"))
+    mine = next((v for n, v in fps.items() if n.startswith(want[kname] + "(")), None)
+    if mine is None:
+        return {"kernel": want[kname], "error": "not found in libhipspmv.so"}
+    with open(os.path.join(REPO, "tests", "golden", "validated_isa.json")) as f:
+        ref = {k["current"]: k["sha256"] for k in json.load(f)["kernels"]}
+    return {"kernel": want[kname], "isa_sha256": mine["sha256"], "instructions": mine["insts"],
+            "same_as_gpu_validated_build": ref.get(want[kname]) == mine["sha256"]}
+
+
 def rocprof_leg(a):
     """`rocprofv3 --kernel-trace --stats` over this same bench (headline mode
     only, no CPU or copy legs) as a CHILD process, started before this process
@@ -535,6 +556,10 @@ def main():
             "rank_kernel_us": [round(v * 1e3, 3) for v in rank_kern_ms],
             "setup_s": round(setup_s, 3),
         }
+        try:  # reported, never fatal
+            out["roofline"]["kernel_provenance"] = kernel_provenance(kname)
+        except Exception as e:
+            out["roofline"]["kernel_provenance"] = {"error": f"{type(e).__name__}: {e}"}
         if rocprof is not None:
             if "avg_us" in rocprof:  # the profiler's per-launch mean vs this run's HIP-event mean
                 rocprof["event_kernel_us"] = round(kern_ms * 1e3, 3)
