@@ -6,8 +6,11 @@ a sample of rows (first, last, the longest, 2,000 random) is recomputed
 sequentially in Python floats -- products rounded, then added in ascending
 column order, exactly SoftwareSpMV's arithmetic (SoftwareSpMV.cpp:59-64) --
 and ORDERED results must match those rows bit for bit, FAST results the
-per-row bound of include/hipspmv.h; runs are deterministic.  Exercises the
-64-bit entry offsets of every kernel and the hub-row path of k_sell."""
+per-row bound of include/hipspmv.h; runs are deterministic.  With the values
+read as u64 the checks are exact over the whole matrix: every kernel gives
+the same bits, y is linear in x mod 2^64 and sum(y) equals a nonzero-wise
+checksum.  Exercises the 64-bit entry offsets of every kernel and the hub-row
+path of k_sell."""
 import numpy as np
 import pytest
 
@@ -61,15 +64,25 @@ def _case(gen):
 
 
 @pytest.fixture(scope="module")
-def c4(gpu):
-    case = _case(lambda: (1 << 24, *hs.gen_stripe_csr(0, 1 << 24, 1 << 24, 32)))
+def c4_csr(gpu):
+    return (1 << 24, *hs.gen_stripe_csr(0, 1 << 24, 1 << 24, 32))
+
+
+@pytest.fixture(scope="module")
+def c5_csr(gpu):
+    return (1 << 24, *hs.gen_rmat_csr(24))
+
+
+@pytest.fixture(scope="module")
+def c4(c4_csr):
+    case = _case(lambda: c4_csr)
     yield case
     case[0].close()
 
 
 @pytest.fixture(scope="module")
-def c5(gpu):
-    case = _case(lambda: (1 << 24, *hs.gen_rmat_csr(24)))
+def c5(c5_csr):
+    case = _case(lambda: c5_csr)
     yield case
     case[0].close()
 
@@ -80,3 +93,42 @@ def c5(gpu):
 def test_full_size_sampled_rows(request, which, kernel, mode):
     h, x, rows, want, absprod, lens = request.getfixturevalue(which)
     _check(h, x, rows, want, absprod, lens, kernel, mode)
+
+
+def _checksum_u64(colind, vals, x, chunk=1 << 26):
+    """sum_i y_i = sum_e a_e * x[col_e] (mod 2^64), in chunks."""
+    s = np.uint64(0)
+    for e0 in range(0, colind.size, chunk):
+        s += np.sum(vals[e0:e0 + chunk] * x[colind[e0:e0 + chunk]], dtype=np.uint64)
+    return int(s)
+
+
+@pytest.mark.parametrize("which", ["c4_csr", "c5_csr"])
+def test_full_size_u64_exact_properties(request, which):
+    """The same matrices with their 8-byte values read as u64 (the integer
+    semiring, exact in every kernel and mode): every kernel/mode gives the
+    same bits, y is linear in x mod 2^64 (A(x1 + x2) = Ax1 + Ax2), and
+    sum(y) equals the nonzero-wise checksum sum_e a_e x[col_e] -- exact
+    whole-matrix checks at full size, no sampling."""
+    n, rowptr, colind, vals = request.getfixturevalue(which)
+    a = vals.view(np.uint64)
+    rng = np.random.default_rng(11)
+    x1 = rng.integers(0, 2**64, n, dtype=np.uint64)
+    x2 = rng.integers(0, 2**64, n, dtype=np.uint64)
+    h = hs.Handle.from_csr(rowptr, colind, a, n, n)
+    try:
+        ref = None
+        with np.errstate(over="ignore"):
+            for kernel, mode in (("auto", hs.MODE_ORDERED), ("auto", hs.MODE_FAST), ("sell", hs.MODE_FAST)):
+                h.set_kernel(kernel)
+                y1 = h.exec(x1, beta=0, mode=mode)
+                if ref is None:
+                    ref = y1
+                    y2 = h.exec(x2, beta=0, mode=mode)
+                    y3 = h.exec(x1 + x2, beta=0, mode=mode)
+                    assert np.array_equal(y3, y1 + y2), (which, kernel)  # linear mod 2^64
+                    assert int(np.sum(y1, dtype=np.uint64)) == _checksum_u64(colind, a, x1), which
+                else:
+                    assert y1.tobytes() == ref.tobytes(), (which, kernel, h.kernel_name(mode))
+    finally:
+        h.close()
