@@ -74,6 +74,11 @@ def c5_csr(gpu):
 
 
 @pytest.fixture(scope="module")
+def c3_csr(gpu):
+    return (1 << 20, *hs.gen_stripe_csr(0, 1 << 20, 1 << 20, 32))
+
+
+@pytest.fixture(scope="module")
 def c4(c4_csr):
     case = _case(lambda: c4_csr)
     yield case
@@ -103,7 +108,15 @@ def _checksum_u64(colind, vals, x, chunk=1 << 26):
     return int(s)
 
 
-@pytest.mark.parametrize("which", ["c4_csr", "c5_csr"])
+U64_KERNELS = {  # (kernel, mode); the C3 list includes the vector-cache kernels bench.py times
+    "c3_csr": [("vcache", hs.MODE_ORDERED), ("vcache_split", hs.MODE_FAST), ("csr_lane", hs.MODE_ORDERED),
+               ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
+    "c4_csr": [("auto", hs.MODE_ORDERED), ("auto", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
+    "c5_csr": [("auto", hs.MODE_ORDERED), ("auto", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
+}
+
+
+@pytest.mark.parametrize("which", ["c3_csr", "c4_csr", "c5_csr"])
 def test_full_size_u64_exact_properties(request, which):
     """The same matrices with their 8-byte values read as u64 (the integer
     semiring, exact in every kernel and mode): every kernel/mode gives the
@@ -119,7 +132,7 @@ def test_full_size_u64_exact_properties(request, which):
     try:
         ref = None
         with np.errstate(over="ignore"):
-            for kernel, mode in (("auto", hs.MODE_ORDERED), ("auto", hs.MODE_FAST), ("sell", hs.MODE_FAST)):
+            for kernel, mode in U64_KERNELS[which]:
                 h.set_kernel(kernel)
                 y1 = h.exec(x1, beta=0, mode=mode)
                 if ref is None:
