@@ -20,7 +20,7 @@ step() {  # step NAME TIMEOUT CMD...
 STEPS=${STEPS:-"pytest smoke bench prof"}
 for s in $STEPS; do
   case $s in
-    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    pytest) step pytest_gpu ${PYTEST_TIMEOUT:-1000} python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchfast) step bench_fast 600 python bench.py --mode fast --no-cpu-baseline ;;

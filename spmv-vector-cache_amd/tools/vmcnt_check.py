@@ -111,7 +111,7 @@ def transfer(state: dict[int, int], ins: str, report=None):
     # registers read / written by this instruction
     if is_load:
         dst, src = vregs(parts[0]) if parts else set(), set().union(*(vregs(p) for p in parts[1:])) if len(parts) > 1 else set()
-    elif VMEM_STORE.match(op) or op.startswith("ds_write") or op.startswith("ds_add") or op.startswith("ds_store") \
+    elif VMEM_STORE.match(op) or op.startswith("ds_write") or op.startswith("ds_add") \
             or op.startswith("s_") or op.startswith("global_load_lds") or op.startswith("buffer_load") and "lds" in ins:
         dst, src = set(), set().union(*(vregs(p) for p in parts)) if parts else set()
     else:

@@ -103,13 +103,6 @@ def test_kernel_resources_within_gfx950_limits(disasm):
         assert alloc * waves_per_simd <= 512, (name, alloc, waves_per_simd)
 
 
-def test_no_scalar_stores(disasm):
-    """No writes through the scalar data cache (a hard rule of the GPU pool)."""
-    for op in ("s_store_dword", "s_buffer_store_dword", "s_scratch_store", "s_dcache_wb", "s_dcache_discard",
-               "s_atomic_", "s_buffer_atomic_"):
-        assert op not in disasm, op
-
-
 def test_product_kernels_are_the_gpu_validated_machine_code():
     """The kernels AUTO selects (vcache ordered + split, csr_lane, csr_vector;
     f64 and u64) compile to exactly the instructions of the build that passed
