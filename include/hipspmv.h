@@ -118,7 +118,13 @@ int hipspmv_exec(hipspmv_t *h, const void *x, void *y, int beta, int mode);
 /* Device-resident variant: d_x, d_y_in and d_y_out are device pointers on the
  * handle's device; enqueued on `stream` (a hipStream_t; NULL is HIP's default
  * stream, as in every HIP API) and returns without synchronising.  d_y_in may
- * equal d_y_out and is ignored for beta == 0. */
+ * equal d_y_out and is ignored for beta == 0.  Concurrency: a handle is used
+ * from one host thread at a time.  Launches of one handle on different streams
+ * may be in flight together; the kernels that combine column parts through the
+ * handle's scratch (VCACHE_SPLIT, VCACHE_SPLIT4, SELL in FAST / u64 with hub
+ * pieces) are ordered by the handle itself: such a launch waits, on the device,
+ * for the previous one when that went to another stream (hipspmv_exec's
+ * internal stream included). */
 int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void *d_y_out, int beta, int mode,
                         void *stream);
 

@@ -98,6 +98,13 @@ struct hipspmv_handle {
   int last_kernel = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool pending = false;  // kernel events recorded by exec_device, not yet read
+  // The column-part combine scratch (vcache_split/split4 tickets + partials,
+  // SELL FAST hub-piece tickets + partials) is one per handle: a launch that
+  // uses it is ordered after the previous such launch when that one went to
+  // another stream (device-side wait on scratch_ev, no host synchronisation).
+  hipEvent_t scratch_ev = nullptr;
+  hipStream_t scratch_stream = nullptr;
+  bool scratch_used = false;
 };
 
 static void release(hipspmv_t* h) {
@@ -120,6 +127,7 @@ static void release(hipspmv_t* h) {
   }
   for (hipEvent_t e : h->ev)
     if (e) (void)hipEventDestroy(e);
+  if (h->scratch_ev) (void)hipEventDestroy(h->scratch_ev);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -128,6 +136,7 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   DeviceGuard g(h->device);
   HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   for (auto& e : h->ev) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipEventCreateWithFlags(&h->scratch_ev, hipEventDisableTiming));
   for (uint32_t r = 0; r < a.rows; ++r) {
     const uint32_t len = a.rowptr[r + 1] - a.rowptr[r];
     h->max_row_len = len > h->max_row_len ? len : h->max_row_len;
@@ -304,6 +313,11 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                   hipStream_t s, int mode) {
   hipError_t e = hipSuccess;
   if (mode == HIPSPMV_MODE_AUTO) mode = h->mode_opt;
+  const bool scratch = kernel == HIPSPMV_KERNEL_VCACHE_SPLIT || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4 ||
+                       (kernel == HIPSPMV_KERNEL_SELL && h->sell.npieces &&
+                        (mode != HIPSPMV_MODE_ORDERED || h->dtype == HIPSPMV_U64));
+  if (scratch && h->scratch_used && h->scratch_stream != s)
+    HIP_TRY(hipStreamWaitEvent(s, h->scratch_ev, 0));
   if (kernel == HIPSPMV_KERNEL_SELL) {
     const auto& q = h->sell;
     SellArgs a{q.d_off,     q.d_width,   q.d_row,     q.d_len, q.d_col,  q.d_vals,
@@ -333,6 +347,11 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     e = kernel == HIPSPMV_KERNEL_CSR_LANE ? launch_csr_lane(h->dtype, a, s) : launch_csr_vector(h->dtype, a, s);
   }
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
+  if (scratch) {
+    HIP_TRY(hipEventRecord(h->scratch_ev, s));
+    h->scratch_stream = s;
+    h->scratch_used = true;
+  }
   h->last_kernel = kernel;
   h->execs++;
   return HIPSPMV_OK;

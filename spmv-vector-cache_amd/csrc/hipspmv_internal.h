@@ -63,6 +63,29 @@ constexpr uint32_t kSellNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kSellPiece = 4096;
 constexpr int kSellPieceWords = 8;
 
+// Launch geometry of a vcache-family kernel (k_vcache, k_wgather): true iff
+// every work unit's rows and panels lie inside the matrix for a kernel
+// compiled for geometry g -- the row-block bound, no surplus blocks (a block
+// with r0 >= rows would compute rows - r0 in uint32 and write past y: the
+// round-1 GPU fault), every column covered by the panels, the
+// column parts each non-empty, and the unit's segment table inside LDS.
+// launch_vcache / launch_wgather return hipErrorInvalidValue without a launch
+// when it is false; tools/vc_sim.cpp checks it on the CPU (incl. the incident
+// geometry).
+inline bool vcache_grid_ok(uint32_t rows, uint32_t cols, uint32_t rows_per_block, uint32_t nblocks,
+                           uint32_t npanels, uint32_t part_panels, uint32_t npad, uint32_t panel, int split,
+                           const VcGeom& g) {
+  if (split != g.split || panel != (uint32_t)g.panel) return false;
+  if (rows == 0 || cols == 0 || nblocks == 0 || rows_per_block == 0 || rows_per_block > (uint32_t)g.rows)
+    return false;
+  if ((uint64_t)nblocks * rows_per_block < rows) return false;         // every row in some block
+  if ((uint64_t)(nblocks - 1) * rows_per_block >= rows) return false;  // no surplus block
+  if (npanels == 0 || (uint64_t)npanels * g.panel < cols) return false;
+  if ((uint64_t)part_panels * split < npanels) return false;          // every panel in some part
+  if ((uint64_t)part_panels * (split - 1) >= npanels) return false;   // the last part has a panel
+  return npad + 1 <= (uint32_t)kVcSegMax && npad >= part_panels;
+}
+
 struct HostCSR {
   uint32_t rows = 0, cols = 0, nnz = 0;
   std::vector<uint32_t> rowptr, colind;

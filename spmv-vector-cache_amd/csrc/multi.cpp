@@ -98,7 +98,8 @@ struct hipspmv_multi {
     hipspmv_t* h = nullptr;
     hipStream_t stream = nullptr;
     void *d_x = nullptr, *d_y = nullptr;
-    hipEvent_t ev[4] = {};  // start (root) / x on the root (others), x ready, kernel done, y copied
+    hipEvent_t ev[5] = {};  // start (root) / x on the root (others), x ready, kernel done, y copied,
+                            // root only: x ready after the broadcast (its kernel starts there)
     uint64_t kernel_ns = 0;
   };
   std::vector<Shard> shards;
@@ -181,7 +182,7 @@ static int multi_create(const uint32_t* colptr, const uint32_t* rowind, const vo
     }
     hipError_t e = hipSuccess;
     if (!st) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-    for (int k = 0; k < 4 && !st && e == hipSuccess; ++k) e = hipEventCreate(&s.ev[k]);
+    for (int k = 0; k < 5 && !st && e == hipSuccess; ++k) e = hipEventCreate(&s.ev[k]);
     if (!st && e == hipSuccess) e = hipMalloc(&s.d_x, 8ull * cols);
     if (!st && e == hipSuccess) e = hipMalloc(&s.d_y, 8ull * std::max<uint32_t>(s.rows, 1));
     if (!st && e != hipSuccess) st = hfail(e, "multi shard setup");
@@ -256,6 +257,10 @@ static int multi_exec(hipspmv_multi_t* m, const void* x, void* y, int beta, int 
     DevGuard g(s.device);
     MTRY(hipEventRecord(s.ev[1], s.stream));
   }
+  {  // the root's own kernel starts after the broadcast it takes part in (RCCL runs on its stream)
+    DevGuard g(root.device);
+    MTRY(hipEventRecord(root.ev[4], root.stream));
+  }
   // 3. per shard: y in (beta 1), kernel, y out
   char* yb = static_cast<char*>(y);
   for (auto& s : m->shards) {
@@ -280,7 +285,7 @@ static int multi_exec(hipspmv_multi_t* m, const void* x, void* y, int beta, int 
     auto& s = m->shards[i];
     if (i > 0) bc = std::max(bc, (uint64_t)(ms_between(s.ev[0], s.ev[1]) * 1e6));
     if (!s.rows) continue;
-    s.kernel_ns = (uint64_t)(ms_between(s.ev[1], s.ev[2]) * 1e6);
+    s.kernel_ns = (uint64_t)(ms_between(i == 0 ? s.ev[4] : s.ev[1], s.ev[2]) * 1e6);
     kern = std::max(kern, s.kernel_ns);
     d2h = std::max(d2h, (uint64_t)(ms_between(s.ev[2], s.ev[3]) * 1e6));
   }
@@ -338,9 +343,13 @@ int hipspmv_multi_stat(hipspmv_multi_t* m, const char* key, uint64_t* out) {
   else if (k == "kernel_ns") *out = m->kernel_ns;
   else if (k == "d2h_ns") *out = m->d2h_ns;
   else if (k == "execs") *out = m->execs;
-  else if (k == "kernel") {  // the kernel block 0 ran last (HIPSPMV_KERNEL_*)
+  else if (k == "kernel") {  // the kernel the first non-empty block ran last (HIPSPMV_KERNEL_*)
     uint64_t v = 0;
-    if (m->shards[0].h) (void)hipspmv_stat(m->shards[0].h, "kernel", &v);
+    for (auto& s : m->shards)  // the first non-empty block (a block of a small matrix may have no rows)
+      if (s.h) {
+        (void)hipspmv_stat(s.h, "kernel", &v);
+        break;
+      }
     *out = v;
   }
   else if (k == "alg_bytes") {

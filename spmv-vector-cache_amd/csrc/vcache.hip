@@ -86,6 +86,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     b = g * 8 + rem % nbg;
   }
   const uint32_t r0 = b * rows_per_block;
+  if (r0 >= rows) return;  // never with a vcache_grid_ok geometry (workgroup-uniform, before any barrier)
   const uint32_t nr = min(rows_per_block, rows - r0);
   const uint32_t p0 = h * part_panels;                  // first global panel of this unit
   const uint32_t npu = min(part_panels, npanels - p0);  // >= 1 (vcache_eligible)
@@ -433,11 +434,8 @@ template <typename T>
 hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   // the layout's geometry must be the one the kernel is compiled for
   const VcGeom g = a.split == 1 ? kVcOrdered : a.split == 2 ? kVcSplit : kVcSplit4;
-  if ((a.split != 1 && a.split != 2 && a.split != 4) || a.panel != (uint32_t)g.panel ||
-      a.rows_per_block > (uint32_t)g.rows ||
-      (uint64_t)a.nblocks * a.rows_per_block < a.rows || a.part_panels * (uint64_t)a.split < a.npanels ||
-      (uint64_t)a.part_panels * (a.split - 1) >= a.npanels ||
-      (uint64_t)a.npanels * g.panel < a.cols || a.npad + 1 > (uint32_t)kVcSegMax)
+  if (!vcache_grid_ok(a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.panel,
+                      a.split, g))
     return hipErrorInvalidValue;
   // cross-lane continuation needs every segment inside the register window
   auto window = [](int split) {

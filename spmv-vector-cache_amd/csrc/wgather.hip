@@ -38,6 +38,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
   const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
   const uint32_t r0 = b * rows_per_block;
+  if (r0 >= rows) return;  // never with a vcache_grid_ok geometry
   const uint32_t nr = min(rows_per_block, rows - r0);
   const uint32_t* sp = seg + (size_t)b * (npad + 1);
   if ((uint32_t)t <= npad) segl[t] = sp[t];
@@ -129,6 +130,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather_pipe(const uint32_t* __r
   const uint32_t lw = t & 63;
   const uint32_t b = blockIdx.x;
   const uint32_t r0 = b * rows_per_block;
+  if (r0 >= rows) return;  // never with a vcache_grid_ok geometry
   const uint32_t nr = min(rows_per_block, rows - r0);
   const uint32_t* sp = seg + (size_t)b * (npad + 1);
   if ((uint32_t)t <= npad) segl[t] = sp[t];
@@ -253,9 +255,9 @@ static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
 
 hipError_t launch_wgather(int dtype, const VcacheArgs& a, hipStream_t s) {
   // the layout must be kWgWindow's (window width, row-block bound, one part)
-  if (a.split != 1 || a.panel != (uint32_t)kWgWindow.panel || a.rows_per_block > (uint32_t)kWgWindow.rows ||
-      (uint64_t)a.nblocks * a.rows_per_block < a.rows || (uint64_t)a.npanels * kWgWindow.panel < a.cols ||
-      a.part_panels != a.npanels || a.npad + 1 > (uint32_t)kVcSegMax)
+  if (!vcache_grid_ok(a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.panel,
+                      a.split, kWgWindow) ||
+      a.part_panels != a.npanels)
     return hipErrorInvalidValue;
   return dtype ? launch_wgather_t<uint64_t>(a, s) : launch_wgather_t<double>(a, s);
 }

@@ -10,6 +10,7 @@ step() {  # step NAME TIMEOUT CMD...
   echo "== $name: $*" | tee -a $OUT/session.log
   timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
+  LAST_RC=$rc
   echo "== $name rc=$rc" | tee -a $OUT/session.log
   tail -5 "$OUT/$name.log"
   if [ $rc -ge 124 ] || [ $rc -gt 1 -a $rc -ne 0 -a "$name" != "pytest_gpu" ]; then
@@ -20,7 +21,12 @@ step() {  # step NAME TIMEOUT CMD...
 STEPS=${STEPS:-"pytest smoke bench prof"}
 for s in $STEPS; do
   case $s in
-    pytest) step pytest_gpu ${PYTEST_TIMEOUT:-1000} python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
+    pytest) step pytest_gpu ${PYTEST_TIMEOUT:-1000} python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
+            # the library these tests just passed with: its product-kernel fingerprints (tests/golden/validated_isa.json)
+            if [ "$LAST_RC" = 0 ] && [ -z "${PYTEST_ARGS:-}" ]; then
+              python spmv-vector-cache_amd/tools/record_validated.py spmv-vector-cache_amd/lib/libhipspmv.so \
+                $OUT/validated_isa.json "$(grep -E '^=+ .*passed' $OUT/pytest_gpu.log | tail -1 | tr -d '=' | xargs)"
+            fi ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchfast) step bench_fast 600 python bench.py --mode fast --no-cpu-baseline ;;
@@ -33,6 +39,7 @@ for s in $STEPS; do
     sweep) step sweep 600 python spmv-vector-cache_amd/tools/kernel_sweep.py ;;
     sweepx) HIPSPMV_EXPERIMENTAL=1 step sweep_exp 900 python spmv-vector-cache_amd/tools/kernel_sweep.py ;;
     sweeprmat) step sweep_rmat 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --rmat 20 ;;
+    sweepwidex) HIPSPMV_EXPERIMENTAL=1 step sweep_wide_exp 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 21 --log2-cols 24 --rounds 2 ;;
     sweepwide) step sweep_wide 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 21 --log2-cols 24 ;;
     c4) step bench_c4 900 python bench.py --workload c4 --steps 20 --warmup 5 ;;
     c5) step bench_c5 900 python bench.py --workload c5 --steps 20 --warmup 5 ;;

@@ -451,6 +451,20 @@ int main(int argc, char** argv) {
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0, 16, 2},
                       {kWgWindow.rows, kWgWindow.panel, 0, 4, 4, 1, 2, kWgWindow.colbits, 2}};
   int failures = check_maps<1>() + check_maps<2>() + check_maps<4>();
+  {  // the round-1 incident geometry: the ordered (split 1) kernel launched with the split layout's
+     // 8192-row blocks -- 256 blocks over 2^20 rows, 128 of them past the last row -- is rejected,
+     // as is any grid with a surplus block or a block taller than the kernel's LDS y block
+    const uint32_t n = 1u << 20, np = (n + kVcOrdered.panel - 1) / kVcOrdered.panel;
+    const bool incident = vcache_grid_ok(n, n, 8192, 256, np, np, np, kVcOrdered.panel, 1, kVcOrdered);
+    const bool surplus = vcache_grid_ok(n, n, 4096, 257, np, np, np, kVcOrdered.panel, 1, kVcOrdered);
+    const bool good = vcache_grid_ok(n, n, 4096, 256, np, np, np, kVcOrdered.panel, 1, kVcOrdered);
+    const uint32_t nps = (n + kVcSplit.panel - 1) / kVcSplit.panel, part = (nps + 1) / 2;
+    const bool split_wrong_kernel = vcache_grid_ok(n, n, 8192, 128, nps, part, part, kVcSplit.panel, 2, kVcOrdered);
+    const bool split_good = vcache_grid_ok(n, n, 8192, 128, nps, part, part, kVcSplit.panel, 2, kVcSplit);
+    const bool ok = !incident && !surplus && good && !split_wrong_kernel && split_good;
+    std::printf("grid guard (incident geometry rejected, product accepted): %s\n", ok ? "ok" : "FAIL");
+    failures += !ok;
+  }
   for (auto& cs : cases) {
     // host-side planning beside the replay: CSC -> CSR (csc_to_csr, the
     // hipspmv_create path) reproduces the case's CSR exactly, and the
@@ -516,6 +530,13 @@ int main(int argc, char** argv) {
       }
       VcacheLayout L;
       build_vcache(cs.A, g, L);
+      // the launcher's guard (vcache_grid_ok) accepts every product layout
+      if (!vcache_grid_ok(cs.A.rows, cs.A.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels, L.npad,
+                          L.geom.panel, c.SPLIT, g)) {
+        std::printf("%-28s split=%d: product layout REJECTED by vcache_grid_ok\n", cs.name.c_str(), c.SPLIT);
+        ++failures;
+        continue;
+      }
       if (c.CX && L.max_seg > (uint32_t)((16 - c.WL) * 64 * c.EPT)) {  // launch_vcache falls back to CX 0
         std::printf("%-28s split=%d cx=%d: segments exceed the window, CX 0 runs\n", cs.name.c_str(), c.SPLIT, c.CX);
         continue;

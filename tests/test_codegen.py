@@ -105,9 +105,10 @@ def test_kernel_resources_within_gfx950_limits(disasm):
 
 def test_product_kernels_are_the_gpu_validated_machine_code():
     """The kernels AUTO selects (vcache ordered + split, csr_lane, csr_vector;
-    f64 and u64) compile to exactly the instructions of the build that passed
-    the round-1 GPU session (tests/golden/validated_isa.json, commit 2552e52):
-    the round-end bench and the validated GPU tests run that machine code."""
+    f64 and u64) compile to exactly the instructions of the last build that
+    passed `pytest -m gpu` on an MI355X (tests/golden/validated_isa.json,
+    recorded on the GPU box by tools/record_validated.py from the library those
+    tests loaded): the round-end bench runs that machine code."""
     import json
     import sys
     sys.path.insert(0, os.path.join(PKG, "tools"))

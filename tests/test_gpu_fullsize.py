@@ -111,8 +111,9 @@ def _checksum_u64(colind, vals, x, chunk=1 << 26):
 U64_KERNELS = {  # (kernel, mode); the C3 list includes the vector-cache kernels bench.py times
     "c3_csr": [("vcache", hs.MODE_ORDERED), ("vcache_split", hs.MODE_FAST), ("csr_lane", hs.MODE_ORDERED),
                ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
-    "c4_csr": [("auto", hs.MODE_ORDERED), ("auto", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
-    "c5_csr": [("auto", hs.MODE_ORDERED), ("auto", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
+    # wide x (16 M columns, no vector-cache layout): every generic kernel by name
+    "c4_csr": [("csr_lane", hs.MODE_ORDERED), ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
+    "c5_csr": [("csr_lane", hs.MODE_ORDERED), ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
 }
 
 
@@ -129,12 +130,14 @@ def test_full_size_u64_exact_properties(request, which):
     x1 = rng.integers(0, 2**64, n, dtype=np.uint64)
     x2 = rng.integers(0, 2**64, n, dtype=np.uint64)
     h = hs.Handle.from_csr(rowptr, colind, a, n, n)
+    ran = set()
     try:
         ref = None
         with np.errstate(over="ignore"):
             for kernel, mode in U64_KERNELS[which]:
                 h.set_kernel(kernel)
                 y1 = h.exec(x1, beta=0, mode=mode)
+                ran.add(h.kernel_name(mode))
                 if ref is None:
                     ref = y1
                     y2 = h.exec(x2, beta=0, mode=mode)
@@ -143,5 +146,6 @@ def test_full_size_u64_exact_properties(request, which):
                     assert int(np.sum(y1, dtype=np.uint64)) == _checksum_u64(colind, a, x1), which
                 else:
                     assert y1.tobytes() == ref.tobytes(), (which, kernel, h.kernel_name(mode))
+        assert len(ran) == len(U64_KERNELS[which]), ran  # distinct kernels, none silently substituted
     finally:
         h.close()

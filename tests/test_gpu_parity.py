@@ -84,8 +84,11 @@ def _random_csc(rows, cols, density, rng, dtype=np.float64, empty_rows=True, lon
         dense[r, :] = True
     colptr = np.concatenate([[0], np.cumsum(dense.sum(0))]).astype(np.uint32)
     rowind = np.concatenate([np.nonzero(dense[:, c])[0] for c in range(cols)]).astype(np.uint32)
-    if dup:  # duplicate some entries inside their column (SoftwareSpMV adds both, in order)
-        pass
+    if dup:  # repeat ~5% of the entries right after themselves in their column (SoftwareSpMV adds both, in order)
+        col_of = np.repeat(np.arange(cols), dense.sum(0))
+        k = 1 + (rng.random(rowind.size) < 0.05).astype(np.int64)
+        rowind, col_of = np.repeat(rowind, k), np.repeat(col_of, k)
+        colptr = np.concatenate([[0], np.cumsum(np.bincount(col_of, minlength=cols))]).astype(np.uint32)
     if dtype == np.float64:
         vals = rng.uniform(-1, 1, rowind.size)
     else:
@@ -114,6 +117,20 @@ def test_random_u64_wraparound(gpu, kernel):
     x = rng.integers(0, 2**64, cols, dtype=np.uint64)
     for beta in (0, 1):
         _check("u64", rows, cols, colptr, rowind, vals, x, kernel, beta, hs.MODE_FAST)
+
+
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
+def test_random_duplicates(gpu, kernel):
+    # repeated (row, col) entries (5 % of a ragged matrix with a full-width row):
+    # ORDERED kernels add each copy in CSC order, bit for bit; FAST within the bound
+    rng = np.random.default_rng(11)
+    rows, cols = 2000, 3000
+    colptr, rowind, vals = _random_csc(rows, cols, 0.01, rng, long_rows=[77], dup=True)
+    assert np.any(np.diff(rowind.astype(np.int64)) == 0)  # some entry is repeated
+    x = rng.uniform(-1, 1, cols)
+    mode = hs.MODE_ORDERED if kernel in ORDERED_KERNELS else hs.MODE_FAST
+    for beta in (0, 1):
+        _check("dup", rows, cols, colptr, rowind, vals, x, kernel, beta, mode)
 
 
 def test_duplicates_and_cms_bits(gpu):
@@ -228,6 +245,38 @@ def test_c3_split_deterministic_and_within_bound(gpu):
     y0 = np.random.default_rng(4).uniform(-1, 1, n)
     y1 = h.exec(x, y0.copy(), beta=1, mode=hs.MODE_FAST)
     assert np.all(np.abs(y1 - (y_ref + y0)) <= _fast_bound(np.full(n, 33), absprod + np.abs(y0), 0) * 2)
+
+
+def test_split_combine_concurrent_streams(gpu):
+    # vcache_split's column-part combine uses per-handle tickets and partials;
+    # launches of one handle on two streams with no host synchronisation are
+    # ordered by the handle (include/hipspmv.h), so every result is the
+    # single-stream one, bit for bit
+    import torch
+    n = 1 << 20
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    assert h.kernel_name(hs.MODE_FAST) == "vcache_split"
+    xs = [torch.from_numpy(hs.gen_vector(n, 3 + i)).cuda() for i in range(2)]
+    want = []
+    for x in xs:
+        y = torch.empty(n, dtype=torch.float64, device="cuda")
+        h.exec_device(x, y, beta=0, mode=hs.MODE_FAST, stream=torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        want.append(y.cpu().numpy().tobytes())
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [[torch.empty(n, dtype=torch.float64, device="cuda") for _ in range(8)] for _ in range(2)]
+    torch.cuda.synchronize()
+    for k in range(8):
+        for i in range(2):
+            h.exec_device(xs[i], outs[i][k], beta=0, mode=hs.MODE_FAST, stream=streams[i])
+    # and the host-buffer path (the handle's own stream) in between
+    y_host = h.exec(xs[0].cpu().numpy(), beta=0, mode=hs.MODE_FAST)
+    torch.cuda.synchronize()
+    assert y_host.tobytes() == want[0]
+    for i in range(2):
+        for k in range(8):
+            assert outs[i][k].cpu().numpy().tobytes() == want[i], (i, k)
 
 
 # ---- experimental vcache variants (never chosen by AUTO): four column parts

@@ -16,6 +16,10 @@ def test_vcache_addressing_replay():
     lines = [l for l in out.stdout.splitlines() if "split=" in l]
     assert sum(": ok" in l for l in lines) >= 16, out.stdout
     assert "VIOLATION" not in out.stderr
+    # launch_vcache's guard: the round-1 incident geometry (split-1 kernel, 256 x 8192-row
+    # blocks over 2^20 rows) is rejected before any launch, every product layout accepted
+    assert "grid guard (incident geometry rejected, product accepted): ok" in out.stdout
+    assert "REJECTED" not in out.stdout
 
 
 def test_layout_builder_and_replay_under_sanitizers():
