@@ -252,8 +252,8 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
         const uint32_t l = (uint32_t)__builtin_ctzll(m);
         uint32_t i = __builtin_amdgcn_readlane(fbi, l);
         const uint64_t ab = __builtin_bit_cast(uint64_t, acc);
-        T a = __builtin_bit_cast(T, (uint64_t)__builtin_amdgcn_readlane((uint32_t)ab, l) |
-                                        ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ab >> 32), l) << 32));
+        T a = __builtin_bit_cast(T, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)ab, l) |
+                                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(ab >> 32), l) << 32));
         uint32_t cd;
         do {
           cd = sload32(ecode + i);

@@ -35,7 +35,8 @@ s = torch.cuda.current_stream()
 O, F = hs.MODE_ORDERED, hs.MODE_FAST
 # (label, kernel, mode, options); the experimental ones need HIPSPMV_EXPERIMENTAL=1 at create
 cands = [("vcache", "vcache", O, {}), ("csr_lane", "csr_lane", O, {}), ("vcache_split", "vcache_split", F, {}),
-         ("csr_vector", "csr_vector", F, {}), ("sell", "sell", O, {}), ("sell fast", "sell", F, {})]
+         ("csr_vector", "csr_vector", F, {}), ("sell", "sell", O, {}), ("sell fast", "sell", F, {}),
+         ("vstream", "vcache", O, {"vcache_engine": 1}), ("vstream split", "vcache_split", F, {"vcache_engine": 1})]
 if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
     cands += [("vcache xl1", "vcache", O, {"vcache_xlane": 1}), ("vcache xl2", "vcache", O, {"vcache_xlane": 2}),
               ("vcache dma", "vcache", O, {"vcache_dma": 1}),
@@ -56,7 +57,7 @@ for rnd in range(a.rounds):  # interleaved rounds in one process (methodology ru
     for label, kname, mode, opts in cands:
         try:
             h.set_kernel(kname)
-            for k in ("vcache_dma", "vcache_xlane", "vcache_map"):
+            for k in ("vcache_dma", "vcache_xlane", "vcache_map", "vcache_engine"):
                 h.set_option(k, opts.get(k, 0))
             h.exec_device(x, y, beta=0, mode=mode, stream=s)
         except hs.HipSpMVError:
