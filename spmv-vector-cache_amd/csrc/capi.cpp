@@ -91,7 +91,6 @@ struct hipspmv_handle {
   int vcache_dma = 0;    // option "vcache_dma": LDS-DMA x loader (experimental)
   int vcache_xlane = 0;  // option "vcache_xlane": cross-lane run continuation (experimental)
   int vcache_map = 0;    // option "vcache_map": XCD-aware part placement, split 4 (experimental)
-  int vcache_engine = 0;  // option "vcache_engine": 0 k_vcache, 1 k_vstream (csrc/vstream.hip)
   void *d_x = nullptr, *d_y = nullptr;
   int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
   uint64_t setup_ns = 0, kernel_ns = 0, h2d_ns = 0, d2h_ns = 0, execs = 0, device_bytes = 0;
@@ -335,7 +334,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                  v.d_tickets, h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
                  v.npad,      h->nnz - 1, v.split,   beta, h->vcache_dma, (uint32_t)geoms[k].panel,
                  h->vcache_xlane, v.max_seg, h->vcache_map};
-    e = h->vcache_engine == 1 && k < 2 ? launch_vstream(h->dtype, a, s) : launch_vcache(h->dtype, a, s);
+    e = launch_vcache(h->dtype, a, s);
   } else if (kernel == HIPSPMV_KERNEL_WGATHER) {
     const auto& v = h->vc[3];
     VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    nullptr,
@@ -419,9 +418,6 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
     h->vcache_dma = value ? 1 : 0;
   } else if (k == "vcache_map") {
     h->vcache_map = value ? 1 : 0;
-  } else if (k == "vcache_engine") {
-    if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
-    h->vcache_engine = (int)value;
   } else if (k == "vcache_xlane") {
     if (value < 0 || value > 3) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_xlane = (int)value;

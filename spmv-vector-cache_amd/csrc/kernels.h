@@ -61,8 +61,6 @@ struct SellArgs {
 };
 
 hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);
-hipError_t launch_vstream(int dtype, const VcacheArgs& a, hipStream_t s);
-uint32_t vstream_window(int split);
 hipError_t launch_sell(int dtype, const SellArgs& a, hipStream_t s);
 hipError_t launch_wgather(int dtype, const VcacheArgs& a, hipStream_t s);
 hipError_t launch_csr_lane(int dtype, const CsrArgs& a, hipStream_t s);

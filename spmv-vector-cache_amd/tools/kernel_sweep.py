@@ -18,6 +18,7 @@ p.add_argument("--k", type=int, default=32)
 p.add_argument("--rmat", type=int, default=0, help="R-MAT scale instead of the stripe generator")
 p.add_argument("--reps", type=int, default=50)
 p.add_argument("--rounds", type=int, default=3)
+p.add_argument("--only", default="", help="comma-separated label substrings to keep")
 a = p.parse_args()
 if a.rmat:
     rowptr, colind, vals = hs.gen_rmat_csr(a.rmat, 16, 4)
@@ -35,8 +36,7 @@ s = torch.cuda.current_stream()
 O, F = hs.MODE_ORDERED, hs.MODE_FAST
 # (label, kernel, mode, options); the experimental ones need HIPSPMV_EXPERIMENTAL=1 at create
 cands = [("vcache", "vcache", O, {}), ("csr_lane", "csr_lane", O, {}), ("vcache_split", "vcache_split", F, {}),
-         ("csr_vector", "csr_vector", F, {}), ("sell", "sell", O, {}), ("sell fast", "sell", F, {}),
-         ("vstream", "vcache", O, {"vcache_engine": 1}), ("vstream split", "vcache_split", F, {"vcache_engine": 1})]
+         ("csr_vector", "csr_vector", F, {}), ("sell", "sell", O, {}), ("sell fast", "sell", F, {})]
 if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
     cands += [("vcache xl1", "vcache", O, {"vcache_xlane": 1}), ("vcache xl2", "vcache", O, {"vcache_xlane": 2}),
               ("vcache dma", "vcache", O, {"vcache_dma": 1}),
@@ -51,13 +51,16 @@ if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
               ("split4 map", "vcache_split4", F, {"vcache_map": 1}),
               ("split4 map xl3", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 3}),
               ("split4 map xl2", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 2})]
+if a.only:
+    keep = a.only.split(",")
+    cands = [c for c in cands if any(k in c[0] for k in keep) or c[0] == "vcache"]
 ref = None
 res, check = {}, {}
 for rnd in range(a.rounds):  # interleaved rounds in one process (methodology rule 24)
     for label, kname, mode, opts in cands:
         try:
             h.set_kernel(kname)
-            for k in ("vcache_dma", "vcache_xlane", "vcache_map", "vcache_engine"):
+            for k in ("vcache_dma", "vcache_xlane", "vcache_map"):
                 h.set_option(k, opts.get(k, 0))
             h.exec_device(x, y, beta=0, mode=mode, stream=s)
         except hs.HipSpMVError:

@@ -333,59 +333,6 @@ def test_experimental_vcache_variants(gpu, kernel, dma, xlane, xmap):
         h.close()
 
 
-@pytest.mark.parametrize("kernel", ["vcache", "vcache_split"])
-@pytest.mark.parametrize("dtype", ["f64", "u64"])
-def test_vstream_engine(gpu, kernel, dtype):
-    """k_vstream (csrc/vstream.hip) on the vcache layouts: ORDERED bit-exact, split within the FAST
-    bound and deterministic, u64 exact -- stripe matrices, ragged rows with long in-segment runs
-    (narrow x: many entries of one row per panel, runs crossing waves), odd column counts."""
-    cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20), (20000, 1 << 21), (18, 999)]
-    for rows, cols in cases:
-        rng = np.random.default_rng(rows + cols)
-        if cols >= 1 << 20:
-            rowptr, colind, vals = hs.gen_stripe_csr(0, rows, cols, 32)
-        else:
-            lens = rng.integers(0, 12 if cols > 1000 else 200, rows)
-            rowptr = np.zeros(rows + 1, np.uint32)
-            rowptr[1:] = np.cumsum(lens)
-            colind = np.concatenate([np.sort(rng.choice(cols, n, replace=False)) for n in lens]).astype(np.uint32)
-            vals = rng.uniform(-1, 1, colind.size)
-        if dtype == "u64":
-            vals = rng.integers(0, 2**64, colind.size, dtype=np.uint64)
-            x = rng.integers(0, 2**64, cols, dtype=np.uint64)
-        else:
-            x = rng.uniform(-1, 1, cols)
-        h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
-        key = "vcache_split_eligible" if kernel == "vcache_split" else "vcache_eligible"
-        if not h.stat(key):
-            h.close()
-            continue
-        h.set_kernel(kernel)
-        h.set_option("vcache_engine", 1)
-        mode = hs.MODE_ORDERED if kernel == "vcache" else hs.MODE_FAST
-        colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
-        for beta in (0, 1):
-            y0 = (rng.uniform(-1, 1, rows) if dtype == "f64" else rng.integers(0, 2**64, rows, dtype=np.uint64))
-            y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else None), rows=rows)
-            try:
-                ys = [h.exec(x, y0.copy(), beta=beta, mode=mode) for _ in range(2)]
-            except hs.HipSpMVError:  # a segment beyond the register window: the launcher refuses it
-                assert h.stat("vcache_max_segment") > 2048 or kernel == "vcache_split"
-                break
-            assert ys[0].tobytes() == ys[1].tobytes(), "not deterministic"
-            if mode == hs.MODE_ORDERED or dtype == "u64":
-                if ys[0].tobytes() != y_ref.tobytes():
-                    bad = np.nonzero(ys[0].view(np.uint64) != y_ref.view(np.uint64))[0]
-                    pytest.fail(f"{rows}x{cols} beta{beta}: {bad.size} rows differ, first {bad[:5]}")
-            else:
-                lens = np.diff(rowptr.astype(np.int64))
-                absprod = np.bincount(np.repeat(np.arange(rows), lens), weights=np.abs(vals * x[colind]),
-                                      minlength=rows)
-                bound = 2.0 * (lens + 1) * 2.0 ** -53 * (absprod + (np.abs(y0) if beta else 0)) + 1e-300
-                assert np.all(np.abs(ys[0] - y_ref) <= bound), (rows, cols, beta)
-        h.close()
-
-
 # ---- analogues of the backend known-answer test (chisel/tests/TestSpMVBackend.scala:122-178):
 # write-out mode (rows come back unchanged: y_in -> y_out with nothing to add) and the stream
 # sums sumUpTo(64) = 2080 carried by the nonzero-value stream and by the input-vector stream.
