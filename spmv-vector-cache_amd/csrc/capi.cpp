@@ -8,6 +8,7 @@
 
 #include <chrono>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <new>
 #include <string>
@@ -76,9 +77,14 @@ struct hipspmv_handle {
     bool ok = false;
     uint32_t *d_seg = nullptr, *d_code = nullptr, *d_tickets = nullptr;
     uint64_t *d_vals = nullptr, *d_partial = nullptr;
-    uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, part_panels = 0, npad = 0, max_seg = 0;
+    uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, part_panels = 0, npad = 0, max_seg = 0, max_run = 0;
+    uint64_t n_cont = 0;
     int split = 1;
-  } vc[4];  // [0] ordered (kVcOrdered), [1] split (kVcSplit); experimental: [2] split4, [3] wgather windows
+  } vc[4];  // [0] ordered (kVcOrdered), [1] split (kVcSplit); experimental: [2] split4; [3] wgather windows
+  // k_wgather (x wider than the vcache geometries): eligibility and longest
+  // in-window run measured at create, layout built on first use
+  bool wg_eligible = false;
+  uint32_t wg_max_run = 0;
   struct Sell {  // k_sell layout, built on first use (option "kernel" = SELL)
     bool built = false;
     uint64_t* d_off = nullptr;
@@ -95,6 +101,7 @@ struct hipspmv_handle {
   int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
   uint64_t setup_ns = 0, kernel_ns = 0, h2d_ns = 0, d2h_ns = 0, execs = 0, device_bytes = 0;
   uint32_t max_row_len = 0, empty_rows = 0;
+  int clock_khz = 0;  // shader clock (hipDeviceAttributeClockRate), for the cycle statistics
   int last_kernel = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool pending = false;  // kernel events recorded by exec_device, not yet read
@@ -132,6 +139,70 @@ static void release(hipspmv_t* h) {
   delete h;
 }
 
+// Build vcache-family layout k (geometry g) from `a` and upload it.
+static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g) {
+  auto& v = h->vc[k];
+  VcacheLayout L;
+  build_vcache(a, g, L);
+  v.split = g.split;
+  v.rows_per_block = L.rows_per_block;
+  v.nblocks = L.nblocks;
+  v.npanels = L.npanels;
+  v.part_panels = L.part_panels;
+  v.npad = L.npad;
+  v.max_seg = L.max_seg;
+  v.max_run = L.max_run;
+  v.n_cont = L.n_cont;
+  int st;
+  if ((st = dev_upload(&v.d_seg, L.seg.data(), L.seg.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&v.d_code, L.code.data(), L.code.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&v.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return st;
+  if (v.split > 1) {
+    std::vector<uint32_t> zeros(v.nblocks, 0u);
+    if ((st = dev_upload(&v.d_tickets, zeros.data(), zeros.size(), h->device_bytes))) return st;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&v.d_partial), 8ull * v.split * a.rows));
+    h->device_bytes += 8ull * v.split * a.rows;
+  }
+  v.ok = true;
+  return HIPSPMV_OK;
+}
+
+// The device CSR copy back on the host (the host CSR is gone after create):
+// the source of the layouts built on first use.
+static int download_csr(hipspmv_t* h, HostCSR& a) {
+  a.rows = h->rows;
+  a.cols = h->cols;
+  a.nnz = h->nnz;
+  a.rowptr.resize((size_t)h->rows + 1);
+  a.colind.resize(h->nnz);
+  a.vals.resize(h->nnz);
+  HIP_TRY(hipMemcpy(a.rowptr.data(), h->d_rowptr, 4ull * (h->rows + 1), hipMemcpyDeviceToHost));
+  if (h->nnz) {
+    HIP_TRY(hipMemcpy(a.colind.data(), h->d_colind, 4ull * h->nnz, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(a.vals.data(), h->d_vals, 8ull * h->nnz, hipMemcpyDeviceToHost));
+  }
+  return HIPSPMV_OK;
+}
+
+static int build_wg_layout(hipspmv_t* h) {
+  if (h->vc[3].ok) return HIPSPMV_OK;
+  if (!h->wg_eligible) return HIPSPMV_ERR_UNSUPPORTED;
+  DeviceGuard g(h->device);
+  HostCSR a;
+  if (int st = download_csr(h, a)) return st;
+  const uint64_t bytes0 = h->device_bytes;
+  int st = upload_vc(h, 3, a, kWgWindow);
+  if (st) {  // a later attempt starts from nothing
+    auto& v = h->vc[3];
+    void* vp[] = {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial};
+    for (void* p : vp)
+      if (p) (void)hipFree(p);
+    v = hipspmv_handle::Vc{};
+    h->device_bytes = bytes0;
+  }
+  return st;
+}
+
 static int finish_create(hipspmv_t* h, HostCSR& a) {
   DeviceGuard g(h->device);
   HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
@@ -151,33 +222,19 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   h->ngroups = (uint32_t)groups.size() - 1;
   if ((st = dev_upload(&h->d_groups, groups.data(), groups.size(), h->device_bytes))) return st;
   const VcGeom geoms[4] = {kVcOrdered, kVcSplit, kVcSplit4, kWgWindow};
-  // the experimental layouts are built only on request
+  // the experimental split4 layout is built only on request
   // (HIPSPMV_EXPERIMENTAL=1): each costs another copy of the entries
   const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
-  const int nlayouts = exp && std::strcmp(exp, "1") == 0 ? 4 : 2;
-  for (int k = 0; k < nlayouts; ++k) {
-    auto& v = h->vc[k];
-    v.ok = vcache_eligible(a, geoms[k]);
-    if (!v.ok) continue;
-    VcacheLayout L;
-    build_vcache(a, geoms[k], L);
-    v.split = geoms[k].split;
-    v.rows_per_block = L.rows_per_block;
-    v.nblocks = L.nblocks;
-    v.npanels = L.npanels;
-    v.part_panels = L.part_panels;
-    v.npad = L.npad;
-    v.max_seg = L.max_seg;
-    if ((st = dev_upload(&v.d_seg, L.seg.data(), L.seg.size(), h->device_bytes))) return st;
-    if ((st = dev_upload(&v.d_code, L.code.data(), L.code.size(), h->device_bytes))) return st;
-    if ((st = dev_upload(&v.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return st;
-    if (v.split > 1) {
-      std::vector<uint32_t> zeros(v.nblocks, 0u);
-      if ((st = dev_upload(&v.d_tickets, zeros.data(), zeros.size(), h->device_bytes))) return st;
-      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&v.d_partial), 8ull * v.split * a.rows));
-      h->device_bytes += 8ull * v.split * a.rows;
-    }
+  const bool experimental = exp && std::strcmp(exp, "1") == 0;
+  for (int k = 0; k < 3; ++k) {
+    if (k == 2 && !experimental) continue;
+    if (!vcache_eligible(a, geoms[k])) continue;
+    if ((st = upload_vc(h, k, a, geoms[k]))) return st;
   }
+  // wide x: the windowed gather kernel; its layout waits for first use
+  h->wg_eligible = vcache_eligible(a, kWgWindow);
+  if (h->wg_eligible) h->wg_max_run = vcache_max_run(a, (uint32_t)kWgWindow.panel);
+  if (h->wg_eligible && experimental && (st = upload_vc(h, 3, a, kWgWindow))) return st;
   return HIPSPMV_OK;
 }
 
@@ -188,17 +245,7 @@ static int build_sell_layout(hipspmv_t* h) {
   if (q.built) return HIPSPMV_OK;
   DeviceGuard g(h->device);
   HostCSR a;
-  a.rows = h->rows;
-  a.cols = h->cols;
-  a.nnz = h->nnz;
-  a.rowptr.resize((size_t)h->rows + 1);
-  a.colind.resize(h->nnz);
-  a.vals.resize(h->nnz);
-  HIP_TRY(hipMemcpy(a.rowptr.data(), h->d_rowptr, 4ull * (h->rows + 1), hipMemcpyDeviceToHost));
-  if (h->nnz) {
-    HIP_TRY(hipMemcpy(a.colind.data(), h->d_colind, 4ull * h->nnz, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(a.vals.data(), h->d_vals, 8ull * h->nnz, hipMemcpyDeviceToHost));
-  }
+  if (int st = download_csr(h, a)) return st;
   SellLayout L;
   build_sell(a, L);
   const uint64_t bytes0 = h->device_bytes;
@@ -261,6 +308,7 @@ static int create_common(uint32_t rows, uint32_t cols, uint32_t nnz, int dtype, 
   h->rows = rows;
   h->cols = cols;
   h->nnz = nnz;
+  if (hipDeviceGetAttribute(&h->clock_khz, hipDeviceAttributeClockRate, device) != hipSuccess) h->clock_khz = 0;
   st = finish_create(h, a);
   if (st) {
     release(h);
@@ -286,12 +334,12 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
     case HIPSPMV_KERNEL_VCACHE_SPLIT4:
       if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
       return h->vc[2].ok ? HIPSPMV_KERNEL_VCACHE_SPLIT4 : -HIPSPMV_ERR_UNSUPPORTED;
-    case HIPSPMV_KERNEL_WGATHER:  // ordered: valid in both modes
-      return h->vc[3].ok ? HIPSPMV_KERNEL_WGATHER : -HIPSPMV_ERR_UNSUPPORTED;
+    case HIPSPMV_KERNEL_WGATHER:  // ordered: valid in both modes; layout built on first use
+      return h->vc[3].ok || h->wg_eligible ? HIPSPMV_KERNEL_WGATHER : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_LANE:
       return HIPSPMV_KERNEL_CSR_LANE;
-    case HIPSPMV_KERNEL_SELL:  // ordered: valid in both modes
-      return h->sell.built ? HIPSPMV_KERNEL_SELL : -HIPSPMV_ERR_UNSUPPORTED;
+    case HIPSPMV_KERNEL_SELL:  // ordered: valid in both modes; layout built on first use
+      return HIPSPMV_KERNEL_SELL;
     case HIPSPMV_KERNEL_CSR_VECTOR:
       return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_AUTO:
@@ -299,14 +347,37 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
     default:
       return -HIPSPMV_ERR_INVALID_ARG;
   }
-  // The LDS vector cache pays when each x element a work unit streams feeds
-  // enough nonzeros.
+  // AUTO, from the round-2 sweeps on MI355X:
+  //  * the LDS vector cache pays when each x element a work unit streams
+  //    feeds enough nonzeros and no row runs long inside a segment (C3 FAST:
+  //    vcache_split 145 us);
+  //  * x wider than the vcache geometries, short runs: the windowed gather
+  //    (2^21 x 2^24 stripe shard: wgather 455 us vs sell 1070, csr_vector 1297);
+  //  * otherwise ORDERED takes SELL (C3: 199 us vs vcache 217, csr_lane 1453;
+  //    R-MAT s20: 527 us vs csr_lane 12136) and FAST csr_vector (R-MAT s20:
+  //    253 us vs sell 573, vcache_split 23572).
   auto worth = [&](const hipspmv_handle::Vc& v) {
-    return v.ok && (uint64_t)h->nnz * 16 * v.split >= (uint64_t)v.nblocks * v.split * h->cols;
+    return v.ok && v.max_run <= kVcRunMax &&
+           (uint64_t)h->nnz * 16 * v.split >= (uint64_t)v.nblocks * v.split * h->cols;
   };
+  const bool wg = !h->vc[0].ok && h->wg_eligible && h->wg_max_run <= kVcRunMax;
   if (fast_ok && worth(h->vc[1])) return HIPSPMV_KERNEL_VCACHE_SPLIT;
-  if (worth(h->vc[0])) return HIPSPMV_KERNEL_VCACHE;
-  return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : HIPSPMV_KERNEL_CSR_LANE;
+  if (wg) return HIPSPMV_KERNEL_WGATHER;
+  return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : HIPSPMV_KERNEL_SELL;
+}
+
+// The layout a chosen kernel needs, built on first use (SELL, WGATHER).
+static int ensure_layout(hipspmv_t* h, int kernel) {
+  try {
+    if (kernel == HIPSPMV_KERNEL_SELL) return build_sell_layout(h);
+    if (kernel == HIPSPMV_KERNEL_WGATHER) return build_wg_layout(h);
+  } catch (const std::bad_alloc&) {
+    return HIPSPMV_ERR_OOM;
+  } catch (...) {  // e.g. std::system_error from the layout builder's threads
+    g_last_error = "layout build failed";
+    return HIPSPMV_ERR_HIP;
+  }
+  return HIPSPMV_OK;
 }
 
 static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in, void* d_y_out, int beta,
@@ -403,16 +474,8 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   const std::string k(key);
   if (k == "kernel") {
     if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_SELL) return HIPSPMV_ERR_INVALID_ARG;
-    if (value == HIPSPMV_KERNEL_SELL) {
-      try {
-        if (int st = build_sell_layout(h)) return st;
-      } catch (const std::bad_alloc&) {
-        return HIPSPMV_ERR_OOM;
-      } catch (...) {  // e.g. std::system_error from the layout builder's threads
-        g_last_error = "sell layout build failed";
-        return HIPSPMV_ERR_HIP;
-      }
-    }
+    if (value == HIPSPMV_KERNEL_SELL || value == HIPSPMV_KERNEL_WGATHER)
+      if (int st = ensure_layout(h, (int)value)) return st;
     h->kernel_opt = (int)value;
   } else if (k == "vcache_dma") {
     h->vcache_dma = value ? 1 : 0;
@@ -436,6 +499,7 @@ int hipspmv_exec(hipspmv_t* h, const void* x, void* y, int beta, int mode) {
   if (!h || !x || !y || (beta != 0 && beta != 1)) return HIPSPMV_ERR_INVALID_ARG;
   const int kernel = choose_kernel(h, mode);
   if (kernel < 0) return -kernel;
+  if (int st = ensure_layout(h, kernel)) return st;
   try {
     DeviceGuard g(h->device);
     const size_t bx = 8ull * h->cols, by = 8ull * h->rows;
@@ -480,6 +544,7 @@ int hipspmv_exec_device(hipspmv_t* h, const void* d_x, const void* d_y_in, void*
   if (!h || !d_x || !d_y_out || (beta != 0 && beta != 1) || (beta && !d_y_in)) return HIPSPMV_ERR_INVALID_ARG;
   const int kernel = choose_kernel(h, mode);
   if (kernel < 0) return -kernel;
+  if (int st = ensure_layout(h, kernel)) return st;
   DeviceGuard g(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the default stream
   if (h->timing) HIP_TRY(hipEventRecord(h->ev[1], s));
@@ -526,7 +591,10 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "vcache_x_bytes") *out = h->vc[0].ok ? 8ull * h->vc[0].nblocks * h->cols : 0;
   else if (k == "vcache_split_x_bytes") *out = h->vc[1].ok ? 8ull * h->vc[1].nblocks * h->cols : 0;
   else if (k == "vcache_split4_eligible") *out = h->vc[2].ok;
-  else if (k == "wgather_eligible") *out = h->vc[3].ok;
+  else if (k == "wgather_eligible") *out = h->vc[3].ok || h->wg_eligible;
+  else if (k == "wgather_max_run") *out = h->wg_max_run;
+  else if (k == "vcache_max_run") *out = h->vc[0].max_run;
+  else if (k == "vcache_split_max_run") *out = h->vc[1].max_run;
   else if (k == "wgather_windows") *out = h->vc[3].npanels;
   else if (k == "vcache_split4_x_bytes") *out = h->vc[2].ok ? 8ull * h->vc[2].nblocks * h->cols : 0;
   else if (k == "sell_slices") *out = h->sell.nslices;
@@ -537,6 +605,31 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "max_row_len") *out = h->max_row_len;
   else if (k == "empty_rows") *out = h->empty_rows;
   else if (k == "execs") *out = h->execs;
+  else if (k == "clock_khz") *out = (uint64_t)h->clock_khz;
+  // The reference accelerator's cache statistics (HardwareSpMVNewCache.cpp:
+  // 189-204), restated for the last kernel's layout:
+  else if (k == "read_misses" || k == "hazard_stalls" || k == "ocm_depth") {
+    const int kn = h->last_kernel;
+    const int li = kn == HIPSPMV_KERNEL_VCACHE ? 0 : kn == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1
+                 : kn == HIPSPMV_KERNEL_VCACHE_SPLIT4 ? 2 : kn == HIPSPMV_KERNEL_WGATHER ? 3 : -1;
+    const bool lds_x = li >= 0 && li < 3;  // x panels staged in LDS (wgather gathers x from L2)
+    if (k == "read_misses")  // x words not held on chip when a product needs them
+      *out = lds_x ? (uint64_t)h->vc[li].nblocks * h->cols : (uint64_t)h->nnz;
+    else if (k == "hazard_stalls")  // adds that must wait for the previous add to the same y row
+      *out = li >= 0 ? h->vc[li].n_cont
+           : kn == HIPSPMV_KERNEL_CSR_VECTOR ? 0 : (uint64_t)h->nnz - (h->rows - h->empty_rows);
+    else  // on-chip vector words per workgroup: the y block + the two x panels
+      *out = li >= 0 ? (uint64_t)h->vc[li].rows_per_block +
+                           (lds_x ? 2ull * (li == 0 ? kVcOrdered.panel : li == 1 ? kVcSplit.panel : kVcSplit4.panel) : 0)
+                     : 0;
+  } else if (k == "total_cycles" || k == "active_cycles") {
+    int st = resolve_pending(h);
+    if (st) return st;
+    const double ghz = h->clock_khz / 1e6;
+    // total: the last launch at the shader clock; active: the cycles it would
+    // take at the HBM roofline (8 TB/s) -- active/total = roofline fraction
+    *out = (uint64_t)std::ceil(k == "total_cycles" ? h->kernel_ns * ghz : alg / 8000.0 * ghz);
+  }
   else return HIPSPMV_ERR_KEY;
   return HIPSPMV_OK;
 }

@@ -38,6 +38,11 @@ constexpr int kVcEpt = 2;             // entries per thread held in registers pe
 constexpr int kVcDepth = 4;           // panels of prefetch in flight (entries + x)
 constexpr uint32_t kVcCont = 1u << 30;  // entry continues the previous entry's row run
 constexpr uint32_t kVcMore = 1u << 31;  // next entry continues this entry's row run
+// AUTO uses a vcache-family kernel only when no row has more than kVcRunMax
+// entries inside one segment: a run is walked by one lane, one dependent load
+// per entry (R-MAT s20 with hub rows: 23.6 ms in k_vcache split against
+// 0.25 ms in csr_vector, round-2 sweep).
+constexpr uint32_t kVcRunMax = 16;
 
 // ---- csr_vector geometry ---------------------------------------------------
 constexpr int kCvGroupNnz = 256;  // max nnz of a multi-row group (4 per lane)
@@ -101,6 +106,8 @@ struct VcacheLayout {
   std::vector<uint32_t> code;   // per entry: col_local | row_local << 16 | CONT | MORE
   std::vector<uint64_t> vals;   // per entry
   uint32_t max_seg = 0;
+  uint32_t max_run = 0;  // longest run of one row inside one segment
+  uint64_t n_cont = 0;   // entries continuing a run (added after another entry of their row in one step)
 };
 
 struct SellLayout {
@@ -125,6 +132,7 @@ int copy_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, u
              uint32_t nnz, HostCSR& out, std::string& why);
 
 bool vcache_eligible(const HostCSR& a, const VcGeom& g);
+uint32_t vcache_max_run(const HostCSR& a, uint32_t panel);
 void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out);
 void build_sell(const HostCSR& a, SellLayout& out);
 // Row groups for csr_vector: group g covers rows [groups[g], groups[g+1]).

@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstring>
 #include <new>
@@ -352,7 +353,23 @@ int hipspmv_multi_stat(hipspmv_multi_t* m, const char* key, uint64_t* out) {
       }
     *out = v;
   }
-  else if (k == "alg_bytes") {
+  else if (k == "total_cycles") {  // the multi-device launch (x ready -> last block done) at block 0's clock
+    uint64_t khz = 0;
+    for (auto& s : m->shards)
+      if (s.h && hipspmv_stat(s.h, "clock_khz", &khz) == HIPSPMV_OK) break;
+    *out = (uint64_t)std::ceil(m->kernel_ns * (khz / 1e6));
+  } else if (k == "read_misses" || k == "hazard_stalls" || k == "ocm_depth" ||
+             k == "active_cycles") {  // summed over blocks (misses, stalls) or the largest block's
+    const bool sum = k == "read_misses" || k == "hazard_stalls";
+    uint64_t acc = 0;
+    for (auto& s : m->shards) {
+      uint64_t v = 0;
+      if (!s.h) continue;
+      if (int st = hipspmv_stat(s.h, key, &v)) return st;
+      acc = sum ? acc + v : std::max(acc, v);
+    }
+    *out = acc;
+  } else if (k == "alg_bytes") {
     // per device: its rows' entries + its rowptr + all of x + its y
     uint64_t b = 0;
     for (auto& s : m->shards) b += 12ull * s.nnz + 4ull * (s.rows + 1ull) + 8ull * m->cols + 8ull * s.rows;

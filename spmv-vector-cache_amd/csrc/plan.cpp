@@ -106,6 +106,24 @@ bool vcache_eligible(const HostCSR& a, const VcGeom& g) {
   return true;
 }
 
+// Longest run of one row inside one panel of `panel` columns (columns sorted
+// within each row, as vcache_eligible requires): the kernels walk a run
+// sequentially in one lane, so AUTO keeps matrices with long runs (R-MAT hub
+// rows) off the vcache-family kernels.
+uint32_t vcache_max_run(const HostCSR& a, uint32_t panel) {
+  uint32_t best = 0;
+  for (uint32_t r = 0; r < a.rows; ++r) {
+    uint32_t run = 0, prev = UINT32_MAX;
+    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+      const uint32_t p = a.colind[e] / panel;
+      run = p == prev ? run + 1 : 1;
+      prev = p;
+      best = std::max(best, run);
+    }
+  }
+  return best;
+}
+
 // Entries of row block b that fall into column panel p form segment (b, p),
 // ordered by (row, column); each row's entries keep their CSR order, so a
 // thread that walks a row run in a segment, and the panels in ascending
@@ -129,6 +147,7 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
   out.code.resize(a.nnz);
   out.vals.resize(a.nnz);
   out.max_seg = 0;
+  out.n_cont = 0;
   std::vector<uint32_t> cnt(np + 1);
   uint32_t base = 0;
   for (uint32_t b = 0; b < nb; ++b) {
@@ -153,6 +172,7 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
         uint32_t code = (c - p * P) | ((r - r0) << g.colbits);
         if (p == prev_p && d == prev_d + 1) {  // same row, same segment, adjacent: extend the run
           code |= kVcCont;
+          ++out.n_cont;
           out.code[prev_d] |= kVcMore;
         }
         out.code[d] = code;
@@ -163,6 +183,7 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
     }
     base += cnt[np];
   }
+  out.max_run = vcache_max_run(a, P);
 }
 
 // SELL-C-sigma layout for k_sell (hipspmv_internal.h): within each window of

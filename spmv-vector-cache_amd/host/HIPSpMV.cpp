@@ -112,7 +112,8 @@ std::vector<std::string> HIPSpMV::statKeys() {
   std::vector<std::string> keys = HardwareSpMV::statKeys();
   for (const char* k : {"kernelTimeUs", "setupTimeUs", "h2dTimeUs", "d2hTimeUs", "algKBytes", "mode", "kernel",
                         "device", "error", "numDevices", "bcastTimeUs", "maxAlive", "maxColSpan", "cmstime",
-                        "maxAliveTime", "maxColSpanTime"})
+                        "maxAliveTime", "maxColSpanTime", "totalCycles", "activeCycles", "readMisses",
+                        "hazardStalls", "ocmDepth"})
     keys.push_back(k);
   return keys;
 }
@@ -149,6 +150,17 @@ unsigned int HIPSpMV::statInt(std::string name) {
   if (name == "cmstime") return (unsigned int)(prepStats().cms_ns / 1000);
   if (name == "maxAliveTime") return (unsigned int)(prepStats().max_alive_ns / 1000);
   if (name == "maxColSpanTime") return (unsigned int)(prepStats().max_col_span_ns / 1000);
+  // the reference's cache-behaviour keys (HardwareSpMVNewCache.cpp:189-204), for the last launch:
+  // totalCycles = kernel time x shader clock; activeCycles = the cycles it would take at the HBM
+  // roofline (activeCycles / totalCycles = roofline fraction, the reference's Active/Total);
+  // readMisses = x words not on chip when a product needed them (streamed into the LDS cache, or
+  // gathered from L2/HBM); hazardStalls = adds that waited on the previous add to their y row;
+  // ocmDepth = on-chip vector-cache words per workgroup (y block + x panels)
+  if (name == "totalCycles") return (unsigned int)statU64("total_cycles");
+  if (name == "activeCycles") return (unsigned int)statU64("active_cycles");
+  if (name == "readMisses") return (unsigned int)statU64("read_misses");
+  if (name == "hazardStalls") return (unsigned int)statU64("hazard_stalls");
+  if (name == "ocmDepth") return (unsigned int)statU64("ocm_depth");
   if (name == "thresColPtr") return m_thres.colPtr;
   if (name == "thresRowInd") return m_thres.rowInd;
   if (name == "thresNZData") return m_thres.nzData;

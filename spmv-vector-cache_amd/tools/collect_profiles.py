@@ -83,7 +83,7 @@ def main():
                "|---|---|---|---|---|---|"]
         for path, rows in stats:
             for name, calls, avg, mn, mx in rows[:6]:
-                short = name.split("(")[0].replace("void ", "")
+                short = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
                 md.append(f"| `{os.path.basename(path)}` | `{short}` | {calls} | {avg:.2f} | {mn:.2f} | {mx:.2f} |")
         md.append("")
     if benches:

@@ -36,7 +36,8 @@ s = torch.cuda.current_stream()
 O, F = hs.MODE_ORDERED, hs.MODE_FAST
 # (label, kernel, mode, options); the experimental ones need HIPSPMV_EXPERIMENTAL=1 at create
 cands = [("vcache", "vcache", O, {}), ("csr_lane", "csr_lane", O, {}), ("vcache_split", "vcache_split", F, {}),
-         ("csr_vector", "csr_vector", F, {}), ("sell", "sell", O, {}), ("sell fast", "sell", F, {})]
+         ("csr_vector", "csr_vector", F, {}), ("sell", "sell", O, {}), ("sell fast", "sell", F, {}),
+         ("wgather", "wgather", O, {})]
 if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
     cands += [("vcache xl1", "vcache", O, {"vcache_xlane": 1}), ("vcache xl2", "vcache", O, {"vcache_xlane": 2}),
               ("vcache dma", "vcache", O, {"vcache_dma": 1}),
@@ -47,7 +48,7 @@ if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
               ("vcache xl3", "vcache", O, {"vcache_xlane": 3}), ("split xl3", "vcache_split", F, {"vcache_xlane": 3}),
               ("split4", "vcache_split4", F, {}), ("split4 xl2", "vcache_split4", F, {"vcache_xlane": 2}),
               ("split4 dma xl2", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 2}),
-              ("wgather", "wgather", O, {}), ("wgather xl2", "wgather", O, {"vcache_xlane": 2}),
+              ("wgather xl2", "wgather", O, {"vcache_xlane": 2}),
               ("split4 map", "vcache_split4", F, {"vcache_map": 1}),
               ("split4 map xl3", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 3}),
               ("split4 map xl2", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 2})]

@@ -104,8 +104,8 @@ def test_kernel_resources_within_gfx950_limits(disasm):
 
 
 def test_product_kernels_are_the_gpu_validated_machine_code():
-    """The kernels AUTO selects (vcache ordered + split, csr_lane, csr_vector;
-    f64 and u64) compile to exactly the instructions of the last build that
+    """The kernels AUTO selects (vcache split, sell, wgather, csr_vector; with
+    vcache ordered and csr_lane; f64 and u64) compile to exactly the instructions of the last build that
     passed `pytest -m gpu` on an MI355X (tests/golden/validated_isa.json,
     recorded on the GPU box by tools/record_validated.py from the library those
     tests loaded): the round-end bench runs that machine code."""
@@ -116,7 +116,7 @@ def test_product_kernels_are_the_gpu_validated_machine_code():
     ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "validated_isa.json")))
     now = kernel_isa.fingerprints(os.path.join(LIBDIR, "libhipspmv.so"))
     base = {n[:n.index(">(") + 1] if ">(" in n else n: v for n, v in now.items()}
-    assert len(ref["kernels"]) == 8
+    assert len(ref["kernels"]) >= 8
     for k in ref["kernels"]:
         assert k["current"] in base, k["current"]
         assert base[k["current"]]["sha256"] == k["sha256"], f"{k['current']} differs from the validated build"

@@ -112,7 +112,8 @@ U64_KERNELS = {  # (kernel, mode); the C3 list includes the vector-cache kernels
     "c3_csr": [("vcache", hs.MODE_ORDERED), ("vcache_split", hs.MODE_FAST), ("csr_lane", hs.MODE_ORDERED),
                ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
     # wide x (16 M columns, no vector-cache layout): every generic kernel by name
-    "c4_csr": [("csr_lane", hs.MODE_ORDERED), ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
+    "c4_csr": [("csr_lane", hs.MODE_ORDERED), ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST),
+               ("wgather", hs.MODE_ORDERED)],
     "c5_csr": [("csr_lane", hs.MODE_ORDERED), ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
 }
 

@@ -157,9 +157,12 @@ def test_synthetic_c3_full_size_ordered(gpu):
     x = hs.gen_vector(n, 3)
     y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=n)
     h = hs.Handle.from_csc(colptr, rowind, cvals, n, n)
-    assert h.kernel_name(hs.MODE_ORDERED) == "vcache"
+    assert h.kernel_name(hs.MODE_ORDERED) == "sell"  # AUTO's ordered kernel
     y = h.exec(x, beta=0, mode=hs.MODE_ORDERED)
     assert y.tobytes() == y_ref.tobytes()
+    h.set_kernel("vcache")
+    assert h.exec(x, beta=0, mode=hs.MODE_ORDERED).tobytes() == y_ref.tobytes()
+    h.set_kernel("auto")
     # the CSR entry point gives the same bits
     h2 = hs.Handle.from_csr(rowptr, colind, vals, n, n)
     assert h2.exec(x, beta=0).tobytes() == y_ref.tobytes()
@@ -221,6 +224,45 @@ def test_plugin_surface_spmvbench(gpu):
         rows, cols, colptr, rowind, _ = fx.load(r["matrix"])
         assert int(r["maxAlive"]) == oracle.max_alive(rowind, rows), r
         assert int(r["maxColSpan"]) == oracle.max_col_span(colptr, rowind), r
+        # the reference NewCache keys (HardwareSpMVNewCache.cpp:189-204), restated for the GPU
+        assert 0 < int(r["activeCycles"]) <= int(r["totalCycles"]), r  # roofline-time <= kernel time
+        assert int(r["readMisses"]) > 0 and int(r["hazardStalls"]) >= 0, r
+
+
+def _layout_runs(rowptr, colind, rows, panel):
+    """entries continuing a run (same row, same panel as the previous entry): CPU count"""
+    c = colind.astype(np.int64) // panel
+    same = np.zeros(colind.size, bool)
+    same[1:] = c[1:] == c[:-1]
+    same[rowptr[:-1].astype(np.int64)[np.diff(rowptr) > 0]] = False  # a row's first entry never continues
+    return int(same.sum())
+
+
+def test_cache_behaviour_stats(gpu):
+    """read_misses / hazard_stalls / ocm_depth / cycles per kernel, checked against the layout computed
+    on the CPU: x words streamed into LDS by every row block, run continuations, y block + 2 panels"""
+    n = 1 << 18
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+    x = hs.gen_vector(n, 3)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    for kernel, mode, panel in [("vcache_split", hs.MODE_FAST, 6080), ("vcache", hs.MODE_ORDERED, 8128)]:
+        h.set_kernel(kernel)
+        h.exec(x, beta=0, mode=mode)
+        # the layout sizes its row blocks to fill the chip (<= 8192 / 4096 rows)
+        nb = h.stat("vcache_split_units") // 2 if kernel == "vcache_split" else h.stat("vcache_blocks")
+        rpb = h.stat("vcache_split_rows_per_block" if kernel == "vcache_split" else "vcache_rows_per_block")
+        assert nb == -(-n // rpb)
+        assert h.stat("read_misses") == nb * n, kernel  # every row block streams all of x through LDS once
+        assert h.stat("hazard_stalls") == _layout_runs(rowptr, colind, n, panel), kernel
+        assert h.stat("ocm_depth") == rpb + 2 * panel, kernel
+        assert 0 < h.stat("active_cycles") < h.stat("total_cycles"), kernel
+    for kernel, mode in [("sell", hs.MODE_ORDERED), ("csr_vector", hs.MODE_FAST)]:
+        h.set_kernel(kernel)
+        h.exec(x, beta=0, mode=mode)
+        assert h.stat("read_misses") == colind.size, kernel  # every product gathers x from memory
+        assert h.stat("hazard_stalls") == (0 if kernel == "csr_vector" else colind.size - n), kernel
+        assert h.stat("ocm_depth") == 0, kernel
+    h.close()
 
 
 def test_c3_split_deterministic_and_within_bound(gpu):
