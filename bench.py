@@ -67,6 +67,8 @@ def parse():
     p.add_argument("--mode", default="fast", choices=list(MODES))
     p.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"])
     p.add_argument("--scale", type=int, default=24, help="log2 of the matrix dimension for c4/c5")
+    p.add_argument("--shard", default="", metavar="R/N",
+                   help="c4/c5 on one GPU: run rank R's shard of the N-GPU row partition (per-shard kernel time)")
     p.add_argument("--log2-rows", type=int, default=20, help="c3: rows per GPU")
     p.add_argument("--log2-cols", type=int, default=20, help="c3: columns")
     p.add_argument("--nnz-per-row", type=int, default=32)
@@ -222,7 +224,8 @@ def rocprof_leg(a):
              "--steps", str(min(a.steps, 100)), "--warmup", "5", "--workload", a.workload, "--scale", str(a.scale),
              "--log2-rows", str(a.log2_rows), "--log2-cols", str(a.log2_cols), "--nnz-per-row", str(a.nnz_per_row),
              "--kernel", a.kernel, "--mode", a.mode, "--vcache-xlane", str(a.vcache_xlane),
-             "--vcache-dma", str(a.vcache_dma), "--vcache-map", str(a.vcache_map)]
+             "--vcache-dma", str(a.vcache_dma), "--vcache-map", str(a.vcache_map)] + \
+        (["--shard", a.shard] if getattr(a, "shard", "") else [])
     cmd = [exe, "--kernel-trace", "--stats", "-d", outdir, "-o", "run", "--output-format", "csv", "--"] + child
     env = dict(os.environ, TMPDIR="/tmp")
     print(f"[bench] rocprof leg: {' '.join(cmd)}", file=sys.stderr, flush=True)
@@ -299,6 +302,14 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     k = a.nnz_per_row
+    # the row partition: this job's ranks, or (--shard R/N, one GPU) rank R of an N-GPU job
+    prank, pworld = rank, world
+    if a.shard:
+        if world > 1 or a.workload == "c3":
+            raise SystemExit("--shard: c4/c5 on one GPU only")
+        prank, pworld = (int(v) for v in a.shard.split("/"))
+        if not 0 <= prank < pworld:
+            raise SystemExit(f"--shard {a.shard}: need 0 <= R < N")
     t0 = time.perf_counter()
     if a.workload == "c3":
         rows, cols = 1 << a.log2_rows, 1 << a.log2_cols
@@ -310,20 +321,23 @@ def main():
     elif a.workload == "c4":
         n = 1 << a.scale
         # equal blocks, cut at multiples of HIPSPMV_SHARD_ALIGN (include/hipspmv.h)
-        cut = lambda r: n if r >= world else (n * r // world) // hs.SHARD_ALIGN * hs.SHARD_ALIGN  # noqa: E731
-        row0, row1 = cut(rank), cut(rank + 1)
+        cut = lambda r: n if r >= pworld else (n * r // pworld) // hs.SHARD_ALIGN * hs.SHARD_ALIGN  # noqa: E731
+        row0, row1 = cut(prank), cut(prank + 1)
         rows, cols = row1 - row0, n
         rowptr, colind, vals = hs.gen_stripe_csr(row0, rows, cols, k, 1, 2)
-        workload = f"C4 stripe-uniform CSR {n}x{n}, {k} nnz/row, {world} equal row blocks"
+        workload = f"C4 stripe-uniform CSR {n}x{n}, {k} nnz/row, {pworld} equal row blocks"
         scaling = "strong"
     else:
         n = 1 << a.scale
-        bounds = hs.partition_row_counts(hs.gen_rmat_row_counts(a.scale, 16, 4), world)
-        row0, row1 = int(bounds[rank]), int(bounds[rank + 1])
+        bounds = hs.partition_row_counts(hs.gen_rmat_row_counts(a.scale, 16, 4), pworld)
+        row0, row1 = int(bounds[prank]), int(bounds[prank + 1])
         rows, cols = row1 - row0, n
         rowptr, colind, vals = hs.gen_rmat_rows(a.scale, row0, row1, 16, 4)
-        workload = f"C5 R-MAT scale {a.scale} (a,b,c=0.57,0.19,0.19), edge factor 16, {world} nnz-balanced row blocks"
+        workload = (f"C5 R-MAT scale {a.scale} (a,b,c=0.57,0.19,0.19), edge factor 16, "
+                    f"{pworld} nnz-balanced row blocks")
         scaling = "strong"
+    if a.shard:
+        workload += f" -- shard {prank} of {pworld} alone on one GPU (rows [{row0},{row1}))"
     h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols, device=local)
     if a.kernel != "auto":
         h.set_kernel(a.kernel)

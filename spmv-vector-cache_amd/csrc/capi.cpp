@@ -355,7 +355,8 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
   //    (2^21 x 2^24 stripe shard: wgather 455 us vs sell 1070, csr_vector 1297);
   //  * otherwise ORDERED takes SELL (C3: 199 us vs vcache 217, csr_lane 1453;
   //    R-MAT s20: 527 us vs csr_lane 12136) and FAST csr_vector (R-MAT s20:
-  //    253 us vs sell 573, vcache_split 23572).
+  //    253 us vs sell 573, vcache_split 23572) unless one row outlasts the
+  //    rest (below).
   auto worth = [&](const hipspmv_handle::Vc& v) {
     return v.ok && v.max_run <= kVcRunMax &&
            (uint64_t)h->nnz * 16 * v.split >= (uint64_t)v.nblocks * v.split * h->cols;
@@ -363,7 +364,14 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
   const bool wg = !h->vc[0].ok && h->wg_eligible && h->wg_max_run <= kVcRunMax;
   if (fast_ok && worth(h->vc[1])) return HIPSPMV_KERNEL_VCACHE_SPLIT;
   if (wg) return HIPSPMV_KERNEL_WGATHER;
-  return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : HIPSPMV_KERNEL_SELL;
+  if (!fast_ok) return HIPSPMV_KERNEL_SELL;
+  // csr_vector gives a long row one wave (256 entries per ~1.6 us step): when
+  // that row alone outlasts the bulk of the matrix (~1 TB/s of algorithmic
+  // bytes), SELL's FAST hub pieces spread it over many waves.  C5 shard 0 of 8
+  // (70 k hub rows, longest 238 k): csr_vector 2019 us, sell 496 us; R-MAT s20
+  // (longest 39.7 k): csr_vector 253 us, sell 573 us.
+  const uint64_t alg = 12ull * h->nnz + 4ull * (h->rows + 1ull) + 8ull * h->cols + 8ull * h->rows;
+  return (uint64_t)h->max_row_len * 4167ull > alg ? HIPSPMV_KERNEL_SELL : HIPSPMV_KERNEL_CSR_VECTOR;
 }
 
 // The layout a chosen kernel needs, built on first use (SELL, WGATHER).

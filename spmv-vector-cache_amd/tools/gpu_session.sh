@@ -43,6 +43,8 @@ for s in $STEPS; do
     sweepwide) step sweep_wide 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 21 --log2-cols 24 ;;
     c4) step bench_c4 900 python bench.py --workload c4 --steps 20 --warmup 5 ;;
     c5) step bench_c5 900 python bench.py --workload c5 --steps 20 --warmup 5 ;;
+    c4shard) step bench_c4_shard 900 python bench.py --workload c4 --shard 0/8 --steps 50 --warmup 5 ;;
+    c5shard) step bench_c5_shard 900 python bench.py --workload c5 --shard 0/8 --steps 50 --warmup 5 ;;
     c4sell) step bench_c4_sell 900 python bench.py --workload c4 --kernel sell --steps 20 --warmup 5 ;;
     c5sell) step bench_c5_sell 900 python bench.py --workload c5 --kernel sell --steps 20 --warmup 5 ;;
     c4wg) HIPSPMV_EXPERIMENTAL=1 step bench_c4_wgather 900 python bench.py --workload c4 --scale 24 --kernel wgather --mode ordered --steps 10 --warmup 3 --no-secondary ;;

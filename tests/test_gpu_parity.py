@@ -265,6 +265,30 @@ def test_cache_behaviour_stats(gpu):
     h.close()
 
 
+def test_auto_fast_long_row_takes_sell(gpu):
+    """AUTO FAST: a row that would outlast the rest in csr_vector (one wave per long row) goes to
+    sell's hub pieces; deterministic and within the FAST bound of the oracle."""
+    rng = np.random.default_rng(5)
+    rows, cols = 2000, 1 << 20
+    lens = np.ones(rows, np.int64)
+    lens[7] = 200_000
+    rowptr = np.zeros(rows + 1, np.uint32)
+    rowptr[1:] = np.cumsum(lens)
+    colind = np.concatenate([np.sort(rng.choice(cols, n, replace=False)) for n in lens]).astype(np.uint32)
+    vals = rng.uniform(-1, 1, colind.size)
+    x = rng.uniform(-1, 1, cols)
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+    assert h.kernel_name(hs.MODE_FAST) == "sell" and h.kernel_name(hs.MODE_ORDERED) == "sell"
+    ys = [h.exec(x, beta=0, mode=hs.MODE_FAST) for _ in range(2)]
+    assert ys[0].tobytes() == ys[1].tobytes()
+    colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+    y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=rows)
+    absprod = np.bincount(np.repeat(np.arange(rows), lens), weights=np.abs(vals * x[colind]), minlength=rows)
+    assert np.all(np.abs(ys[0] - y_ref) <= _fast_bound(lens, absprod, 0))
+    assert h.exec(x, beta=0, mode=hs.MODE_ORDERED).tobytes() == y_ref.tobytes()
+    h.close()
+
+
 def test_c3_split_deterministic_and_within_bound(gpu):
     # vcache_split: two column-half partials combined in fixed order -> identical
     # bits on every run, and within the FAST-mode bound of the oracle
