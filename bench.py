@@ -203,6 +203,43 @@ def kernel_provenance(kname: str, dtype: str = "double"):
             "same_as_gpu_validated_build": ref.get(want[kname]) == mine["sha256"]}
 
 
+def _bench_child(a, steps: int, warmup: int):
+    """This bench, headline mode only (no CPU, copy or secondary legs), as a child command line."""
+    return [sys.executable, os.path.abspath(__file__), "--rocprof-child", "--no-cpu-baseline", "--no-secondary",
+            "--steps", str(steps), "--warmup", str(warmup), "--workload", a.workload, "--scale", str(a.scale),
+            "--log2-rows", str(a.log2_rows), "--log2-cols", str(a.log2_cols), "--nnz-per-row", str(a.nnz_per_row),
+            "--kernel", a.kernel, "--mode", a.mode, "--vcache-xlane", str(a.vcache_xlane),
+            "--vcache-dma", str(a.vcache_dma), "--vcache-map", str(a.vcache_map)] + \
+        (["--shard", a.shard] if getattr(a, "shard", "") else [])
+
+
+def _run_profiled(cmd, logpath: str, timeout: float, label: str):
+    """Run a profiler command as a child in its own session (never exec'd from
+    this process), printing progress every 20 s; killed at `timeout`.
+    Returns (rc or None on time-out, seconds)."""
+    import signal
+    import subprocess
+    env = dict(os.environ, TMPDIR="/tmp")
+    print(f"[bench] {label}: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    t = time.perf_counter()
+    with open(logpath, "w") as log:
+        p = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT, env=env, start_new_session=True, cwd=REPO)
+        rc = None
+        while rc is None:  # a progress line every 20 s, so a watchdog never sees a silent run
+            try:
+                rc = p.wait(timeout=max(0.1, min(20.0, timeout - (time.perf_counter() - t))))
+            except subprocess.TimeoutExpired:
+                waited = time.perf_counter() - t
+                if waited >= timeout:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait()
+                    return None, waited
+                print(f"[bench] {label} running ({waited:.0f} s)", file=sys.stderr, flush=True)
+    dt = time.perf_counter() - t
+    print(f"[bench] {label} done: rc={rc} in {dt:.1f} s", file=sys.stderr, flush=True)
+    return rc, dt
+
+
 def rocprof_leg(a):
     """`rocprofv3 --kernel-trace --stats` over this same bench (headline mode
     only, no CPU or copy legs) as a CHILD process, started before this process
@@ -212,38 +249,17 @@ def rocprof_leg(a):
     the HIP-event one; the full CSVs stay under gpurun_out/rocprof_bench/."""
     import glob
     import shutil
-    import signal
-    import subprocess
     exe = shutil.which("rocprofv3")
     if exe is None:
         return {"error": "rocprofv3 not on PATH"}
     outdir = os.path.join(REPO, ROCPROF_DIR)
     shutil.rmtree(outdir, ignore_errors=True)
     os.makedirs(outdir, exist_ok=True)
-    child = [sys.executable, os.path.abspath(__file__), "--rocprof-child", "--no-cpu-baseline", "--no-secondary",
-             "--steps", str(min(a.steps, 100)), "--warmup", "5", "--workload", a.workload, "--scale", str(a.scale),
-             "--log2-rows", str(a.log2_rows), "--log2-cols", str(a.log2_cols), "--nnz-per-row", str(a.nnz_per_row),
-             "--kernel", a.kernel, "--mode", a.mode, "--vcache-xlane", str(a.vcache_xlane),
-             "--vcache-dma", str(a.vcache_dma), "--vcache-map", str(a.vcache_map)] + \
-        (["--shard", a.shard] if getattr(a, "shard", "") else [])
+    child = _bench_child(a, min(a.steps, 100), 5)
     cmd = [exe, "--kernel-trace", "--stats", "-d", outdir, "-o", "run", "--output-format", "csv", "--"] + child
-    env = dict(os.environ, TMPDIR="/tmp")
-    print(f"[bench] rocprof leg: {' '.join(cmd)}", file=sys.stderr, flush=True)
-    t = time.perf_counter()
-    with open(os.path.join(outdir, "child.log"), "w") as log:
-        p = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT, env=env, start_new_session=True, cwd=REPO)
-        rc = None
-        while rc is None:  # a progress line every 20 s, so a watchdog never sees a silent run
-            try:
-                rc = p.wait(timeout=max(0.1, min(20.0, a.rocprof_timeout - (time.perf_counter() - t))))
-            except subprocess.TimeoutExpired:
-                waited = time.perf_counter() - t
-                if waited >= a.rocprof_timeout:
-                    os.killpg(p.pid, signal.SIGKILL)
-                    p.wait()
-                    return {"error": f"timed out after {a.rocprof_timeout:.0f} s"}
-                print(f"[bench] rocprof leg running ({waited:.0f} s)", file=sys.stderr, flush=True)
-    print(f"[bench] rocprof leg done: rc={rc} in {time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
+    rc, _ = _run_profiled(cmd, os.path.join(outdir, "child.log"), a.rocprof_timeout, "rocprof leg")
+    if rc is None:
+        return {"error": f"timed out after {a.rocprof_timeout:.0f} s"}
     files = sorted(glob.glob(os.path.join(outdir, "**", "*kernel_stats.csv"), recursive=True))
     if rc != 0 or not files:
         return {"error": f"rocprofv3 rc={rc}, {len(files)} kernel_stats.csv files"}
@@ -256,6 +272,34 @@ def rocprof_leg(a):
     s["launches"] = f"{min(a.steps, 100)} timed + 5 warmup + {min(a.steps, 100) + 1} per-launch, headline mode"
     s["csv"] = os.path.relpath(files[0], REPO)
     return s
+
+
+def pmc_leg(a):
+    """HBM traffic of the headline kernel measured by THIS run: two
+    `rocprofv3 --pmc` child passes over the same bench (FETCH_SIZE, then
+    WRITE_SIZE: they cannot share a pass on gfx950, MI355X_MICROARCH.md), each
+    under its own time limit, before this process touches the GPU.  Returns
+    the list of counter CSVs (traffic_from_csv corrects and averages them) or
+    an error string."""
+    import glob
+    import shutil
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return "rocprofv3 not on PATH"
+    files = []
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        outdir = os.path.join(REPO, ROCPROF_DIR + "_pmc_" + counter.lower())
+        shutil.rmtree(outdir, ignore_errors=True)
+        os.makedirs(outdir, exist_ok=True)
+        cmd = [exe, "--pmc", counter, "-d", outdir, "-o", "run", "--output-format", "csv", "--"] + \
+            _bench_child(a, 5, 2)
+        rc, _ = _run_profiled(cmd, os.path.join(outdir, "child.log"), min(a.rocprof_timeout, 120.0),
+                              f"pmc leg {counter}")
+        got = sorted(glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True))
+        if rc != 0 or not got:
+            return f"rocprofv3 --pmc {counter}: rc={rc}, {len(got)} counter CSVs"
+        files += got
+    return files
 
 
 def host_transfer_us(xd, yd, reps: int = 5):
@@ -283,10 +327,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("HIPSPMV_BENCH_BACKEND", "nccl") != "nccl":  # rehearsal: ranks may share a GPU
+        local %= max(torch.cuda.device_count(), 1)
     if world == 1 and a.gpus > 1:
         sys.exit(f"--gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes")
     # N=1: the profiler leg first, while this process has not touched the GPU
     rocprof = None
+    pmc_files = None  # this run's --pmc passes (list of CSVs) or why there are none (str)
     # never nested: a bench already running under a profiler (its env names it) skips the leg
     profiled = any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", "")
     if world == 1 and not a.rocprof_child and not a.no_rocprof and not profiled:
@@ -294,12 +341,23 @@ def main():
             rocprof = rocprof_leg(a)
         except Exception as e:  # reported, never fatal: the bench itself still runs
             rocprof = {"error": f"{type(e).__name__}: {e}"}
+        if not a.traffic_csv:
+            try:
+                pmc_files = pmc_leg(a)
+            except Exception as e:
+                pmc_files = f"{type(e).__name__}: {e}"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL over xGMI ("nccl" is RCCL on ROCm); HIPSPMV_BENCH_BACKEND=gloo rehearses the N>1 path
+        # with several ranks on one GPU (RCCL refuses two ranks on one device)
+        backend = os.environ.get("HIPSPMV_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     k = a.nnz_per_row
     # the row partition: this job's ranks, or (--shard R/N, one GPU) rank R of an N-GPU job
@@ -469,6 +527,11 @@ def main():
     ksub = "k_vcache" if "vcache" in kname else "k_" + kname
     if a.traffic_csv and os.path.exists(a.traffic_csv):
         traffic, traffic_src = traffic_from_csv(a.traffic_csv, ksub), a.traffic_csv
+    elif isinstance(pmc_files, list) and traffic_from_csv(pmc_files, ksub) is not None:
+        traffic = traffic_from_csv(pmc_files, ksub)
+        traffic_src = ("this run: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE child passes of the headline kernel "
+                       "(5 timed + 2 warmup launches each), FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md; "
+                       + ", ".join(os.path.relpath(f, REPO) for f in pmc_files))
     elif kname in PMC_PROFILES and not (a.vcache_xlane or a.vcache_dma or a.vcache_map) and a.workload == "c3" and \
             (rows, cols, k) == (1 << 20, 1 << 20, 32):
         import glob
@@ -547,6 +610,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
+                         **({"traffic_pmc_error": pmc_files} if isinstance(pmc_files, str) else {}),
                          "kernel": "k_" + kname, "alg_bytes_per_launch": alg_bytes,
                          "kernel_us": round(kern_ms * 1e3, 3), "kernel_us_per_launch": launch_us,
                          "measured_copy_gbs": round(copy_gbs, 1),

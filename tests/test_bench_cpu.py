@@ -166,6 +166,48 @@ def test_rocprof_leg_plumbing(tmp_path, monkeypatch):
     assert s["csv"].endswith("run_kernel_stats.csv") and s["tool"] == "rocprofv3 --kernel-trace --stats"
 
 
+FAKE_ROCPROF_PMC = """#!/usr/bin/env python3
+import os, sys
+args = sys.argv[1:]
+assert args[0] == "--pmc" and len(args[1].split()) == 1, args  # one counter per pass, its own run
+assert "--kernel-trace" not in args and "--stats" not in args and "-s" not in args, args
+sep = args.index("--")
+prog = args[sep + 1:]
+assert os.path.basename(prog[0]).startswith("python") and prog[1].endswith("bench.py"), prog
+assert "--rocprof-child" in prog and "--no-secondary" in prog, prog
+d = args[args.index("-d") + 1]
+os.makedirs(os.path.join(d, "host", "9"), exist_ok=True)
+val = {"FETCH_SIZE": 200000.0, "WRITE_SIZE": 16384.0}[args[1]]
+with open(os.path.join(d, "host", "9", "run_counter_collection.csv"), "w") as f:
+    f.write("Correlation_Id,Dispatch_Id,Agent_Id,Queue_Id,Process_Id,Thread_Id,Grid_Size,Kernel_Id,Kernel_Name,"
+            "Workgroup_Size,LDS_Block_Size,Scratch_Size,VGPR_Count,Accum_VGPR_Count,SGPR_Count,Counter_Name,"
+            "Counter_Value\\n")
+    for disp in (1, 2):
+        f.write(f'{disp},{disp},1,1,1,1,262144,7,"void hipspmv::k_vcache<double, 2>(int)",1024,163840,0,88,0,'
+                f'40,{args[1]},{val}\\n')
+"""
+
+
+def test_pmc_leg_traffic(tmp_path, monkeypatch):
+    """The traffic leg: two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over the bench in child mode;
+    traffic = FETCH_SIZE KB x 1024 x 2 + WRITE_SIZE KB x 1024 per launch (a fake rocprofv3; no GPU)."""
+    import argparse
+    import shutil
+    sys.path.insert(0, REPO)
+    import bench
+    fake = tmp_path / "rocprofv3"
+    fake.write_text(FAKE_ROCPROF_PMC)
+    fake.chmod(0o755)
+    monkeypatch.setattr(shutil, "which", lambda name: str(fake) if name == "rocprofv3" else None)
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    a = argparse.Namespace(steps=200, workload="c3", scale=24, log2_rows=20, log2_cols=20, nnz_per_row=32,
+                           kernel="auto", mode="fast", vcache_xlane=0, vcache_dma=0, vcache_map=0,
+                           rocprof_timeout=60.0)
+    files = bench.pmc_leg(a)
+    assert isinstance(files, list) and len(files) == 2, files
+    assert bench.traffic_from_csv(files, "k_vcache") == 200000.0 * 1024 * 2 + 16384.0 * 1024
+
+
 def test_rocprof_leg_timeout_kills_child(tmp_path, monkeypatch):
     import argparse
     import shutil
