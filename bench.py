@@ -77,7 +77,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true", help="skip timing the other mode")
-    p.add_argument("--vcache-xlane", type=int, default=0, choices=[0, 1, 2, 3],
+    p.add_argument("--vcache-xlane", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
                    help="experimental vcache option (include/hipspmv.h); not the default path")
     p.add_argument("--vcache-dma", type=int, default=0, choices=[0, 1], help="experimental LDS-DMA x loader")
     p.add_argument("--vcache-map", type=int, default=0, choices=[0, 1],
@@ -99,13 +99,6 @@ def cpu_model() -> str:
     except OSError:
         pass
     return platform.processor()
-
-
-# PMC passes committed under profiles/ for kernels whose code has not changed
-# since they were collected (the product kernels are checked instruction for
-# instruction against the round-1 build): used for roofline.traffic when no
-# --traffic-csv is given, and named in roofline.traffic_source.
-PMC_PROFILES = {"vcache_split": "profiles/r01/pmc_vcache_split"}
 
 
 def traffic_from_csv(paths, kernel_substr: str):
@@ -182,17 +175,19 @@ def kernel_stats_summary(path: str):
             "min_us": us("minns"), "max_us": us("maxns"), "stddev_us": us("stddev")}
 
 
-def kernel_provenance(kname: str, dtype: str = "double"):
+def kernel_provenance(kname: str, dtype: str = "double", exact: bool = False):
     """Machine-code fingerprint of the timed kernel (tools/kernel_isa.py over
     the libhipspmv.so this run loaded) and whether it equals the build that
-    passed the round-1 GPU session (tests/golden/validated_isa.json)."""
+    last passed `pytest -m gpu` on an MI355X (tests/golden/validated_isa.json)."""
     sys.path.insert(0, os.path.join(REPO, "spmv-vector-cache_amd", "tools"))
     import kernel_isa
     want = {"vcache": f"void hipspmv::k_vcache<{dtype}, 1, 8, 4, 3, 0, 0, false, 0, 0>",
-            "vcache_split": f"void hipspmv::k_vcache<{dtype}, 2, 6, 4, 3, 0, 0, false, 0, 0>",
-            "csr_lane": f"void hipspmv::k_csr_lane<{dtype}>", "csr_vector": f"void hipspmv::k_csr_vector<{dtype}>"}
+            "vcache_split": f"void hipspmv::k_vcache<{dtype}, 3, 6, 4, 3, 0, 0, false, 0, 3>",
+            "csr_lane": f"void hipspmv::k_csr_lane<{dtype}>", "csr_vector": f"void hipspmv::k_csr_vector<{dtype}>",
+            "wgather": f"void hipspmv::k_wgather<{dtype}, 17, 4, 2>",
+            "sell": f"void hipspmv::(anonymous namespace)::k_sell<{dtype}, {'true' if exact else 'false'}>"}
     if kname not in want:
-        return {"kernel": kname, "note": "not one of the round-1 validated kernels"}
+        return {"kernel": kname, "note": "not one of the GPU-validated product kernels"}
     fps = kernel_isa.fingerprints(os.path.join(hs.LIB_DIR, "libhipspmv.so"))
     mine = next((v for n, v in fps.items() if n.startswith(want[kname] + "(")), None)
     if mine is None:
@@ -399,7 +394,7 @@ def main():
     h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols, device=local)
     if a.kernel != "auto":
         h.set_kernel(a.kernel)
-    if a.vcache_xlane or a.vcache_dma or a.vcache_map:
+    if a.vcache_xlane != -1 or a.vcache_dma or a.vcache_map:
         h.set_option("vcache_map", a.vcache_map)
         h.set_option("vcache_xlane", a.vcache_xlane)
         h.set_option("vcache_dma", a.vcache_dma)
@@ -532,15 +527,6 @@ def main():
         traffic_src = ("this run: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE child passes of the headline kernel "
                        "(5 timed + 2 warmup launches each), FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md; "
                        + ", ".join(os.path.relpath(f, REPO) for f in pmc_files))
-    elif kname in PMC_PROFILES and not (a.vcache_xlane or a.vcache_dma or a.vcache_map) and a.workload == "c3" and \
-            (rows, cols, k) == (1 << 20, 1 << 20, 32):
-        import glob
-        d = os.path.join(REPO, PMC_PROFILES[kname])
-        files = sorted(glob.glob(os.path.join(d, "pass*.csv")))
-        if files:
-            traffic = traffic_from_csv(files, ksub)
-            traffic_src = (f"{PMC_PROFILES[kname]}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this kernel "
-                           f"on this workload (committed profile, not this run)")
 
     # parity on rank 0 at N=1: the timed kernels' outputs vs the oracle (checker only)
     cpu = None
@@ -605,7 +591,7 @@ def main():
                        "nnz_total": int(nnz_t.item()), "kernel": kname,
                        "mode": a.mode, "parallelism": f"row-partition x{world}, x broadcast (RCCL) before timing",
                        **({"vcache_xlane": a.vcache_xlane, "vcache_dma": a.vcache_dma, "vcache_map": a.vcache_map}
-                          if a.vcache_xlane or a.vcache_dma or a.vcache_map else {})},
+                          if a.vcache_xlane != -1 or a.vcache_dma or a.vcache_map else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic),

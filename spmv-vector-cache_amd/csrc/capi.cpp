@@ -95,7 +95,7 @@ struct hipspmv_handle {
     uint64_t padding = 0;
   } sell;
   int vcache_dma = 0;    // option "vcache_dma": LDS-DMA x loader (experimental)
-  int vcache_xlane = 0;  // option "vcache_xlane": cross-lane run continuation (experimental)
+  int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
   int vcache_map = 0;    // option "vcache_map": XCD-aware part placement, split 4 (experimental)
   void *d_x = nullptr, *d_y = nullptr;
   int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
@@ -490,7 +490,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "vcache_map") {
     h->vcache_map = value ? 1 : 0;
   } else if (k == "vcache_xlane") {
-    if (value < 0 || value > 3) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < -1 || value > 3) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_xlane = (int)value;
   } else if (k == "mode") {
     if (value != HIPSPMV_MODE_ORDERED && value != HIPSPMV_MODE_FAST) return HIPSPMV_ERR_INVALID_ARG;

@@ -14,17 +14,20 @@ namespace hipspmv {
 // One 1024-thread workgroup per work unit = (row block, column part); LDS
 // holds the block's y accumulators (<= rows doubles), two x panels of `panel`
 // doubles and the unit's segment table (<= kVcSegMax offsets), 163840 B total:
-//   ordered: 4096 rows, 1 part  : 32768 + 2*8128*8 + 1024
-//   split  : 8192 rows, 2 parts : 65536 + 2*6080*8 + 1024
-// The split geometry halves the x bytes each CU streams (the measured limit,
-// DESIGN.md §6.0) and combines the two column-half partials in fixed order
-// (p0 + p1), so it is deterministic but not bit-identical: FAST mode.
+//   ordered: 4096 rows, 1 part   : 32768 + 2*8128*8 + 1024
+//   split  : 12352 rows, 3 parts : 98816 + 2*4000*8 + 1024
+// The split geometry cuts the x bytes each CU streams to a third (each CU's
+// L1->L2 request slots are the measured limit; 3 parts beat
+// 2 and 4 on C3: 131.7 vs 146 and 139.5 us) and combines the column-part
+// partials in fixed order (p0 + p1 + p2), so it is deterministic but not
+// bit-identical: FAST mode.  12352 rows = ceil(2^20 / 85): 85 blocks x 3
+// parts fill the 256 CUs once.
 struct VcGeom {
   int rows, panel, split;
   int colbits = 16;  // entry code: col_local | row_local << colbits | CONT | MORE
 };
 constexpr VcGeom kVcOrdered{4096, 8128, 1};
-constexpr VcGeom kVcSplit{8192, 6080, 2};
+constexpr VcGeom kVcSplit{12352, 4000, 3};
 //   split4 : 16384 rows, 4 parts: 131072 + 2*1984*8 + 1024 (experimental)
 constexpr VcGeom kVcSplit4{16384, 1984, 4};
 // ---- k_wgather: the same segment layout over column WINDOWS of 2^17 columns

@@ -84,7 +84,8 @@ int copy_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, u
 static uint32_t vcache_rows_per_block(uint32_t rows, const VcGeom& g) {
   // About one work unit per CU (256 CUs on MI355X), never more rows than the
   // LDS y budget; at least 64 rows so tiny matrices use few units.
-  uint32_t r = (uint32_t)(((uint64_t)rows * g.split + 255) / 256);
+  const uint32_t units = 256 / (uint32_t)g.split;  // blocks that fill the chip once
+  uint32_t r = (uint32_t)(((uint64_t)rows + units - 1) / units);
   r = std::max<uint32_t>(r, 64);
   return std::min<uint32_t>(r, (uint32_t)g.rows);
 }

@@ -9,10 +9,11 @@
 //
 // Work unit = (row block b, column part h).  SPLIT == 1 (ordered geometry):
 // one part, every row's products are added in ascending column order, starting
-// from y_in or +0.0 -- bit-identical to SoftwareSpMV.  SPLIT == 2 (4): two
-// (four) column parts per block (halving (quartering) the x bytes each CU
-// streams, the measured limit), combined in fixed order y = p0 + p1 (+ p2 +
-// p3) by whichever workgroup of the block finishes last: deterministic,
+// from y_in or +0.0 -- bit-identical to SoftwareSpMV.  SPLIT == 3 (product
+// FAST geometry) or 4 (experimental): three (four) column parts per block,
+// each streaming a third (quarter) of x -- the x requests hold each CU's
+// L1->L2 slots -- combined in fixed order y = p0 + p1 + p2
+// (+ p3) by whichever workgroup of the block finishes last: deterministic,
 // FAST-mode tolerance.
 //
 // Waves are specialised (producer/consumer): waves [0, WL) stream x panels
@@ -39,7 +40,7 @@ struct VcCfg<1> {  // 4096 rows; x panel 63.5 KiB; 8 loader waves (8 pairs/lane)
   static constexpr int VR = kVcOrdered.rows, VP = kVcOrdered.panel, WL = 8, DE = 4, EPT = 3;
 };
 template <>
-struct VcCfg<2> {  // 8192 rows; x panel 47.5 KiB; 6 loader waves (8 pairs/lane), 10 compute waves
+struct VcCfg<3> {  // 12352 rows; x panel 31.25 KiB; 6 loader waves (6 pairs/lane), 10 compute waves
   static constexpr int VR = kVcSplit.rows, VP = kVcSplit.panel, WL = 6, DE = 4, EPT = 3;
 };
 template <>
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   constexpr int NJ = (PAIRS + LT - 1) / LT;  // pairs per loader lane per panel
   static_assert(VR * 8 + 2 * VP * 8 + kVcSegMax * 4 <= 163840, "LDS budget");
   static_assert(WL > 0 && WC > 0, "both roles need waves");
-  static_assert(SPLIT == 1 || SPLIT == 2 || SPLIT == 4, "column parts");
+  static_assert(SPLIT == 1 || SPLIT == 3 || SPLIT == 4, "column parts");
   __shared__ T ylds[VR];
   __shared__ T xb[2][VP];
   __shared__ uint32_t segl[kVcSegMax];
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
     return;
   }
-  // ---- combine the column parts, fixed order p0 + p1 (+ p2 + p3).  Hand-off
+  // ---- combine the column parts, fixed order p0 + p1 + p2 (+ p3).  Hand-off
   // per MI355X_MICROARCH.md (Valid forms, table row 1): every partial byte
   // stored write-through (sc1: agent-scope relaxed atomic store), each storing
   // wave drains vmcnt, one lane adds to the block's counter after the barrier;
@@ -433,25 +434,28 @@ static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
 template <typename T>
 hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   // the layout's geometry must be the one the kernel is compiled for
-  const VcGeom g = a.split == 1 ? kVcOrdered : a.split == 2 ? kVcSplit : kVcSplit4;
+  const VcGeom g = a.split == 1 ? kVcOrdered : a.split == 3 ? kVcSplit : kVcSplit4;
   if (!vcache_grid_ok(a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.panel,
                       a.split, g))
     return hipErrorInvalidValue;
   // cross-lane continuation needs every segment inside the register window
   auto window = [](int split) {
-    const int wl = split == 1 ? VcCfg<1>::WL : split == 2 ? VcCfg<2>::WL : VcCfg<4>::WL;
-    const int ept = split == 1 ? VcCfg<1>::EPT : split == 2 ? VcCfg<2>::EPT : VcCfg<4>::EPT;
+    const int wl = split == 1 ? VcCfg<1>::WL : split == 3 ? VcCfg<3>::WL : VcCfg<4>::WL;
+    const int ept = split == 1 ? VcCfg<1>::EPT : split == 3 ? VcCfg<3>::EPT : VcCfg<4>::EPT;
     return (uint32_t)((kVcThreads / 64 - wl) * 64 * ept);
   };
   // xlane 1: cross-lane continuation; 2: also padded loops and asm rings
   // (entries, and x unless LDS-DMA stages it) with explicit vmcnt waits;
-  // 3: cross-lane continuation and padded loops, the compiler's own waits
-  const int cx = a.xlane && a.max_seg <= window(a.split) ? a.xlane : 0;
+  // 3: cross-lane continuation and padded loops, the compiler's own waits.
+  // -1 (default): 3 for the split geometry (C3: 131.7 us against 135.7 with
+  // the run continuation re-read from memory), 0 for the others.
+  const int xl = a.xlane < 0 ? (a.split == 3 ? 3 : 0) : a.xlane;
+  const int cx = xl && a.max_seg <= window(a.split) ? xl : 0;
   const int ld = a.dma ? 1 : cx == 2 ? 2 : 0;
   if (a.split == 1)
     dispatch<T, 1>(a, s, ld, cx);
-  else if (a.split == 2)
-    dispatch<T, 2>(a, s, ld, cx);
+  else if (a.split == 3)
+    dispatch<T, 3>(a, s, ld, cx);
   else if (a.map)  // experimental: XCD-aware placement of the four column parts
     dispatch<T, 4, 1>(a, s, ld, cx);
   else

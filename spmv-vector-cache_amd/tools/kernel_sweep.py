@@ -49,6 +49,8 @@ if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
               ("split4", "vcache_split4", F, {}), ("split4 xl2", "vcache_split4", F, {"vcache_xlane": 2}),
               ("split4 dma xl2", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 2}),
               ("wgather xl2", "wgather", O, {"vcache_xlane": 2}),
+              ("split4 xl3", "vcache_split4", F, {"vcache_xlane": 3}),
+              ("split4 dma xl3", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 3}),
               ("split4 map", "vcache_split4", F, {"vcache_map": 1}),
               ("split4 map xl3", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 3}),
               ("split4 map xl2", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 2})]
@@ -62,7 +64,7 @@ for rnd in range(a.rounds):  # interleaved rounds in one process (methodology ru
         try:
             h.set_kernel(kname)
             for k in ("vcache_dma", "vcache_xlane", "vcache_map"):
-                h.set_option(k, opts.get(k, 0))
+                h.set_option(k, opts.get(k, -1 if k == "vcache_xlane" else 0))
             h.exec_device(x, y, beta=0, mode=mode, stream=s)
         except hs.HipSpMVError:
             continue

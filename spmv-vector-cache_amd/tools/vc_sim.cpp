@@ -443,14 +443,14 @@ int main(int argc, char** argv) {
                       {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 0},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0},
                       {kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 1},
-                      {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 1},
+                      {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 3, 1},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 1},
                       {kWgWindow.rows, kWgWindow.panel, 0, 4, 2, 1, 2, kWgWindow.colbits},
                       {kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 0, 16, 2},
-                      {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 0, 16, 2},
+                      {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 3, 0, 16, 2},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0, 16, 2},
                       {kWgWindow.rows, kWgWindow.panel, 0, 4, 4, 1, 2, kWgWindow.colbits, 2}};
-  int failures = check_maps<1>() + check_maps<2>() + check_maps<4>();
+  int failures = check_maps<1>() + check_maps<2>() + check_maps<3>() + check_maps<4>();
   {  // the round-1 incident geometry: the ordered (split 1) kernel launched with the split layout's
      // 8192-row blocks -- 256 blocks over 2^20 rows, 128 of them past the last row -- is rejected,
      // as is any grid with a surplus block or a block taller than the kernel's LDS y block
@@ -458,9 +458,10 @@ int main(int argc, char** argv) {
     const bool incident = vcache_grid_ok(n, n, 8192, 256, np, np, np, kVcOrdered.panel, 1, kVcOrdered);
     const bool surplus = vcache_grid_ok(n, n, 4096, 257, np, np, np, kVcOrdered.panel, 1, kVcOrdered);
     const bool good = vcache_grid_ok(n, n, 4096, 256, np, np, np, kVcOrdered.panel, 1, kVcOrdered);
-    const uint32_t nps = (n + kVcSplit.panel - 1) / kVcSplit.panel, part = (nps + 1) / 2;
-    const bool split_wrong_kernel = vcache_grid_ok(n, n, 8192, 128, nps, part, part, kVcSplit.panel, 2, kVcOrdered);
-    const bool split_good = vcache_grid_ok(n, n, 8192, 128, nps, part, part, kVcSplit.panel, 2, kVcSplit);
+    const uint32_t nps = (n + kVcSplit.panel - 1) / kVcSplit.panel, part = (nps + 2) / 3;
+    const uint32_t rs = (n + 84) / 85;  // the product split layout: 85 blocks x 3 parts
+    const bool split_wrong_kernel = vcache_grid_ok(n, n, rs, 85, nps, part, part, kVcSplit.panel, 3, kVcOrdered);
+    const bool split_good = vcache_grid_ok(n, n, rs, 85, nps, part, part, kVcSplit.panel, 3, kVcSplit);
     const bool ok = !incident && !surplus && good && !split_wrong_kernel && split_good;
     std::printf("grid guard (incident geometry rejected, product accepted): %s\n", ok ? "ok" : "FAIL");
     failures += !ok;

@@ -119,7 +119,7 @@ def test_bench_json_contract_single(monkeypatch):
     assert out["parity"].startswith("within FAST bound")
     assert out["secondary"]["mode"] == "ordered" and out["secondary"]["parity"] == "bit-exact vs oracle"
     prov = rf["kernel_provenance"]  # the stand-in reports vcache_split: the real library's fingerprint
-    assert prov["same_as_gpu_validated_build"] is True and prov["kernel"].startswith("void hipspmv::k_vcache<double, 2")
+    assert prov["same_as_gpu_validated_build"] is True and prov["kernel"].startswith("void hipspmv::k_vcache<double, 3")
     rp = out["rocprof"]
     assert rp["kernel"] == "hipspmv::k_fake" and rp["event_kernel_us"] == rf["kernel_us"]
     assert abs(rp["event_over_rocprof"] - rf["kernel_us"] / 1.0) < 1e-3

@@ -245,11 +245,11 @@ def test_cache_behaviour_stats(gpu):
     rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
     x = hs.gen_vector(n, 3)
     h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
-    for kernel, mode, panel in [("vcache_split", hs.MODE_FAST, 6080), ("vcache", hs.MODE_ORDERED, 8128)]:
+    for kernel, mode, panel in [("vcache_split", hs.MODE_FAST, 4000), ("vcache", hs.MODE_ORDERED, 8128)]:
         h.set_kernel(kernel)
         h.exec(x, beta=0, mode=mode)
-        # the layout sizes its row blocks to fill the chip (<= 8192 / 4096 rows)
-        nb = h.stat("vcache_split_units") // 2 if kernel == "vcache_split" else h.stat("vcache_blocks")
+        # the layout sizes its row blocks to fill the chip (<= 12352 / 4096 rows; split: 3 column parts)
+        nb = h.stat("vcache_split_units") // 3 if kernel == "vcache_split" else h.stat("vcache_blocks")
         rpb = h.stat("vcache_split_rows_per_block" if kernel == "vcache_split" else "vcache_rows_per_block")
         assert nb == -(-n // rpb)
         assert h.stat("read_misses") == nb * n, kernel  # every row block streams all of x through LDS once
@@ -290,7 +290,7 @@ def test_auto_fast_long_row_takes_sell(gpu):
 
 
 def test_c3_split_deterministic_and_within_bound(gpu):
-    # vcache_split: two column-half partials combined in fixed order -> identical
+    # vcache_split: three column-part partials combined in fixed order -> identical
     # bits on every run, and within the FAST-mode bound of the oracle
     n = 1 << 20
     rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
@@ -298,8 +298,9 @@ def test_c3_split_deterministic_and_within_bound(gpu):
     h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
     assert h.stat("vcache_split_eligible") == 1
     assert h.kernel_name(hs.MODE_FAST) == "vcache_split"
-    # x streamed into LDS per launch: 256 ordered units x 8 MB, 128 split row blocks x 8 MB
-    assert h.stat("vcache_x_bytes") == 256 * 8 * n and h.stat("vcache_split_x_bytes") == 128 * 8 * n
+    # x streamed into LDS per launch: 256 ordered units x 8 MB; 85 split row blocks x 8 MB (3 parts x 1/3 each)
+    assert h.stat("vcache_x_bytes") == 256 * 8 * n and h.stat("vcache_split_x_bytes") == 85 * 8 * n
+    assert h.stat("vcache_split_units") == 255 and h.stat("vcache_split_rows_per_block") == -(-n // 85)
     ys = [h.exec(x, beta=0, mode=hs.MODE_FAST) for _ in range(3)]
     assert ys[0].tobytes() == ys[1].tobytes() == ys[2].tobytes()
     colptr, rowind, cvals = oracle.csr2csc(n, n, rowptr, colind, vals)
