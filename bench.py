@@ -77,6 +77,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true", help="skip timing the other mode")
+    p.add_argument("--no-graph", action="store_true", help="time K plain launches instead of a captured HIP graph")
     p.add_argument("--vcache-xlane", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
                    help="experimental vcache option (include/hipspmv.h); not the default path")
     p.add_argument("--vcache-dma", type=int, default=0, choices=[0, 1], help="experimental LDS-DMA x loader")
@@ -441,20 +442,45 @@ def main():
         del ys, xg
     stream = torch.cuda.current_stream(dev)
 
+    graph_info = {}
+
     def timed(mode: int):
-        """W warmup + K timed steps; returns (max-over-ranks wall s, kernel ms/launch from HIP events)."""
+        """W warmup + K timed steps; returns (max-over-ranks wall s, kernel ms/launch from HIP events).
+        With --graph (default) the K launches are captured once into a HIP graph on a side stream
+        and the timed region replays it: the same K kernels, without K host launch gaps."""
+        run_stream, g = stream, None
+        if not a.no_graph:
+            gs = torch.cuda.Stream(dev)
+            for _ in range(a.warmup):  # on the capture stream: the handle's scratch ordering stays on it
+                h.exec_device(xd, yd, beta=0, mode=mode, stream=gs)
+            torch.cuda.synchronize()
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=gs):
+                    for _ in range(a.steps):
+                        h.exec_device(xd, yd, beta=0, mode=mode, stream=gs)
+                run_stream = gs
+                graph_info[mode] = f"hipGraph of {a.steps} launches, replayed once"
+            except Exception as e:  # reported; the plain launches below run instead
+                g = None
+                graph_info[mode] = f"capture failed ({type(e).__name__}: {e}); plain launches"
+                torch.cuda.synchronize()
         for _ in range(a.warmup):
-            h.exec_device(xd, yd, beta=0, mode=mode, stream=stream)
+            h.exec_device(xd, yd, beta=0, mode=mode, stream=run_stream)
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         tw = time.perf_counter()
-        ev0.record(stream)
-        for _ in range(a.steps):
-            h.exec_device(xd, yd, beta=0, mode=mode, stream=stream)
-        ev1.record(stream)
+        ev0.record(run_stream)
+        if g is not None:
+            with torch.cuda.stream(run_stream):  # replay() launches on the current stream
+                g.replay()
+        else:
+            for _ in range(a.steps):
+                h.exec_device(xd, yd, beta=0, mode=mode, stream=run_stream)
+        ev1.record(run_stream)
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -590,6 +616,7 @@ def main():
                        "rows_per_gpu": rows, "cols": cols, "nnz_per_gpu": nnz,
                        "nnz_total": int(nnz_t.item()), "kernel": kname,
                        "mode": a.mode, "parallelism": f"row-partition x{world}, x broadcast (RCCL) before timing",
+                       "launch": graph_info.get(mode, f"{a.steps} plain launches"),
                        **({"vcache_xlane": a.vcache_xlane, "vcache_dma": a.vcache_dma, "vcache_map": a.vcache_map}
                           if a.vcache_xlane != -1 or a.vcache_dma or a.vcache_map else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
