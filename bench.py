@@ -80,7 +80,8 @@ def parse():
     p.add_argument("--no-graph", action="store_true", help="time K plain launches instead of a captured HIP graph")
     p.add_argument("--vcache-xlane", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
                    help="experimental vcache option (include/hipspmv.h); not the default path")
-    p.add_argument("--vcache-dma", type=int, default=0, choices=[0, 1], help="experimental LDS-DMA x loader")
+    p.add_argument("--vcache-dma", type=int, default=-1, choices=[-1, 0, 1],
+                   help="LDS-DMA x loader (-1: the library default, on for the split geometry)")
     p.add_argument("--vcache-map", type=int, default=0, choices=[0, 1],
                    help="experimental XCD-aware placement of vcache_split4's column parts")
     p.add_argument("--traffic-csv", default=None,
@@ -183,7 +184,7 @@ def kernel_provenance(kname: str, dtype: str = "double", exact: bool = False):
     sys.path.insert(0, os.path.join(REPO, "spmv-vector-cache_amd", "tools"))
     import kernel_isa
     want = {"vcache": f"void hipspmv::k_vcache<{dtype}, 1, 8, 4, 3, 0, 0, false, 0, 0>",
-            "vcache_split": f"void hipspmv::k_vcache<{dtype}, 3, 6, 4, 3, 0, 0, false, 0, 3>",
+            "vcache_split": f"void hipspmv::k_vcache<{dtype}, 3, 2, 4, 2, 0, 0, false, 1, 3>",
             "csr_lane": f"void hipspmv::k_csr_lane<{dtype}>", "csr_vector": f"void hipspmv::k_csr_vector<{dtype}>",
             "wgather": f"void hipspmv::k_wgather<{dtype}, 17, 4, 2>",
             "sell": f"void hipspmv::(anonymous namespace)::k_sell<{dtype}, {'true' if exact else 'false'}>"}
@@ -395,7 +396,7 @@ def main():
     h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols, device=local)
     if a.kernel != "auto":
         h.set_kernel(a.kernel)
-    if a.vcache_xlane != -1 or a.vcache_dma or a.vcache_map:
+    if a.vcache_xlane != -1 or a.vcache_dma != -1 or a.vcache_map:
         h.set_option("vcache_map", a.vcache_map)
         h.set_option("vcache_xlane", a.vcache_xlane)
         h.set_option("vcache_dma", a.vcache_dma)
@@ -618,7 +619,7 @@ def main():
                        "mode": a.mode, "parallelism": f"row-partition x{world}, x broadcast (RCCL) before timing",
                        "launch": graph_info.get(mode, f"{a.steps} plain launches"),
                        **({"vcache_xlane": a.vcache_xlane, "vcache_dma": a.vcache_dma, "vcache_map": a.vcache_map}
-                          if a.vcache_xlane != -1 or a.vcache_dma or a.vcache_map else {})},
+                          if a.vcache_xlane != -1 or a.vcache_dma != -1 or a.vcache_map else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic),

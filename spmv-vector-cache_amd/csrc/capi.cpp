@@ -94,7 +94,7 @@ struct hipspmv_handle {
     uint32_t nslices = 0, nhubs = 0, npieces = 0;
     uint64_t padding = 0;
   } sell;
-  int vcache_dma = 0;    // option "vcache_dma": LDS-DMA x loader (experimental)
+  int vcache_dma = -1;   // option "vcache_dma": LDS-DMA x loader (-1 default: on for the split geometry)
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
   int vcache_map = 0;    // option "vcache_map": XCD-aware part placement, split 4 (experimental)
   void *d_x = nullptr, *d_y = nullptr;
@@ -486,7 +486,8 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
       if (int st = ensure_layout(h, (int)value)) return st;
     h->kernel_opt = (int)value;
   } else if (k == "vcache_dma") {
-    h->vcache_dma = value ? 1 : 0;
+    if (value < -1 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
+    h->vcache_dma = (int)value;
   } else if (k == "vcache_map") {
     h->vcache_map = value ? 1 : 0;
   } else if (k == "vcache_xlane") {

@@ -40,8 +40,11 @@ struct VcCfg<1> {  // 4096 rows; x panel 63.5 KiB; 8 loader waves (8 pairs/lane)
   static constexpr int VR = kVcOrdered.rows, VP = kVcOrdered.panel, WL = 8, DE = 4, EPT = 3;
 };
 template <>
-struct VcCfg<3> {  // 12352 rows; x panel 31.25 KiB; 6 loader waves (6 pairs/lane), 10 compute waves
-  static constexpr int VR = kVcSplit.rows, VP = kVcSplit.panel, WL = 6, DE = 4, EPT = 3;
+struct VcCfg<3> {  // 12352 rows; x panel 31.25 KiB; 2 LDS-DMA loader waves, 14 compute waves (2 entries/lane)
+  // round-2 sweep on C3 (WL, DE, EPT, loader): 2/4/2 DMA 125.8 us; 2/6/2 DMA 126.8; 2/8/2 DMA 127.0;
+  // 4/4/3 DMA 128.9; 6/4/3 DMA 129.7; 6/4/3 registers 131.6; 4/4/3, 5/4/3, 6/6/3 registers 133.6-134.2;
+  // 2/4/3 DMA 132.4; 8/4/4 registers 150.4; 1/4/2 and 1/6/2 DMA 172-173 (one loader wave falls behind)
+  static constexpr int VR = kVcSplit.rows, VP = kVcSplit.panel, WL = 2, DE = 4, EPT = 2;
 };
 template <>
 struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane), 14 compute waves
@@ -420,7 +423,16 @@ static void launch_one(const VcacheArgs& a, hipStream_t s) {
 
 template <typename T, int SPLIT, int MAP = 0>
 static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
-  if (cx == 0) {
+  if constexpr (SPLIT == 3) {  // two loader waves: LDS-DMA only (a register-staged panel would spill)
+    if (cx == 0)
+      launch_one<T, 3, 1, 0, MAP>(a, s);
+    else if (cx == 1)
+      launch_one<T, 3, 1, 1, MAP>(a, s);
+    else if (cx == 2)
+      launch_one<T, 3, 1, 2, MAP>(a, s);
+    else
+      launch_one<T, 3, 1, 3, MAP>(a, s);
+  } else if (cx == 0) {
     ld == 1 ? launch_one<T, SPLIT, 1, 0, MAP>(a, s) : launch_one<T, SPLIT, 0, 0, MAP>(a, s);
   } else if (cx == 1) {
     ld == 1 ? launch_one<T, SPLIT, 1, 1, MAP>(a, s) : launch_one<T, SPLIT, 0, 1, MAP>(a, s);
@@ -451,7 +463,10 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   // the run continuation re-read from memory), 0 for the others.
   const int xl = a.xlane < 0 ? (a.split == 3 ? 3 : 0) : a.xlane;
   const int cx = xl && a.max_seg <= window(a.split) ? xl : 0;
-  const int ld = a.dma ? 1 : cx == 2 ? 2 : 0;
+  // dma -1 (default): register-staged x loaders; the split geometry's two
+  // loader waves always stage by LDS-DMA (dispatch)
+  const int dma = a.dma < 0 ? 0 : a.dma;
+  const int ld = dma ? 1 : cx == 2 ? 2 : 0;
   if (a.split == 1)
     dispatch<T, 1>(a, s, ld, cx);
   else if (a.split == 3)

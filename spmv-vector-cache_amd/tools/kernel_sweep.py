@@ -64,7 +64,7 @@ for rnd in range(a.rounds):  # interleaved rounds in one process (methodology ru
         try:
             h.set_kernel(kname)
             for k in ("vcache_dma", "vcache_xlane", "vcache_map"):
-                h.set_option(k, opts.get(k, -1 if k == "vcache_xlane" else 0))
+                h.set_option(k, opts.get(k, -1 if k in ("vcache_xlane", "vcache_dma") else 0))
             h.exec_device(x, y, beta=0, mode=mode, stream=s)
         except hs.HipSpMVError:
             continue

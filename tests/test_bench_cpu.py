@@ -167,7 +167,7 @@ def test_rocprof_leg_plumbing(tmp_path, monkeypatch):
     monkeypatch.setattr(shutil, "which", lambda name: str(fake) if name == "rocprofv3" else None)
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
     a = argparse.Namespace(steps=200, workload="c3", scale=24, log2_rows=20, log2_cols=20, nnz_per_row=32,
-                           kernel="auto", mode="fast", vcache_xlane=0, vcache_dma=0, vcache_map=0,
+                           kernel="auto", mode="fast", vcache_xlane=-1, vcache_dma=-1, vcache_map=0,
                            rocprof_timeout=60.0)
     s = bench.rocprof_leg(a)
     assert "error" not in s, s
@@ -211,7 +211,7 @@ def test_pmc_leg_traffic(tmp_path, monkeypatch):
     monkeypatch.setattr(shutil, "which", lambda name: str(fake) if name == "rocprofv3" else None)
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
     a = argparse.Namespace(steps=200, workload="c3", scale=24, log2_rows=20, log2_cols=20, nnz_per_row=32,
-                           kernel="auto", mode="fast", vcache_xlane=0, vcache_dma=0, vcache_map=0,
+                           kernel="auto", mode="fast", vcache_xlane=-1, vcache_dma=-1, vcache_map=0,
                            rocprof_timeout=60.0)
     files = bench.pmc_leg(a)
     assert isinstance(files, list) and len(files) == 2, files
@@ -229,7 +229,7 @@ def test_rocprof_leg_timeout_kills_child(tmp_path, monkeypatch):
     monkeypatch.setattr(shutil, "which", lambda name: str(fake) if name == "rocprofv3" else None)
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
     a = argparse.Namespace(steps=5, workload="c3", scale=24, log2_rows=20, log2_cols=20, nnz_per_row=32,
-                           kernel="auto", mode="fast", vcache_xlane=0, vcache_dma=0, vcache_map=0,
+                           kernel="auto", mode="fast", vcache_xlane=-1, vcache_dma=-1, vcache_map=0,
                            rocprof_timeout=1.0)
     t = time.perf_counter()
     s = bench.rocprof_leg(a)
