@@ -37,6 +37,8 @@ template <int SPLIT>
 struct VcCfg;
 template <>
 struct VcCfg<1> {  // 4096 rows; x panel 63.5 KiB; 8 loader waves (8 pairs/lane), 8 compute waves
+  // (round 2: 2 / 5 LDS-DMA loaders with 14 / 11 compute waves and cross-lane runs measured 247 / 201 us
+  // against 217 here -- each CU streams all 8 MB of x, so the loaders bound it; AUTO's ORDERED kernel is sell)
   static constexpr int VR = kVcOrdered.rows, VP = kVcOrdered.panel, WL = 8, DE = 4, EPT = 3;
 };
 template <>
@@ -425,13 +427,13 @@ template <typename T, int SPLIT, int MAP = 0>
 static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
   if constexpr (SPLIT == 3) {  // two loader waves: LDS-DMA only (a register-staged panel would spill)
     if (cx == 0)
-      launch_one<T, 3, 1, 0, MAP>(a, s);
+      launch_one<T, SPLIT, 1, 0, MAP>(a, s);
     else if (cx == 1)
-      launch_one<T, 3, 1, 1, MAP>(a, s);
+      launch_one<T, SPLIT, 1, 1, MAP>(a, s);
     else if (cx == 2)
-      launch_one<T, 3, 1, 2, MAP>(a, s);
+      launch_one<T, SPLIT, 1, 2, MAP>(a, s);
     else
-      launch_one<T, 3, 1, 3, MAP>(a, s);
+      launch_one<T, SPLIT, 1, 3, MAP>(a, s);
   } else if (cx == 0) {
     ld == 1 ? launch_one<T, SPLIT, 1, 0, MAP>(a, s) : launch_one<T, SPLIT, 0, 0, MAP>(a, s);
   } else if (cx == 1) {
