@@ -123,25 +123,15 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 1, 8, 4, 3, 3>, 1, "no x", 3);
       variant(k_vcache<double, 1, 8, 4, 3, 12>, 1, "no entries/compute", 12);
       variant(k_vcache<double, 1, 8, 4, 3, 15>, 1, "skeleton", 15);
-    } else if (g.split == 2) {
-      variant(k_vcache<double, 2>, 2, "default (WL6 DE4 EPT3)", 0);
-      variant(k_vcache<double, 2, 6, 4, 3, 0, 0, false, 0, 1>, 2, "xlane1", 0, 10 * 64 * 3);
-      variant(k_vcache<double, 2, 6, 4, 3, 0, 0, false, 2, 2>, 2, "xlane2 (asm rings)", 0, 10 * 64 * 3);
-      variant(k_vcache<double, 2, 6, 4, 3, 0, 0, false, 0, 3>, 2, "xlane3 (padded, compiler waits)", 0, 10 * 64 * 3);
-      variant(k_vcache<double, 2, 6, 6, 3, 0, 0, false, 2, 2>, 2, "xlane2 DE6", 0, 10 * 64 * 3);
-      variant(k_vcache<double, 2, 4, 4, 3, 0, 0, false, 2, 2>, 2, "xlane2 WL4", 0, 12 * 64 * 3);
-      variant(k_vcache<double, 2, 2, 4, 3, 0, 0, false, 1, 2>, 2, "xlane2 DMA WL2", 0, 14 * 64 * 3);
-      variant(k_vcache<double, 2, 6, 4, 3, 12, 0, false, 2, 2>, 2, "xlane2 no entries/compute", 12, 10 * 64 * 3);
-      variant(k_vcache<double, 2, 6, 4, 3, 3, 0, false, 2, 2>, 2, "xlane2 no x", 3, 10 * 64 * 3);
-      variant(k_vcache<double, 2, 2, 4, 3, 0, 0, false, 1>, 2, "DMA WL2 DE4 EPT3", 0);
-      variant(k_vcache<double, 2, 1, 4, 3, 0, 0, false, 1>, 2, "DMA WL1 DE4 EPT3", 0);
-      variant(k_vcache<double, 2, 2, 4, 2, 0, 0, false, 1>, 2, "DMA WL2 DE4 EPT2", 0);
-      variant(k_vcache<double, 2, 4, 4, 2, 0, 0, false, 1>, 2, "DMA WL4 DE4 EPT2", 0);
-      variant(k_vcache<double, 2, 2, 6, 2, 0, 0, false, 1>, 2, "DMA WL2 DE6 EPT2", 0);
-      variant(k_vcache<double, 2, 6, 4, 3, 3>, 2, "no x", 3);
-      variant(k_vcache<double, 2, 6, 4, 3, 12>, 2, "no entries/compute", 12);
-      variant(k_vcache<double, 2, 6, 4, 3, 15>, 2, "skeleton", 15);
-      variant(k_vcache<double, 2, 2, 4, 3, 12, 0, false, 1>, 2, "DMA no entries/compute", 12);
+    } else if (g.split == 3) {  // the product FAST geometry (round 2)
+      variant(k_vcache<double, 3, 2, 4, 2, 0, 0, false, 1, 3>, 3, "product (DMA WL2 DE4 EPT2, xlane3)", 0,
+              14 * 64 * 2);
+      variant(k_vcache<double, 3, 2, 4, 2, 0, 0, false, 1, 0>, 3, "DMA WL2, runs re-read", 0);
+      variant(k_vcache<double, 3, 4, 4, 3, 0, 0, false, 1, 3>, 3, "DMA WL4 EPT3 xlane3", 0, 12 * 64 * 3);
+      variant(k_vcache<double, 3, 6, 4, 3, 0, 0, false, 0, 3>, 3, "registers WL6 EPT3 xlane3", 0, 10 * 64 * 3);
+      variant(k_vcache<double, 3, 2, 4, 2, 3, 0, false, 1, 3>, 3, "no x", 3, 14 * 64 * 2);
+      variant(k_vcache<double, 3, 2, 4, 2, 12, 0, false, 1, 3>, 3, "no entries/compute", 12, 14 * 64 * 2);
+      variant(k_vcache<double, 3, 2, 4, 2, 15, 0, false, 1, 3>, 3, "skeleton", 15, 14 * 64 * 2);
     } else {
       variant(k_vcache<double, 4>, 4, "default (WL2 DE4 EPT2)", 0);
       variant(k_vcache<double, 4, 2, 4, 2, 0, 0, false, 2, 2>, 4, "xlane2 (asm rings)", 0, 14 * 64 * 2);
