@@ -457,7 +457,8 @@ def main():
             torch.cuda.synchronize()
             try:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=gs):
+                # thread_local: other threads' HIP calls (the RCCL watchdog at N>1) stay legal during capture
+                with torch.cuda.graph(g, stream=gs, capture_error_mode="thread_local"):
                     for _ in range(a.steps):
                         h.exec_device(xd, yd, beta=0, mode=mode, stream=gs)
                 run_stream = gs
