@@ -56,7 +56,7 @@ struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane
 // AB: ablation mask for the diagnostic build (tools/vc_ablate.hip); the
 // product instantiates AB = 0 and every hook folds away.  Bits: 1 no x loads,
 // 2 no x LDS stores, 4 no entry loads, 8 no compute, 16 x always from panel 0,
-// 32 no per-panel barrier (wrong results, timing only).
+// 32 no per-panel barrier, 64 no column-part combine (wrong results, timing only).
 template <typename T, int SPLIT, int WL = VcCfg<SPLIT>::WL, int DE = VcCfg<SPLIT>::DE, int EPT = VcCfg<SPLIT>::EPT,
           int AB = 0, int MAP = 0, bool NT = false, int LD = 0, int CX = 0>
 __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restrict__ seg,
@@ -366,6 +366,10 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       }
     }
     if (CX == 2) vm_wait<0>();  // the clamped prefetches past the last panel
+  }
+  if (AB & 64) {  // ablation: no combine, y straight from LDS (timing only)
+    for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
+    return;
   }
   if (SPLIT == 1) {
     for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];

@@ -134,6 +134,10 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 3, 2, 4, 2, 15, 0, false, 1, 3>, 3, "skeleton", 15, 14 * 64 * 2);
       variant(k_vcache<double, 3, 2, 4, 2, 47, 0, false, 1, 3>, 3, "skeleton without step barriers", 47,
               14 * 64 * 2);
+      variant(k_vcache<double, 3, 2, 4, 2, 111, 0, false, 1, 3>, 3, "... and without the combine", 111,
+              14 * 64 * 2);
+      variant(k_vcache<double, 3, 2, 4, 2, 64, 0, false, 1, 3>, 3, "product without the combine", 64,
+              14 * 64 * 2);
     } else {
       variant(k_vcache<double, 4>, 4, "default (WL2 DE4 EPT2)", 0);
       variant(k_vcache<double, 4, 2, 4, 2, 0, 0, false, 2, 2>, 4, "xlane2 (asm rings)", 0, 14 * 64 * 2);
