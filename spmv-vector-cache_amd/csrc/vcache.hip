@@ -42,11 +42,12 @@ struct VcCfg<1> {  // 4096 rows; x panel 63.5 KiB; 8 loader waves (8 pairs/lane)
   static constexpr int VR = kVcOrdered.rows, VP = kVcOrdered.panel, WL = 8, DE = 4, EPT = 3;
 };
 template <>
-struct VcCfg<3> {  // 12352 rows; x panel 31.25 KiB; 2 LDS-DMA loader waves, 14 compute waves (2 entries/lane)
-  // round-2 sweep on C3 (WL, DE, EPT, loader): 2/4/2 DMA 125.8 us; 2/6/2 DMA 126.8; 2/8/2 DMA 127.0;
+struct VcCfg<3> {  // 12352 rows; x panel 31.25 KiB; 3 LDS-DMA loader waves, 13 compute waves (2 entries/lane)
+  // round-2 sweep on C3 (WL, DE, EPT, loader): 3/4/2 DMA 124.6 us; 3/4/3 DMA 131.2; 2/4/2 DMA 125.8-126.3;
+  // 2/6/2 DMA 126.8; 2/8/2 DMA 127.0;
   // 4/4/3 DMA 128.9; 6/4/3 DMA 129.7; 6/4/3 registers 131.6; 4/4/3, 5/4/3, 6/6/3 registers 133.6-134.2;
   // 2/4/3 DMA 132.4; 8/4/4 registers 150.4; 1/4/2 and 1/6/2 DMA 172-173 (one loader wave falls behind)
-  static constexpr int VR = kVcSplit.rows, VP = kVcSplit.panel, WL = 2, DE = 4, EPT = 2;
+  static constexpr int VR = kVcSplit.rows, VP = kVcSplit.panel, WL = 3, DE = 4, EPT = 2;
 };
 template <>
 struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane), 14 compute waves
