@@ -438,16 +438,18 @@ int main(int argc, char** argv) {
   cases.push_back({"random 5000x333", random_csr(5000, 333, 0.12, 9, false)});
   cases.push_back({"random 257x12161 dense rows", random_csr(257, 12161, 0.3, 11, true)});
   cases.push_back({"random 70000x13001", random_csr(70000, 13001, 0.0008, 13, false)});
-  // must match VcCfg<1>/VcCfg<2> in csrc/vcache.hip (WL, DE, EPT)
+  // must match VcCfg<1>/VcCfg<3> in csrc/vcache.hip (WL, DE, EPT); the split product: 3 LDS-DMA loaders,
+  // cross-lane run continuation (CX 2 here models the kernel's xlane 3: same arithmetic, padded loops)
   const Cfg cfgs[] = {{kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 0},
-                      {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 2, 0},
+                      {kVcSplit.rows, kVcSplit.panel, 3, 4, 2, 3, 1, 16, 2},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0},
                       {kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 1},
-                      {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 3, 1},
+                      {kVcSplit.rows, kVcSplit.panel, 3, 4, 2, 3, 1},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 1},
                       {kWgWindow.rows, kWgWindow.panel, 0, 4, 2, 1, 2, kWgWindow.colbits},
                       {kVcOrdered.rows, kVcOrdered.panel, 8, 4, 3, 1, 0, 16, 2},
                       {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 3, 0, 16, 2},
+                      {kVcSplit.rows, kVcSplit.panel, 3, 4, 2, 3, 1, 16, 1},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0, 16, 2},
                       {kWgWindow.rows, kWgWindow.panel, 0, 4, 4, 1, 2, kWgWindow.colbits, 2}};
   int failures = check_maps<1>() + check_maps<2>() + check_maps<3>() + check_maps<4>();
