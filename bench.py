@@ -90,6 +90,11 @@ def parse():
                    help="skip the rocprofv3 --kernel-trace --stats leg (N=1 only; runs before this process uses the GPU)")
     p.add_argument("--rocprof-timeout", type=float, default=300.0)
     p.add_argument("--rocprof-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--no-strong", action="store_true",
+                   help="c3: skip the strong-scaling C4 block (the 2^s x 2^s stripe matrix split over the N ranks)")
+    p.add_argument("--strong-scale", type=int, default=24, help="log2 of the strong block's matrix dimension (C4: 24)")
+    p.add_argument("--parity-rows", type=int, default=2000,
+                   help="rows of each rank's shard recomputed by the oracle after timing (per-rank parity)")
     return p.parse_args()
 
 
@@ -206,7 +211,7 @@ def _bench_child(a, steps: int, warmup: int):
             "--steps", str(steps), "--warmup", str(warmup), "--workload", a.workload, "--scale", str(a.scale),
             "--log2-rows", str(a.log2_rows), "--log2-cols", str(a.log2_cols), "--nnz-per-row", str(a.nnz_per_row),
             "--kernel", a.kernel, "--mode", a.mode, "--vcache-xlane", str(a.vcache_xlane),
-            "--vcache-dma", str(a.vcache_dma), "--vcache-map", str(a.vcache_map)] + \
+            "--vcache-dma", str(a.vcache_dma), "--vcache-map", str(a.vcache_map), "--no-strong"] + \
         (["--shard", a.shard] if getattr(a, "shard", "") else [])
 
 
@@ -319,6 +324,176 @@ def host_transfer_us(xd, yd, reps: int = 5):
     return out[0], out[1]
 
 
+def time_steps(a, h, xd, yd, mode: int, stream, dev, dist, world: int, graph_info: dict):
+    """W warmup + K timed steps of h on (xd -> yd); returns (max-over-ranks wall s, this rank's kernel
+    ms/launch from HIP events, every rank's kernel ms/launch).  With --graph (default) the K launches are
+    captured once into a HIP graph on a side stream and the timed region replays it: the same K kernels,
+    without K host launch gaps."""
+    run_stream, g = stream, None
+    if not a.no_graph:
+        gs = torch.cuda.Stream(dev)
+        for _ in range(a.warmup):  # eager launches on the capture stream, synchronised before the capture
+            h.exec_device(xd, yd, beta=0, mode=mode, stream=gs)
+        torch.cuda.synchronize()
+        try:
+            g = torch.cuda.CUDAGraph()
+            # thread_local: other threads' HIP calls (the RCCL watchdog at N>1) stay legal during capture
+            with torch.cuda.graph(g, stream=gs, capture_error_mode="thread_local"):
+                for _ in range(a.steps):
+                    h.exec_device(xd, yd, beta=0, mode=mode, stream=gs)
+            run_stream = gs
+            graph_info[mode] = f"hipGraph of {a.steps} launches, replayed once"
+        except Exception as e:  # reported; the plain launches below run instead
+            g = None
+            graph_info[mode] = f"capture failed ({type(e).__name__}: {e}); plain launches"
+            torch.cuda.synchronize()
+    for _ in range(a.warmup):
+        h.exec_device(xd, yd, beta=0, mode=mode, stream=run_stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    tw = time.perf_counter()
+    ev0.record(run_stream)
+    if g is not None:
+        with torch.cuda.stream(run_stream):  # replay() launches on the current stream
+            g.replay()
+    else:
+        for _ in range(a.steps):
+            h.exec_device(xd, yd, beta=0, mode=mode, stream=run_stream)
+    ev1.record(run_stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - tw
+    kern = ev0.elapsed_time(ev1) / a.steps
+    del g
+    if dist is None:
+        return wall, kern, [kern]
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+    dist.all_gather(per, torch.tensor([kern], dtype=torch.float64, device=dev))
+    return float(t.item()), kern, [float(v.item()) for v in per]
+
+
+def sample_rows(rowptr: np.ndarray, n: int, seed: int = 0) -> np.ndarray:
+    """Up to n seeded rows of a shard plus its first, last and longest row, ascending."""
+    rows = rowptr.size - 1
+    lens = np.diff(rowptr.astype(np.int64))
+    pick = set(np.random.default_rng(seed).choice(rows, size=min(n, rows), replace=False).tolist())
+    pick |= {0, rows - 1, int(np.argmax(lens))}
+    return np.array(sorted(pick), dtype=np.int64)
+
+
+def shard_parity(rowptr, colind, vals, x: np.ndarray, y: np.ndarray, mode: int, sample: np.ndarray) -> str:
+    """The sampled rows of one rank's y against the oracle (checker only, after the timed region): the
+    rows' sub-CSR summed by oracle.time_spmv_csr_f64_mt on one thread, which adds each row in CSR order
+    with the product rounded first -- SoftwareSpMV's arithmetic (bit-exact vs its CSC scatter for
+    column-sorted rows, as bench's cpu_baseline_all_cores checks).  ORDERED: bit-exact; FAST: the per-row
+    bound of include/hipspmv.h."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    rp = rowptr.astype(np.int64)
+    lens = rp[sample + 1] - rp[sample]
+    idx = np.concatenate([np.arange(rp[r], rp[r + 1]) for r in sample]) if lens.sum() else np.zeros(0, np.int64)
+    sub_rowptr = np.zeros(sample.size + 1, dtype=np.uint32)
+    sub_rowptr[1:] = np.cumsum(lens)
+    sub_col, sub_val = colind[idx], vals[idx]
+    _, y_ref = oracle.time_spmv_csr_f64_mt(sub_rowptr, sub_col, sub_val, x, 1, 1)
+    got = y[sample]
+    if mode == hs.MODE_ORDERED:
+        bad = int(np.sum(got.view(np.uint64) != y_ref.view(np.uint64)))
+        return f"bit-exact vs oracle on {sample.size} rows" if bad == 0 else f"MISMATCH in {bad} of {sample.size} rows"
+    row_of = np.repeat(np.arange(sample.size), lens)
+    absprod = np.bincount(row_of, weights=np.abs(sub_val * x[sub_col]), minlength=sample.size)
+    bound = 2.0 * np.maximum(lens, 1) * 2.0 ** -53 * absprod + 1e-300
+    r = np.abs(got - y_ref) / bound
+    exact = int(np.sum(got.view(np.uint64) == y_ref.view(np.uint64)))
+    return (f"within FAST bound on {sample.size} rows (max err/bound {float(r.max()):.3f}; {exact} bit-exact)"
+            if np.all(r <= 1.0) else f"BOUND VIOLATED in {int(np.sum(r > 1.0))} of {sample.size} rows")
+
+
+def gather_objects(dist, obj, world: int):
+    """Every rank's obj on every rank (a list in rank order); [obj] without torch.distributed."""
+    if dist is None:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def broadcast_x(dist, xd, rank: int, n: int):
+    """x generated on rank 0 and broadcast over RCCL (xGMI); returns the broadcast's mean us (None at N=1)."""
+    if rank == 0:
+        xd.copy_(torch.from_numpy(hs.gen_vector(n, 3)))
+    if dist is None:
+        return None
+    for _ in range(3):
+        dist.broadcast(xd, src=0)
+    torch.cuda.synchronize()
+    dist.barrier()
+    tb = time.perf_counter()
+    reps = 10
+    for _ in range(reps):
+        dist.broadcast(xd, src=0)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - tb) / reps * 1e6
+
+
+def run_strong(a, dist, dev, local: int, rank: int, world: int, stream) -> dict:
+    """SURVEY §8(d)'s strong-scaling view, beside the weak-scaled C3 headline: the C4 stripe matrix
+    (2^s x 2^s, 32 nnz/row) cut into `world` equal row blocks (at multiples of HIPSPMV_SHARD_ALIGN), one
+    per rank, x (all 2^s columns) replicated by an RCCL broadcast before timing; FAST mode, the same step
+    and timing protocol as the headline.  value = all ranks' flops / the max-over-ranks step time, so the
+    driver's 1/2/4/8-GPU runs give the strong-scaling curve (ideal 7.02x at 8, x replicated: SURVEY §8(d)).
+    Each rank checks sampled rows of its shard against the oracle after timing."""
+    n, k = 1 << a.strong_scale, a.nnz_per_row
+    cut = lambda r: n if r >= world else (n * r // world) // hs.SHARD_ALIGN * hs.SHARD_ALIGN  # noqa: E731
+    row0, row1 = cut(rank), cut(rank + 1)
+    rows = row1 - row0
+    tg = time.perf_counter()
+    rowptr, colind, vals = hs.gen_stripe_csr(row0, rows, n, k, 1, 2)
+    gen_s = time.perf_counter() - tg
+    ts = time.perf_counter()
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, n, device=local)
+    setup_s = time.perf_counter() - ts
+    xd = torch.empty(n, dtype=torch.float64, device=dev)
+    bcast_us = broadcast_x(dist, xd, rank, n)
+    yd = torch.empty(rows, dtype=torch.float64, device=dev)
+    mode = hs.MODE_FAST
+    kname = h.kernel_name(mode)
+    graph_info = {}
+    wall, kern, per_rank = time_steps(a, h, xd, yd, mode, stream, dev, dist, world, graph_info)
+    alg = h.stat("alg_bytes")
+    nnz_t = torch.tensor([float(colind.size)], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(nnz_t)
+    nnz_total = int(nnz_t.item())
+    ms = wall / a.steps * 1e3
+    parity = None
+    if not a.no_cpu_baseline:
+        parity = shard_parity(rowptr, colind, vals, xd.cpu().numpy(), yd.cpu().numpy(), mode,
+                              sample_rows(rowptr, a.parity_rows, seed=rank))
+    parities = gather_objects(dist, parity, world)
+    setup_ns = h.stat("setup_ns")
+    h.close()
+    del xd, yd
+    torch.cuda.empty_cache()
+    return {"workload": f"C4 stripe-uniform CSR {n}x{n}, {k} nnz/row, {world} equal row blocks (rows of rank 0: "
+                        f"[{row0},{row1}))", "scaling": "strong", "mode": "fast", "kernel": kname,
+            "value": round(2.0 * nnz_total / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s", "ms_per_step": round(ms, 5),
+            "nnz_total": nnz_total, "rows_per_rank": rows,
+            "launch": graph_info.get(mode, f"{a.steps} plain launches"),
+            "rank_kernel_us": [round(v * 1e3, 3) for v in per_rank],
+            "roofline_frac_rank0": round(alg / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "alg_bytes_rank0": alg, "x_bcast_us": None if bcast_us is None else round(bcast_us, 2),
+            "rank_parity": parities, "gen_s": round(gen_s, 3), "setup_s": round(setup_s, 3),
+            "setup_ns_lib": setup_ns}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -365,7 +540,7 @@ def main():
         prank, pworld = (int(v) for v in a.shard.split("/"))
         if not 0 <= prank < pworld:
             raise SystemExit(f"--shard {a.shard}: need 0 <= R < N")
-    t0 = time.perf_counter()
+    t0 = time.perf_counter()  # synthetic generation (host), then the handle: gen_s / setup_s
     if a.workload == "c3":
         rows, cols = 1 << a.log2_rows, 1 << a.log2_cols
         row0 = rank * rows
@@ -393,6 +568,8 @@ def main():
         scaling = "strong"
     if a.shard:
         workload += f" -- shard {prank} of {pworld} alone on one GPU (rows [{row0},{row1}))"
+    gen_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
     h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols, device=local)
     if a.kernel != "auto":
         h.set_kernel(a.kernel)
@@ -405,20 +582,7 @@ def main():
 
     # x: generated on rank 0, broadcast over RCCL (xGMI) -- the path's one exchange step
     xd = torch.empty(cols, dtype=torch.float64, device=dev)
-    if rank == 0:
-        xd.copy_(torch.from_numpy(hs.gen_vector(cols, 3)))
-    bcast_us = None
-    if dist is not None:
-        for _ in range(3):
-            dist.broadcast(xd, src=0)
-        torch.cuda.synchronize()
-        dist.barrier()
-        tb = time.perf_counter()
-        reps = 10
-        for _ in range(reps):
-            dist.broadcast(xd, src=0)
-        torch.cuda.synchronize()
-        bcast_us = (time.perf_counter() - tb) / reps * 1e6
+    bcast_us = broadcast_x(dist, xd, rank, cols)
     yd = torch.empty(rows, dtype=torch.float64, device=dev)
     # Square, strong-scaled matrices (C4/C5): when y feeds the next x (power
     # iteration), the exchange is an allgather of the y slices into every
@@ -446,56 +610,7 @@ def main():
     graph_info = {}
 
     def timed(mode: int):
-        """W warmup + K timed steps; returns (max-over-ranks wall s, kernel ms/launch from HIP events).
-        With --graph (default) the K launches are captured once into a HIP graph on a side stream
-        and the timed region replays it: the same K kernels, without K host launch gaps."""
-        run_stream, g = stream, None
-        if not a.no_graph:
-            gs = torch.cuda.Stream(dev)
-            for _ in range(a.warmup):  # on the capture stream: the handle's scratch ordering stays on it
-                h.exec_device(xd, yd, beta=0, mode=mode, stream=gs)
-            torch.cuda.synchronize()
-            try:
-                g = torch.cuda.CUDAGraph()
-                # thread_local: other threads' HIP calls (the RCCL watchdog at N>1) stay legal during capture
-                with torch.cuda.graph(g, stream=gs, capture_error_mode="thread_local"):
-                    for _ in range(a.steps):
-                        h.exec_device(xd, yd, beta=0, mode=mode, stream=gs)
-                run_stream = gs
-                graph_info[mode] = f"hipGraph of {a.steps} launches, replayed once"
-            except Exception as e:  # reported; the plain launches below run instead
-                g = None
-                graph_info[mode] = f"capture failed ({type(e).__name__}: {e}); plain launches"
-                torch.cuda.synchronize()
-        for _ in range(a.warmup):
-            h.exec_device(xd, yd, beta=0, mode=mode, stream=run_stream)
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        tw = time.perf_counter()
-        ev0.record(run_stream)
-        if g is not None:
-            with torch.cuda.stream(run_stream):  # replay() launches on the current stream
-                g.replay()
-        else:
-            for _ in range(a.steps):
-                h.exec_device(xd, yd, beta=0, mode=mode, stream=run_stream)
-        ev1.record(run_stream)
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        wall = time.perf_counter() - tw
-        kern = ev0.elapsed_time(ev1) / a.steps
-        if dist is None:
-            return wall, kern, [kern]
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        per = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
-        dist.all_gather(per, torch.tensor([kern], dtype=torch.float64, device=dev))
-        return float(t.item()), kern, [float(v.item()) for v in per]
+        return time_steps(a, h, xd, yd, mode, stream, dev, dist, world, graph_info)
 
     def per_launch_us(mode: int):
         """A separate pass of K launches, one HIP event pair around each on the
@@ -514,8 +629,9 @@ def main():
 
     mode = MODES[a.mode]
     kname = h.kernel_name(mode)
+    other = "ordered" if a.mode == "fast" else "fast"
     wall_max, kern_ms, rank_kern_ms = timed(mode)
-    y_main = yd.cpu().numpy().copy() if rank == 0 else None
+    y_main = yd.cpu().numpy().copy()
     launch_us = per_launch_us(mode)
     if a.rocprof_child:  # only the SpMV kernel in the profiler's table
         copy_gbs, h2d_us, d2h_us = 0.0, 0.0, 0.0
@@ -532,7 +648,7 @@ def main():
     value = total_flops / (ms_per_step * 1e-3) / 1e9
 
     secondary = None
-    other = "ordered" if a.mode == "fast" else "fast"
+    y_other = None
     if not a.no_secondary:
         try:
             k2 = h.kernel_name(MODES[other])
@@ -541,7 +657,7 @@ def main():
                          "value": round(total_flops / (w2 / a.steps) / 1e9, 2),
                          "ms_per_step": round(w2 / a.steps * 1e3, 5), "kernel_us": round(km2 * 1e3, 3),
                          "roofline_frac": round(alg_bytes / (km2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-            y_other = yd.cpu().numpy().copy() if rank == 0 else None
+            y_other = yd.cpu().numpy().copy()
         except hs.HipSpMVError as e:
             secondary = {"mode": other, "error": str(e)}
             y_other = None
@@ -555,6 +671,27 @@ def main():
         traffic_src = ("this run: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE child passes of the headline kernel "
                        "(5 timed + 2 warmup launches each), FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md; "
                        + ", ".join(os.path.relpath(f, REPO) for f in pmc_files))
+
+    setup_ns_lib = h.stat("setup_ns")
+
+    # per-rank parity at every N: sampled rows of each rank's shard vs the oracle (checker only, after timing)
+    rank_parity = None
+    if not a.no_cpu_baseline and not a.rocprof_child:
+        xs = xd.cpu().numpy()
+        smp = sample_rows(rowptr, a.parity_rows, seed=rank)
+        mine = {"rank": rank, "rows": [int(row0), int(row0 + rows)],
+                a.mode: shard_parity(rowptr, colind, vals, xs, y_main, mode, smp)}
+        if secondary is not None and y_other is not None:
+            mine[other] = shard_parity(rowptr, colind, vals, xs, y_other, MODES[other], smp)
+        rank_parity = gather_objects(dist, mine, world)
+
+    # C4 strong-scaling block beside the weak-scaled C3 headline
+    strong = None
+    if a.workload == "c3" and not a.no_strong and not a.rocprof_child:
+        try:
+            strong = run_strong(a, dist, dev, local, rank, world, stream)
+        except Exception as e:  # reported, never fatal for the headline line
+            strong = {"error": f"{type(e).__name__}: {e}"}
 
     # parity on rank 0 at N=1: the timed kernels' outputs vs the oracle (checker only)
     cpu = None
@@ -647,7 +784,14 @@ def main():
             "pcie_us": {"x_h2d": round(h2d_us, 2), "y_d2h": round(d2h_us, 2),
                         "note": "host-buffer path legs (hipspmv_exec), not in value"},
             "rank_kernel_us": [round(v * 1e3, 3) for v in rank_kern_ms],
+            "rank_parity": rank_parity,
+            "strong": strong,
+            # host time to generate the synthetic shard / to build the handle (transpose-free CSR
+            # create: validation, upload, every layout AUTO runs); setup_ns_lib: the library's own
+            # setup_ns statistic after the timed runs (create + layouts built later, if any)
+            "gen_s": round(gen_s, 3),
             "setup_s": round(setup_s, 3),
+            "setup_ns_lib": setup_ns_lib,
         }
         try:  # reported, never fatal
             out["roofline"]["kernel_provenance"] = kernel_provenance(kname)

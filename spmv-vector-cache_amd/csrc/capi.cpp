@@ -81,11 +81,15 @@ struct hipspmv_handle {
     uint64_t n_cont = 0;
     int split = 1;
   } vc[4];  // [0] ordered (kVcOrdered), [1] split (kVcSplit); experimental: [2] split4; [3] wgather windows
+  // The ordered vcache layout is only ever selected by name: its eligibility
+  // and geometry are known at create, its entries built on first selection.
+  bool vc0_eligible = false;
   // k_wgather (x wider than the vcache geometries): eligibility and longest
-  // in-window run measured at create, layout built on first use
+  // in-window run measured at create; the layout is built at create when AUTO
+  // picks the kernel, else on first selection by name
   bool wg_eligible = false;
   uint32_t wg_max_run = 0;
-  struct Sell {  // k_sell layout, built on first use (option "kernel" = SELL)
+  struct Sell {  // k_sell layout: built at create when AUTO picks SELL, else on first selection
     bool built = false;
     uint64_t* d_off = nullptr;
     uint32_t *d_width = nullptr, *d_row = nullptr, *d_len = nullptr, *d_col = nullptr, *d_hubs = nullptr;
@@ -97,9 +101,18 @@ struct hipspmv_handle {
   int vcache_dma = -1;   // option "vcache_dma": LDS-DMA x loader (-1 default: on for the split geometry)
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
   int vcache_map = 0;    // option "vcache_map": XCD-aware part placement, split 4 (experimental)
+  // option "wgather_chunk": row blocks per k_wgather launch:
+  // one launch's blocks are all resident at once (2 per CU), so they walk
+  // the x windows together and the gathered window stays in L2
+  uint32_t wgather_chunk = kWgChunk;
   void *d_x = nullptr, *d_y = nullptr;
   int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
-  uint64_t setup_ns = 0, kernel_ns = 0, h2d_ns = 0, d2h_ns = 0, execs = 0, device_bytes = 0;
+  // setup_ns: create (transpose, validation, uploads, every layout AUTO uses);
+  // layout_ns: layouts built later, on first selection by name (also counted
+  // in the "setup_ns" statistic, so the plugin's setupTimeUs covers them)
+  uint64_t setup_ns = 0, layout_ns = 0, kernel_ns = 0, h2d_ns = 0, d2h_ns = 0, execs = 0, device_bytes = 0;
+  int auto_fallback = 0;  // AUTO layouts that could not be built (device OOM): the generic kernel runs instead
+  int last_beta = 0;
   uint32_t max_row_len = 0, empty_rows = 0;
   int clock_khz = 0;  // shader clock (hipDeviceAttributeClockRate), for the cycle statistics
   int last_kernel = 0;
@@ -139,9 +152,19 @@ static void release(hipspmv_t* h) {
   delete h;
 }
 
-// Build vcache-family layout k (geometry g) from `a` and upload it.
+static void free_vc(hipspmv_t* h, int k) {
+  auto& v = h->vc[k];
+  void* vp[] = {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial};
+  for (void* p : vp)
+    if (p) (void)hipFree(p);
+  v = hipspmv_handle::Vc{};
+}
+
+// Build vcache-family layout k (geometry g) from `a` and upload it; on
+// failure nothing of it stays allocated.
 static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g) {
   auto& v = h->vc[k];
+  const uint64_t bytes0 = h->device_bytes;
   VcacheLayout L;
   build_vcache(a, g, L);
   v.split = g.split;
@@ -153,22 +176,33 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g) {
   v.max_seg = L.max_seg;
   v.max_run = L.max_run;
   v.n_cont = L.n_cont;
+  auto fail = [&](int st) {
+    free_vc(h, k);
+    h->device_bytes = bytes0;
+    return st;
+  };
   int st;
-  if ((st = dev_upload(&v.d_seg, L.seg.data(), L.seg.size(), h->device_bytes))) return st;
-  if ((st = dev_upload(&v.d_code, L.code.data(), L.code.size(), h->device_bytes))) return st;
-  if ((st = dev_upload(&v.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&v.d_seg, L.seg.data(), L.seg.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&v.d_code, L.code.data(), L.code.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&v.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return fail(st);
   if (v.split > 1) {
-    std::vector<uint32_t> zeros(v.nblocks, 0u);
-    if ((st = dev_upload(&v.d_tickets, zeros.data(), zeros.size(), h->device_bytes))) return st;
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&v.d_partial), 8ull * v.split * a.rows));
-    h->device_bytes += 8ull * v.split * a.rows;
+    // [0, nblocks): arrival tickets, [nblocks, 2 nblocks): published partials
+    // (the ticket-first combine of k_vcache); both self-reset after each launch
+    std::vector<uint32_t> zeros(2ull * v.nblocks, 0u);
+    if ((st = dev_upload(&v.d_tickets, zeros.data(), zeros.size(), h->device_bytes))) return fail(st);
+    // partials: part q of block b at (q * nblocks + b) * VRP doubles, VRP = the
+    // geometry's y block rounded up to even (k_vcache's 16-byte combine)
+    const uint64_t pbytes = 8ull * v.split * v.nblocks * (((uint32_t)g.rows + 1) & ~1u);
+    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&v.d_partial), pbytes);
+    if (e != hipSuccess) return fail(hip_fail(e, "hipMalloc(partials)"));
+    h->device_bytes += pbytes;
   }
   v.ok = true;
   return HIPSPMV_OK;
 }
 
 // The device CSR copy back on the host (the host CSR is gone after create):
-// the source of the layouts built on first use.
+// the source of the layouts built on first selection by name.
 static int download_csr(hipspmv_t* h, HostCSR& a) {
   a.rows = h->rows;
   a.cols = h->cols;
@@ -184,68 +218,11 @@ static int download_csr(hipspmv_t* h, HostCSR& a) {
   return HIPSPMV_OK;
 }
 
-static int build_wg_layout(hipspmv_t* h) {
-  if (h->vc[3].ok) return HIPSPMV_OK;
-  if (!h->wg_eligible) return HIPSPMV_ERR_UNSUPPORTED;
-  DeviceGuard g(h->device);
-  HostCSR a;
-  if (int st = download_csr(h, a)) return st;
-  const uint64_t bytes0 = h->device_bytes;
-  int st = upload_vc(h, 3, a, kWgWindow);
-  if (st) {  // a later attempt starts from nothing
-    auto& v = h->vc[3];
-    void* vp[] = {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial};
-    for (void* p : vp)
-      if (p) (void)hipFree(p);
-    v = hipspmv_handle::Vc{};
-    h->device_bytes = bytes0;
-  }
-  return st;
-}
-
-static int finish_create(hipspmv_t* h, HostCSR& a) {
-  DeviceGuard g(h->device);
-  HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-  for (auto& e : h->ev) HIP_TRY(hipEventCreate(&e));
-  HIP_TRY(hipEventCreateWithFlags(&h->scratch_ev, hipEventDisableTiming));
-  for (uint32_t r = 0; r < a.rows; ++r) {
-    const uint32_t len = a.rowptr[r + 1] - a.rowptr[r];
-    h->max_row_len = len > h->max_row_len ? len : h->max_row_len;
-    h->empty_rows += len == 0;
-  }
-  int st;
-  if ((st = dev_upload(&h->d_rowptr, a.rowptr.data(), a.rowptr.size(), h->device_bytes))) return st;
-  if ((st = dev_upload(&h->d_colind, a.colind.data(), a.colind.size(), h->device_bytes))) return st;
-  if ((st = dev_upload(&h->d_vals, a.vals.data(), a.vals.size(), h->device_bytes))) return st;
-  std::vector<uint32_t> groups;
-  build_row_groups(a, groups);
-  h->ngroups = (uint32_t)groups.size() - 1;
-  if ((st = dev_upload(&h->d_groups, groups.data(), groups.size(), h->device_bytes))) return st;
-  const VcGeom geoms[4] = {kVcOrdered, kVcSplit, kVcSplit4, kWgWindow};
-  // the experimental split4 layout is built only on request
-  // (HIPSPMV_EXPERIMENTAL=1): each costs another copy of the entries
-  const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
-  const bool experimental = exp && std::strcmp(exp, "1") == 0;
-  for (int k = 0; k < 3; ++k) {
-    if (k == 2 && !experimental) continue;
-    if (!vcache_eligible(a, geoms[k])) continue;
-    if ((st = upload_vc(h, k, a, geoms[k]))) return st;
-  }
-  // wide x: the windowed gather kernel; its layout waits for first use
-  h->wg_eligible = vcache_eligible(a, kWgWindow);
-  if (h->wg_eligible) h->wg_max_run = vcache_max_run(a, (uint32_t)kWgWindow.panel);
-  if (h->wg_eligible && experimental && (st = upload_vc(h, 3, a, kWgWindow))) return st;
-  return HIPSPMV_OK;
-}
-
-// The SELL layout is built from the device CSR copy (the host CSR is gone
-// after create), once, when the kernel is first selected.
-static int build_sell_layout(hipspmv_t* h) {
+// The SELL layout from the CSR `a`.
+static int build_sell_layout(hipspmv_t* h, const HostCSR& a) {
   auto& q = h->sell;
   if (q.built) return HIPSPMV_OK;
   DeviceGuard g(h->device);
-  HostCSR a;
-  if (int st = download_csr(h, a)) return st;
   SellLayout L;
   build_sell(a, L);
   const uint64_t bytes0 = h->device_bytes;
@@ -278,6 +255,109 @@ static int build_sell_layout(hipspmv_t* h) {
   q.nhubs = L.nhubs;
   q.padding = L.padding;
   q.built = true;
+  return HIPSPMV_OK;
+}
+
+// The vcache-family layout k from the CSR `a` (k 0: ordered vcache, 3: wgather).
+static int build_vc_layout(hipspmv_t* h, int k, const HostCSR& a) {
+  if (h->vc[k].ok) return HIPSPMV_OK;
+  if (k == 0 && !h->vc0_eligible) return HIPSPMV_ERR_UNSUPPORTED;
+  if (k == 3 && !h->wg_eligible) return HIPSPMV_ERR_UNSUPPORTED;
+  DeviceGuard g(h->device);
+  return upload_vc(h, k, a, k == 0 ? kVcOrdered : kWgWindow);
+}
+
+// AUTO, from the round-2 sweeps on MI355X:
+//  * the LDS vector cache pays when each x element a work unit streams
+//    feeds enough nonzeros and no row runs long inside a segment (C3 FAST:
+//    vcache_split 124 us);
+//  * x wider than the vcache geometries, short runs: the windowed gather
+//    (2^21 x 2^24 stripe shard: wgather 455 us vs sell 1070, csr_vector 1297);
+//  * otherwise ORDERED takes SELL (C3: 199 us vs vcache 217, csr_lane 1453;
+//    R-MAT s20: 527 us vs csr_lane 12136) and FAST csr_vector (R-MAT s20:
+//    253 us vs sell 573, vcache_split 23572) unless one row outlasts the
+//    rest (below).
+// `built`: only kernels whose layout exists (the exec paths); false: what
+// AUTO wants (create, which then builds those layouts).  A wanted layout that
+// could not be built falls back to the generic kernel of the mode: csr_lane
+// (ORDERED) or csr_vector (FAST), which need nothing beyond the CSR copy.
+static int auto_pick(const hipspmv_t* h, bool fast_ok, bool built) {
+  auto worth = [&](const hipspmv_handle::Vc& v) {
+    return v.ok && v.max_run <= kVcRunMax &&
+           (uint64_t)h->nnz * 16 * v.split >= (uint64_t)v.nblocks * v.split * h->cols;
+  };
+  const int generic = fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : HIPSPMV_KERNEL_CSR_LANE;
+  if (fast_ok && worth(h->vc[1])) return HIPSPMV_KERNEL_VCACHE_SPLIT;
+  if (!h->vc0_eligible && h->wg_eligible && h->wg_max_run <= kVcRunMax)
+    return !built || h->vc[3].ok ? HIPSPMV_KERNEL_WGATHER : generic;
+  if (!fast_ok) return !built || h->sell.built ? HIPSPMV_KERNEL_SELL : generic;
+  // csr_vector gives a long row one wave (256 entries per ~1.6 us step): when
+  // that row alone outlasts the bulk of the matrix (~1 TB/s of algorithmic
+  // bytes), SELL's FAST hub pieces spread it over many waves.  C5 shard 0 of 8
+  // (70 k hub rows, longest 238 k): csr_vector 2019 us, sell 496 us; R-MAT s20
+  // (longest 39.7 k): csr_vector 253 us, sell 573 us.
+  const uint64_t alg = 12ull * h->nnz + 4ull * (h->rows + 1ull) + 8ull * h->cols + 8ull * h->rows;
+  if ((uint64_t)h->max_row_len * 4167ull > alg) return !built || h->sell.built ? HIPSPMV_KERNEL_SELL : generic;
+  return HIPSPMV_KERNEL_CSR_VECTOR;
+}
+
+static int finish_create(hipspmv_t* h, HostCSR& a) {
+  DeviceGuard g(h->device);
+  HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  for (auto& e : h->ev) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipEventCreateWithFlags(&h->scratch_ev, hipEventDisableTiming));
+  for (uint32_t r = 0; r < a.rows; ++r) {
+    const uint32_t len = a.rowptr[r + 1] - a.rowptr[r];
+    h->max_row_len = len > h->max_row_len ? len : h->max_row_len;
+    h->empty_rows += len == 0;
+  }
+  int st;
+  if ((st = dev_upload(&h->d_rowptr, a.rowptr.data(), a.rowptr.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&h->d_colind, a.colind.data(), a.colind.size(), h->device_bytes))) return st;
+  if ((st = dev_upload(&h->d_vals, a.vals.data(), a.vals.size(), h->device_bytes))) return st;
+  std::vector<uint32_t> groups;
+  build_row_groups(a, groups);
+  h->ngroups = (uint32_t)groups.size() - 1;
+  if ((st = dev_upload(&h->d_groups, groups.data(), groups.size(), h->device_bytes))) return st;
+  // the experimental split4 layout is built only on request
+  // (HIPSPMV_EXPERIMENTAL=1): each costs another copy of the entries
+  const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
+  const bool experimental = exp && std::strcmp(exp, "1") == 0;
+  // ordered vcache: geometry now, entries on first selection by name
+  h->vc0_eligible = vcache_eligible(a, kVcOrdered);
+  if (h->vc0_eligible) {
+    VcacheLayout G;
+    vcache_geometry(a.rows, a.cols, kVcOrdered, G);
+    auto& v = h->vc[0];
+    v.split = 1;
+    v.rows_per_block = G.rows_per_block;
+    v.nblocks = G.nblocks;
+    v.npanels = G.npanels;
+    v.part_panels = G.part_panels;
+    v.npad = G.npad;
+    v.max_run = vcache_max_run(a, (uint32_t)kVcOrdered.panel);
+  }
+  if (vcache_eligible(a, kVcSplit) && (st = upload_vc(h, 1, a, kVcSplit))) return st;
+  if (experimental && vcache_eligible(a, kVcSplit4) && (st = upload_vc(h, 2, a, kVcSplit4))) return st;
+  h->wg_eligible = vcache_eligible(a, kWgWindow);
+  if (h->wg_eligible) h->wg_max_run = vcache_max_run(a, (uint32_t)kWgWindow.panel);
+  // the layouts AUTO will run, built now from the host CSR (no copy back off
+  // the device at first use, and their time is setup time); device OOM here
+  // leaves AUTO on the generic kernels instead of failing the create
+  const bool exact_any = h->dtype == HIPSPMV_U64;
+  for (const bool fast_ok : {exact_any, true}) {
+    const int k = auto_pick(h, fast_ok, false);
+    if (k == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
+    else if (k == HIPSPMV_KERNEL_WGATHER) st = build_vc_layout(h, 3, a);
+    else st = HIPSPMV_OK;
+    if (st == HIPSPMV_ERR_OOM) {
+      h->auto_fallback++;
+      (void)hipGetLastError();  // the failed allocation must not leak into a later check
+    } else if (st) {
+      return st;
+    }
+  }
+  if (experimental && h->wg_eligible && (st = build_vc_layout(h, 3, a))) return st;
   return HIPSPMV_OK;
 }
 
@@ -326,66 +406,55 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
   const bool exact_any = h->dtype == HIPSPMV_U64;  // integer sums are order-independent
   const bool fast_ok = mode == HIPSPMV_MODE_FAST || exact_any;
   switch (h->kernel_opt) {
-    case HIPSPMV_KERNEL_VCACHE:
-      return h->vc[0].ok ? HIPSPMV_KERNEL_VCACHE : -HIPSPMV_ERR_UNSUPPORTED;
+    case HIPSPMV_KERNEL_VCACHE:  // layout built on first selection
+      return h->vc0_eligible ? HIPSPMV_KERNEL_VCACHE : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_VCACHE_SPLIT:
       if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
       return h->vc[1].ok ? HIPSPMV_KERNEL_VCACHE_SPLIT : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_VCACHE_SPLIT4:
       if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
       return h->vc[2].ok ? HIPSPMV_KERNEL_VCACHE_SPLIT4 : -HIPSPMV_ERR_UNSUPPORTED;
-    case HIPSPMV_KERNEL_WGATHER:  // ordered: valid in both modes; layout built on first use
+    case HIPSPMV_KERNEL_WGATHER:  // ordered: valid in both modes
       return h->vc[3].ok || h->wg_eligible ? HIPSPMV_KERNEL_WGATHER : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_LANE:
       return HIPSPMV_KERNEL_CSR_LANE;
-    case HIPSPMV_KERNEL_SELL:  // ordered: valid in both modes; layout built on first use
+    case HIPSPMV_KERNEL_SELL:  // ordered: valid in both modes
       return HIPSPMV_KERNEL_SELL;
     case HIPSPMV_KERNEL_CSR_VECTOR:
       return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_AUTO:
-      break;
+      return auto_pick(h, fast_ok, true);
     default:
       return -HIPSPMV_ERR_INVALID_ARG;
   }
-  // AUTO, from the round-2 sweeps on MI355X:
-  //  * the LDS vector cache pays when each x element a work unit streams
-  //    feeds enough nonzeros and no row runs long inside a segment (C3 FAST:
-  //    vcache_split 145 us);
-  //  * x wider than the vcache geometries, short runs: the windowed gather
-  //    (2^21 x 2^24 stripe shard: wgather 455 us vs sell 1070, csr_vector 1297);
-  //  * otherwise ORDERED takes SELL (C3: 199 us vs vcache 217, csr_lane 1453;
-  //    R-MAT s20: 527 us vs csr_lane 12136) and FAST csr_vector (R-MAT s20:
-  //    253 us vs sell 573, vcache_split 23572) unless one row outlasts the
-  //    rest (below).
-  auto worth = [&](const hipspmv_handle::Vc& v) {
-    return v.ok && v.max_run <= kVcRunMax &&
-           (uint64_t)h->nnz * 16 * v.split >= (uint64_t)v.nblocks * v.split * h->cols;
-  };
-  const bool wg = !h->vc[0].ok && h->wg_eligible && h->wg_max_run <= kVcRunMax;
-  if (fast_ok && worth(h->vc[1])) return HIPSPMV_KERNEL_VCACHE_SPLIT;
-  if (wg) return HIPSPMV_KERNEL_WGATHER;
-  if (!fast_ok) return HIPSPMV_KERNEL_SELL;
-  // csr_vector gives a long row one wave (256 entries per ~1.6 us step): when
-  // that row alone outlasts the bulk of the matrix (~1 TB/s of algorithmic
-  // bytes), SELL's FAST hub pieces spread it over many waves.  C5 shard 0 of 8
-  // (70 k hub rows, longest 238 k): csr_vector 2019 us, sell 496 us; R-MAT s20
-  // (longest 39.7 k): csr_vector 253 us, sell 573 us.
-  const uint64_t alg = 12ull * h->nnz + 4ull * (h->rows + 1ull) + 8ull * h->cols + 8ull * h->rows;
-  return (uint64_t)h->max_row_len * 4167ull > alg ? HIPSPMV_KERNEL_SELL : HIPSPMV_KERNEL_CSR_VECTOR;
 }
 
-// The layout a chosen kernel needs, built on first use (SELL, WGATHER).
+// The layout a kernel selected by name needs, built on its first selection
+// from the device CSR copy (AUTO's layouts exist since create); the time is
+// added to the handle's setup time.
 static int ensure_layout(hipspmv_t* h, int kernel) {
+  const bool need = (kernel == HIPSPMV_KERNEL_SELL && !h->sell.built) ||
+                    (kernel == HIPSPMV_KERNEL_WGATHER && !h->vc[3].ok) ||
+                    (kernel == HIPSPMV_KERNEL_VCACHE && !h->vc[0].ok);
+  if (!need) return HIPSPMV_OK;
+  const uint64_t t0 = now_ns();
+  int st;
   try {
-    if (kernel == HIPSPMV_KERNEL_SELL) return build_sell_layout(h);
-    if (kernel == HIPSPMV_KERNEL_WGATHER) return build_wg_layout(h);
+    DeviceGuard g(h->device);
+    HostCSR a;
+    st = download_csr(h, a);
+    if (!st) {
+      if (kernel == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
+      else st = build_vc_layout(h, kernel == HIPSPMV_KERNEL_WGATHER ? 3 : 0, a);
+    }
   } catch (const std::bad_alloc&) {
-    return HIPSPMV_ERR_OOM;
+    st = HIPSPMV_ERR_OOM;
   } catch (...) {  // e.g. std::system_error from the layout builder's threads
     g_last_error = "layout build failed";
-    return HIPSPMV_ERR_HIP;
+    st = HIPSPMV_ERR_HIP;
   }
-  return HIPSPMV_OK;
+  h->layout_ns += now_ns() - t0;
+  return st;
 }
 
 static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in, void* d_y_out, int beta,
@@ -395,7 +464,15 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   const bool scratch = kernel == HIPSPMV_KERNEL_VCACHE_SPLIT || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4 ||
                        (kernel == HIPSPMV_KERNEL_SELL && h->sell.npieces &&
                         (mode != HIPSPMV_MODE_ORDERED || h->dtype == HIPSPMV_U64));
-  if (scratch && h->scratch_used && h->scratch_stream != s)
+  // Inside a stream capture the handle does not order anything: a graph's
+  // launches are ordered by the graph and the stream it is replayed on, and a
+  // wait on (or a record of) scratch_ev there would tie the graph to an event
+  // recorded outside it.  The caller orders replays against other launches of
+  // the handle (include/hipspmv.h).
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (scratch) HIP_TRY(hipStreamIsCapturing(s, &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (scratch && !capturing && h->scratch_used && h->scratch_stream != s)
     HIP_TRY(hipStreamWaitEvent(s, h->scratch_ev, 0));
   if (kernel == HIPSPMV_KERNEL_SELL) {
     const auto& q = h->sell;
@@ -420,18 +497,20 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                  nullptr,     h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
                  v.npad,      h->nnz - 1, 1,         beta, 0,       (uint32_t)kWgWindow.panel,
                  h->vcache_xlane, v.max_seg};
+    a.chunk = h->wgather_chunk;
     e = launch_wgather(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
     e = kernel == HIPSPMV_KERNEL_CSR_LANE ? launch_csr_lane(h->dtype, a, s) : launch_csr_vector(h->dtype, a, s);
   }
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
-  if (scratch) {
+  if (scratch && !capturing) {
     HIP_TRY(hipEventRecord(h->scratch_ev, s));
     h->scratch_stream = s;
     h->scratch_used = true;
   }
   h->last_kernel = kernel;
+  h->last_beta = beta;
   h->execs++;
   return HIPSPMV_OK;
 }
@@ -482,14 +561,18 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   const std::string k(key);
   if (k == "kernel") {
     if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_SELL) return HIPSPMV_ERR_INVALID_ARG;
-    if (value == HIPSPMV_KERNEL_SELL || value == HIPSPMV_KERNEL_WGATHER)
-      if (int st = ensure_layout(h, (int)value)) return st;
+    if (value == HIPSPMV_KERNEL_VCACHE && !h->vc0_eligible) return HIPSPMV_ERR_UNSUPPORTED;
+    if (value == HIPSPMV_KERNEL_WGATHER && !h->wg_eligible) return HIPSPMV_ERR_UNSUPPORTED;
+    if (int st = ensure_layout(h, (int)value)) return st;
     h->kernel_opt = (int)value;
   } else if (k == "vcache_dma") {
     if (value < -1 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_dma = (int)value;
   } else if (k == "vcache_map") {
     h->vcache_map = value ? 1 : 0;
+  } else if (k == "wgather_chunk") {  // row blocks per k_wgather launch (0: all in one launch)
+    if (value < 0 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
+    h->wgather_chunk = (uint32_t)value;
   } else if (k == "vcache_xlane") {
     if (value < -1 || value > 3) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_xlane = (int)value;
@@ -576,7 +659,11 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "dtype") *out = (uint64_t)h->dtype;
   else if (k == "device") *out = (uint64_t)h->device;
   else if (k == "kernel") *out = (uint64_t)h->last_kernel;
-  else if (k == "setup_ns") *out = h->setup_ns;
+  else if (k == "setup_ns") *out = h->setup_ns + h->layout_ns;
+  else if (k == "create_ns") *out = h->setup_ns;
+  else if (k == "layout_ns") *out = h->layout_ns;
+  else if (k == "auto_fallback") *out = (uint64_t)h->auto_fallback;
+  else if (k == "wgather_chunk") *out = h->wgather_chunk;
   else if (k == "kernel_ns") {
     int st = resolve_pending(h);
     if (st) return st;
@@ -591,13 +678,13 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "vcache_panels") *out = h->vc[0].npanels;
   else if (k == "vcache_rows_per_block") *out = h->vc[0].rows_per_block;
   else if (k == "vcache_max_segment") *out = h->vc[0].max_seg;
-  else if (k == "vcache_eligible") *out = h->vc[0].ok;
+  else if (k == "vcache_eligible") *out = h->vc0_eligible;
   else if (k == "vcache_split_eligible") *out = h->vc[1].ok;
   else if (k == "vcache_split_units") *out = (uint64_t)h->vc[1].nblocks * h->vc[1].split;
   else if (k == "vcache_split_rows_per_block") *out = h->vc[1].rows_per_block;
   // x bytes a launch streams from L2/MALL into LDS: every row block reads all
   // columns once (split: its two halves read one half each)
-  else if (k == "vcache_x_bytes") *out = h->vc[0].ok ? 8ull * h->vc[0].nblocks * h->cols : 0;
+  else if (k == "vcache_x_bytes") *out = h->vc0_eligible ? 8ull * h->vc[0].nblocks * h->cols : 0;
   else if (k == "vcache_split_x_bytes") *out = h->vc[1].ok ? 8ull * h->vc[1].nblocks * h->cols : 0;
   else if (k == "vcache_split4_eligible") *out = h->vc[2].ok;
   else if (k == "wgather_eligible") *out = h->vc[3].ok || h->wg_eligible;

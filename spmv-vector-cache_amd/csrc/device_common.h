@@ -42,6 +42,22 @@ __device__ __forceinline__ u64x2 ald_128(const void* p) {
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
   return r;
 }
+// Write-through (sc1) 16-byte store / load through a buffer descriptor: the
+// hand-off accesses of the column-part combine (MI355X_MICROARCH.md, Valid
+// forms, table row 1: every handed-off byte stored and loaded sc1; aux 16 =
+// sc1, cdna_hip_programming.md Guideline 16 R1).  Builtins, not inline asm:
+// the compiler counts them in its waits and keeps their data registers until
+// the store has read them.  `base` must be wave-uniform; offsets in bytes.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void st_128_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, u64x2 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, 16);
+}
+__device__ __forceinline__ u64x2 ld_128_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16));
+}
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt field");

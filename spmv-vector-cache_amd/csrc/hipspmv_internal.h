@@ -20,8 +20,9 @@ namespace hipspmv {
 // L1->L2 request slots are the measured limit; 3 parts beat
 // 2 and 4 on C3: 131.7 vs 146 and 139.5 us) and combines the column-part
 // partials in fixed order (p0 + p1 + p2), so it is deterministic but not
-// bit-identical: FAST mode.  12352 rows = ceil(2^20 / 85): 85 blocks x 3
-// parts fill the 256 CUs once.
+// bit-identical: FAST mode.  12352 rows is the LDS budget; the layout sizes
+// its blocks to fill the chip once (vcache_rows_per_block: ceil(2^20 / 85) =
+// 12337 rows on C3, 85 blocks x 3 parts = 255 units).
 struct VcGeom {
   int rows, panel, split;
   int colbits = 16;  // entry code: col_local | row_local << colbits | CONT | MORE
@@ -35,6 +36,15 @@ constexpr VcGeom kVcSplit4{16384, 1984, 4};
 // staged in LDS -- for matrices whose x is too wide for LDS streaming to pay
 // (C4/C5: 16M columns).  y block in LDS (<= 8192 rows, 13 bits), ORDERED.
 constexpr VcGeom kWgWindow{8192, 1 << 17, 1, 17};
+// Row blocks per k_wgather launch (option "wgather_chunk"): one per CU.  A
+// matrix with more blocks than that (full C4: 2048 blocks of 8192 rows) runs
+// in several launches, so every launch's workgroups are resident together
+// and walk the x windows in step (one L2-resident window at a time); in one
+// launch, later blocks start at window 0 while earlier ones are deep into x
+// and the chip's gathers spread over many windows.  Full C4 on one GPU
+// (profiles/r03/logs/sweep_c4_s7.log): one launch 6468 us, chunks of 1024
+// 5287, 512 (two per CU) 4078, 256 (one per CU) 3620.
+constexpr uint32_t kWgChunk = 256;
 constexpr int kVcThreads = 1024;
 constexpr int kVcSegMax = 256;        // npad + 1 <= kVcSegMax per unit
 constexpr int kVcEpt = 2;             // entries per thread held in registers per panel
@@ -71,15 +81,25 @@ constexpr uint32_t kSellNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kSellPiece = 4096;
 constexpr int kSellPieceWords = 8;
 
+// Column part h of a geometry with `split` parts owns panels
+// [vc_part_first(h), vc_part_first(h + 1)): floor cuts, so the parts differ by
+// at most one panel and every part owns one as soon as npanels >= split (a
+// ceil cut left the last of three parts empty for 4 panels, 12001-16000
+// columns).  constexpr: the same function on the host (plan.cpp, vc_sim) and
+// in the kernels.
+constexpr uint32_t vc_part_first(uint32_t h, uint32_t npanels, uint32_t split) {
+  return (uint32_t)((uint64_t)h * npanels / split);
+}
+
 // Launch geometry of a vcache-family kernel (k_vcache, k_wgather): true iff
 // every work unit's rows and panels lie inside the matrix for a kernel
 // compiled for geometry g -- the row-block bound, no surplus blocks (a block
 // with r0 >= rows would compute rows - r0 in uint32 and write past y: the
-// round-1 GPU fault), every column covered by the panels, the
-// column parts each non-empty, and the unit's segment table inside LDS.
-// launch_vcache / launch_wgather return hipErrorInvalidValue without a launch
-// when it is false; tools/vc_sim.cpp checks it on the CPU (incl. the incident
-// geometry).
+// round-1 GPU fault), every column covered by the panels, every
+// column part non-empty (npanels >= split), part_panels the largest part, and
+// the unit's segment table inside LDS.  launch_vcache / launch_wgather return
+// hipErrorInvalidValue without a launch when it is false; tools/vc_sim.cpp
+// checks it on the CPU (incl. the incident geometry).
 inline bool vcache_grid_ok(uint32_t rows, uint32_t cols, uint32_t rows_per_block, uint32_t nblocks,
                            uint32_t npanels, uint32_t part_panels, uint32_t npad, uint32_t panel, int split,
                            const VcGeom& g) {
@@ -89,8 +109,8 @@ inline bool vcache_grid_ok(uint32_t rows, uint32_t cols, uint32_t rows_per_block
   if ((uint64_t)nblocks * rows_per_block < rows) return false;         // every row in some block
   if ((uint64_t)(nblocks - 1) * rows_per_block >= rows) return false;  // no surplus block
   if (npanels == 0 || (uint64_t)npanels * g.panel < cols) return false;
-  if ((uint64_t)part_panels * split < npanels) return false;          // every panel in some part
-  if ((uint64_t)part_panels * (split - 1) >= npanels) return false;   // the last part has a panel
+  if (npanels < (uint32_t)split) return false;                         // every part owns a panel
+  if (part_panels != (npanels + split - 1) / split) return false;      // the largest part
   return npad + 1 <= (uint32_t)kVcSegMax && npad >= part_panels;
 }
 
@@ -103,7 +123,7 @@ struct HostCSR {
 struct VcacheLayout {
   VcGeom geom{};
   uint32_t rows_per_block = 0, nblocks = 0, npanels = 0;
-  uint32_t part_panels = 0;  // panels per column part (the last part may have fewer)
+  uint32_t part_panels = 0;  // panels of the largest column part (vc_part_first cuts: parts differ by <= 1)
   uint32_t npad = 0;         // seg entries per unit - 1 (= part_panels)
   std::vector<uint32_t> seg;    // (nblocks * split) units * (npad + 1) global entry offsets
   std::vector<uint32_t> code;   // per entry: col_local | row_local << 16 | CONT | MORE
@@ -135,6 +155,9 @@ int copy_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, u
              uint32_t nnz, HostCSR& out, std::string& why);
 
 bool vcache_eligible(const HostCSR& a, const VcGeom& g);
+// The block / panel / part geometry build_vcache will use, without the entries
+// (rows_per_block, nblocks, npanels, part_panels, npad).
+void vcache_geometry(uint32_t rows, uint32_t cols, const VcGeom& g, VcacheLayout& out);
 uint32_t vcache_max_run(const HostCSR& a, uint32_t panel);
 void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out);
 void build_sell(const HostCSR& a, SellLayout& out);

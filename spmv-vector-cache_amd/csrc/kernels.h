@@ -23,6 +23,7 @@ struct VcacheArgs {
   int xlane = 0;      // cross-lane run continuation (experimental, option "vcache_xlane")
   uint32_t max_seg = 0;  // longest segment of the layout (xlane needs it in the register window)
   int map = 0;           // split 4: XCD-aware unit placement (experimental, option "vcache_map")
+  uint32_t chunk = 0;    // k_wgather: row blocks per launch (0: one launch)
 };
 
 struct CsrArgs {

@@ -90,14 +90,23 @@ static uint32_t vcache_rows_per_block(uint32_t rows, const VcGeom& g) {
   return std::min<uint32_t>(r, (uint32_t)g.rows);
 }
 
+void vcache_geometry(uint32_t rows, uint32_t cols, const VcGeom& g, VcacheLayout& out) {
+  const uint32_t P = (uint32_t)g.panel, S = (uint32_t)g.split;
+  out.geom = g;
+  out.rows_per_block = vcache_rows_per_block(rows, g);
+  out.nblocks = (rows + out.rows_per_block - 1) / out.rows_per_block;
+  out.npanels = (cols + P - 1) / P;
+  out.part_panels = (out.npanels + S - 1) / S;  // the largest part (vc_part_first cuts)
+  out.npad = out.part_panels;                   // the kernel clamps prefetches past its last panel
+}
+
 bool vcache_eligible(const HostCSR& a, const VcGeom& g) {
   if (a.cols < 2 || a.rows == 0 || a.nnz == 0) return false;
   // the entry code must hold col_local and row_local
   if ((uint64_t)g.panel > (1ull << g.colbits) || (uint64_t)g.rows > (1ull << (30 - g.colbits))) return false;
   const uint32_t np = (a.cols + g.panel - 1) / g.panel;
-  if (np < (uint32_t)g.split) return false;  // every column part needs >= 1 panel
+  if (np < (uint32_t)g.split) return false;  // every column part owns >= 1 panel (vc_part_first)
   const uint32_t part = (np + g.split - 1) / g.split;
-  if ((uint64_t)(g.split - 1) * part >= np) return false;  // every part must own >= 1 panel
   const uint32_t npad = part;  // the kernel clamps prefetches past its last panel
   if (npad + 1 > (uint32_t)kVcSegMax) return false;
   // panel order must equal each row's summation order: columns non-decreasing
@@ -129,21 +138,12 @@ uint32_t vcache_max_run(const HostCSR& a, uint32_t panel) {
 // ordered by (row, column); each row's entries keep their CSR order, so a
 // thread that walks a row run in a segment, and the panels in ascending
 // order, adds the row's products in ascending column order.  A work unit
-// (b, h) covers panels [h*part, (h+1)*part); its seg row lists npad+1 offsets
-// (empty segments past its last panel).
+// (b, h) covers panels [vc_part_first(h), vc_part_first(h+1)); its seg row
+// lists npad+1 offsets (empty segments past its last panel).
 void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
   const uint32_t P = (uint32_t)g.panel, S = (uint32_t)g.split;
-  const uint32_t R = vcache_rows_per_block(a.rows, g);
-  const uint32_t nb = (a.rows + R - 1) / R;
-  const uint32_t np = (a.cols + P - 1) / P;
-  const uint32_t part = (np + S - 1) / S;
-  const uint32_t npad = part;  // the kernel clamps prefetches past its last panel
-  out.geom = g;
-  out.rows_per_block = R;
-  out.nblocks = nb;
-  out.npanels = np;
-  out.part_panels = part;
-  out.npad = npad;
+  vcache_geometry(a.rows, a.cols, g, out);
+  const uint32_t R = out.rows_per_block, nb = out.nblocks, np = out.npanels, npad = out.npad;
   out.seg.assign((size_t)nb * S * (npad + 1), 0);
   out.code.resize(a.nnz);
   out.vals.resize(a.nnz);
@@ -161,8 +161,8 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
     }
     for (uint32_t h = 0; h < S; ++h) {
       uint32_t* seg = &out.seg[((size_t)b * S + h) * (npad + 1)];
-      const uint32_t plast = std::min((h + 1) * part, np);
-      for (uint32_t i = 0; i <= npad; ++i) seg[i] = base + cnt[std::min(h * part + i, plast)];
+      const uint32_t pfirst = vc_part_first(h, np, S), plast = vc_part_first(h + 1, np, S);
+      for (uint32_t i = 0; i <= npad; ++i) seg[i] = base + cnt[std::min(pfirst + i, plast)];
     }
     std::vector<uint32_t> cur(cnt.begin(), cnt.end() - 1);
     for (uint32_t r = r0; r < r1; ++r) {

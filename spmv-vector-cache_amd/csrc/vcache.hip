@@ -77,7 +77,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   static_assert(VR * 8 + 2 * VP * 8 + kVcSegMax * 4 <= 163840, "LDS budget");
   static_assert(WL > 0 && WC > 0, "both roles need waves");
   static_assert(SPLIT == 1 || SPLIT == 3 || SPLIT == 4, "column parts");
-  __shared__ T ylds[VR];
+  __shared__ alignas(16) T ylds[VR];  // 16-B aligned: the combine moves row pairs
   __shared__ T xb[2][VP];
   __shared__ uint32_t segl[kVcSegMax];
 
@@ -95,8 +95,8 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   const uint32_t r0 = b * rows_per_block;
   if (r0 >= rows) return;  // never with a vcache_grid_ok geometry (workgroup-uniform, before any barrier)
   const uint32_t nr = min(rows_per_block, rows - r0);
-  const uint32_t p0 = h * part_panels;                  // first global panel of this unit
-  const uint32_t npu = min(part_panels, npanels - p0);  // >= 1 (vcache_eligible)
+  const uint32_t p0 = vc_part_first(h, npanels, SPLIT);             // first global panel of this unit
+  const uint32_t npu = vc_part_first(h + 1, npanels, SPLIT) - p0;   // >= 1 (vcache_grid_ok)
   const uint32_t* sp = seg + ((size_t)b * SPLIT + h) * (npad + 1);
   if ((uint32_t)t <= npad) segl[t] = sp[t];
   for (uint32_t i = t; i < nr; i += VT) ylds[i] = (beta && h == 0) ? y_in[r0 + i] : T(0);
@@ -376,47 +376,77 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
     return;
   }
-  // ---- combine the column parts, fixed order p0 + p1 + p2 (+ p3).  Hand-off
-  // per MI355X_MICROARCH.md (Valid forms, table row 1): every partial byte
-  // stored write-through (sc1: agent-scope relaxed atomic store), each storing
-  // wave drains vmcnt, one lane adds to the block's counter after the barrier;
-  // the workgroup whose add returned SPLIT-1 reads the other partials with sc1
-  // loads and adds all parts in part order, its own from LDS.
-  uint64_t* mine = reinterpret_cast<uint64_t*>(partial) + (size_t)h * rows;
-  for (uint32_t i = t; i < nr; i += VT)
-    __hip_atomic_store(mine + r0 + i, __builtin_bit_cast(uint64_t, ylds[i]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // ---- combine the column parts, fixed order p0 + p1 + p2 (+ p3), ticket
+  // first: one lane adds to the block's arrival counter tickets[b]; the
+  // workgroups that arrive before the last publish their partial and count it
+  // in tickets[nblocks + b]; the last one does not publish (its partial stays
+  // in LDS), waits for the others' count, reads their partials and writes y.
+  // Hand-off per MI355X_MICROARCH.md (Valid forms, table row 1): every
+  // partial byte stored write-through (sc1: agent-scope relaxed atomic
+  // store), every storing wave drains vmcnt, then after the barrier one lane
+  // makes the agent-scope add; the consumer polls the count with sc1 loads
+  // from one lane and its waves load (sc1) after the barrier that lane joins.
+  // No wait can deadlock: the publishers took their tickets before the last
+  // arriver did, so they are running and publish unconditionally.
+  // Partials: part q of block b at partial + (q * nblocks + b) * VRP, VRP even,
+  // so each lane moves row pairs with 16-byte write-through (sc1) buffer
+  // accesses, NP of them in flight per lane.
+  constexpr uint32_t VRP = (VR + 1) & ~1u;
+  constexpr int NP = (VRP / 2 + VT - 1) / VT;  // row pairs per lane
+  uint32_t* const published = tickets + nblocks;
+  if (t == 0) segl[0] = __hip_atomic_fetch_add(tickets + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  const u64x2* const yl2 = reinterpret_cast<const u64x2*>(ylds);  // ylds: VR (even) doubles, 16-B aligned
+  const uint32_t npairs = (nr + 1) / 2;
+  if (segl[0] != (uint32_t)SPLIT - 1) {
+    const __amdgpu_buffer_rsrc_t mine = buf_rsrc(partial + ((size_t)h * nblocks + b) * VRP, 8 * VRP);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const uint32_t p = t + j * VT;
+      if (p < npairs) st_128_sc1(mine, 16 * p, yl2[p]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) __hip_atomic_fetch_add(published + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   if (t == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(tickets + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == (uint32_t)SPLIT - 1)
-      __hip_atomic_store(tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-    segl[0] = old;
+    // bounded spin (~0.3 s of sc1 polls): the protocol cannot deadlock, and a bound keeps a
+    // broken invariant from hanging the GPU (the parity tests would see it)
+    for (uint32_t spin = 0; spin < (1u << 18); ++spin) {
+      if (__hip_atomic_load(published + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)SPLIT - 1) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    // both counters back to zero for the next launch (every add of this one is in)
+    __hip_atomic_store(published + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (SPLIT == 2 && segl[0] == 1) {  // (the round-1 validated form of the two-part case)
-    const uint64_t* other = reinterpret_cast<const uint64_t*>(partial) + (size_t)(1 - h) * rows;
-    for (uint32_t i = t; i < nr; i += VT) {
-      const T o = __builtin_bit_cast(
-          T, __hip_atomic_load(other + r0 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      const T m = ylds[i];
-      y_out[r0 + i] = h == 0 ? m + o : o + m;
-    }
-  } else if (SPLIT > 2 && segl[0] == (uint32_t)SPLIT - 1) {
-    const uint64_t* parts = reinterpret_cast<const uint64_t*>(partial);
-    for (uint32_t i = t; i < nr; i += VT) {
-      T acc = T(0);
+  // y = p0 + p1 + p2 (+ p3) in part order; part h from LDS, the others loaded
+  T acc[NP][2];
 #pragma unroll
-      for (int q = 0; q < SPLIT; ++q) {
-        const T v = (uint32_t)q == h ? ylds[i]
-                                     : __builtin_bit_cast(T, __hip_atomic_load(parts + (size_t)q * rows + r0 + i,
-                                                                                __ATOMIC_RELAXED,
-                                                                                __HIP_MEMORY_SCOPE_AGENT));
-        acc = q == 0 ? v : acc + v;
-      }
-      y_out[r0 + i] = acc;
+  for (int q = 0; q < SPLIT; ++q) {
+    u64x2 v[NP];
+    if ((uint32_t)q == h) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) v[j] = yl2[min((uint32_t)(t + j * VT), VRP / 2 - 1)];
+    } else {
+      const __amdgpu_buffer_rsrc_t src = buf_rsrc(partial + ((size_t)q * nblocks + b) * VRP, 8 * VRP);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) v[j] = ld_128_sc1(src, 16 * min((uint32_t)(t + j * VT), VRP / 2 - 1));
     }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {  // components by name (.x/.y): an indexed subscript lost .y
+      const T w0 = __builtin_bit_cast(T, (uint64_t)v[j].x), w1 = __builtin_bit_cast(T, (uint64_t)v[j].y);
+      acc[j][0] = q == 0 ? w0 : acc[j][0] + w0;
+      acc[j][1] = q == 0 ? w1 : acc[j][1] + w1;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const uint32_t p = t + j * VT;
+    if (2 * p < nr) y_out[r0 + 2 * p] = acc[j][0];
+    if (2 * p + 1 < nr) y_out[r0 + 2 * p + 1] = acc[j][1];
   }
 }
 

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
                                                          const T* __restrict__ evals, const T* __restrict__ x,
                                                          const T* __restrict__ y_in, T* __restrict__ y_out,
                                                          uint32_t rows, uint32_t rows_per_block, uint32_t npanels,
-                                                         uint32_t npad, uint32_t last, int beta) {
+                                                         uint32_t npad, uint32_t last, int beta, uint32_t b0) {
 #pragma clang fp contract(off)
   constexpr int VT = kVcThreads;
   constexpr uint32_t W = 1u << CB, CMASK = W - 1, RMASK = (1u << (30 - CB)) - 1;
@@ -36,7 +36,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
   __shared__ T ylds[VR];
   __shared__ uint32_t segl[kVcSegMax];
   const int t = threadIdx.x;
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = b0 + blockIdx.x;  // this launch's blocks start at b0 (launch chunks, kWgChunk)
   const uint32_t r0 = b * rows_per_block;
   if (r0 >= rows) return;  // never with a vcache_grid_ok geometry
   const uint32_t nr = min(rows_per_block, rows - r0);
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather_pipe(const uint32_t* __r
                                                               const T* __restrict__ y_in, T* __restrict__ y_out,
                                                               uint32_t rows, uint32_t rows_per_block,
                                                               uint32_t npanels, uint32_t npad, uint32_t last,
-                                                              int beta) {
+                                                              int beta, uint32_t b0) {
 #pragma clang fp contract(off)
   constexpr int VT = kVcThreads;
   constexpr uint32_t W = 1u << CB, CMASK = W - 1, RMASK = (1u << (30 - CB)) - 1;
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather_pipe(const uint32_t* __r
   __shared__ uint32_t segl[kVcSegMax];
   const int t = threadIdx.x;
   const uint32_t lw = t & 63;
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = b0 + blockIdx.x;
   const uint32_t r0 = b * rows_per_block;
   if (r0 >= rows) return;  // never with a vcache_grid_ok geometry
   const uint32_t nr = min(rows_per_block, rows - r0);
@@ -238,19 +238,27 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather_pipe(const uint32_t* __r
 
 template <typename T>
 static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
-  if (a.xlane >= 2 && a.max_seg <= 2u * kVcThreads)
-    hipLaunchKernelGGL((k_wgather_pipe<T, 17, 4, 2>), dim3(a.nblocks), dim3(kVcThreads), 0, s, a.seg, a.code,
-                       (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
-                       a.npanels, a.npad, a.last, a.beta);
-  else if (a.xlane >= 2 && a.max_seg <= 4u * kVcThreads)
-    hipLaunchKernelGGL((k_wgather_pipe<T, 17, 4, 4>), dim3(a.nblocks), dim3(kVcThreads), 0, s, a.seg, a.code,
-                       (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
-                       a.npanels, a.npad, a.last, a.beta);
-  else
-    hipLaunchKernelGGL((k_wgather<T, 17, 4, 2>), dim3(a.nblocks), dim3(kVcThreads), 0, s, a.seg, a.code,
-                       (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
-                       a.npanels, a.npad, a.last, a.beta);
-  return hipGetLastError();
+  // blocks [b0, b0 + n) per launch: a chunk the chip holds at once walks the x
+  // windows together (kWgChunk); the launches run in stream order
+  const uint32_t chunk = a.chunk ? a.chunk : a.nblocks;
+  for (uint32_t b0 = 0; b0 < a.nblocks; b0 += chunk) {
+    const uint32_t n = a.nblocks - b0 < chunk ? a.nblocks - b0 : chunk;
+    if (a.xlane >= 2 && a.max_seg <= 2u * kVcThreads)
+      hipLaunchKernelGGL((k_wgather_pipe<T, 17, 4, 2>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
+                         (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
+                         a.npanels, a.npad, a.last, a.beta, b0);
+    else if (a.xlane >= 2 && a.max_seg <= 4u * kVcThreads)
+      hipLaunchKernelGGL((k_wgather_pipe<T, 17, 4, 4>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
+                         (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
+                         a.npanels, a.npad, a.last, a.beta, b0);
+    else
+      hipLaunchKernelGGL((k_wgather<T, 17, 4, 2>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
+                         (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
+                         a.npanels, a.npad, a.last, a.beta, b0);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_wgather(int dtype, const VcacheArgs& a, hipStream_t s) {

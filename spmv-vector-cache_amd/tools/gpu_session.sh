@@ -41,6 +41,7 @@ for s in $STEPS; do
     sweeprmat) step sweep_rmat 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --rmat 20 ;;
     sweepwidex) HIPSPMV_EXPERIMENTAL=1 step sweep_wide_exp 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 21 --log2-cols 24 --rounds 2 ;;
     sweepwide) step sweep_wide 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 21 --log2-cols 24 ;;
+    sweepc4) step sweep_c4 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 24 --log2-cols 24 --only wgather --rounds 2 --reps 10 ;;
     c4) step bench_c4 900 python bench.py --workload c4 --steps 20 --warmup 5 ;;
     c5) step bench_c5 900 python bench.py --workload c5 --steps 20 --warmup 5 ;;
     c4shard) step bench_c4_shard 900 python bench.py --workload c4 --shard 0/8 --steps 50 --warmup 5 ;;

@@ -37,7 +37,9 @@ O, F = hs.MODE_ORDERED, hs.MODE_FAST
 # (label, kernel, mode, options); the experimental ones need HIPSPMV_EXPERIMENTAL=1 at create
 cands = [("vcache", "vcache", O, {}), ("csr_lane", "csr_lane", O, {}), ("vcache_split", "vcache_split", F, {}),
          ("csr_vector", "csr_vector", F, {}), ("sell", "sell", O, {}), ("sell fast", "sell", F, {}),
-         ("wgather", "wgather", O, {})]
+         ("wgather", "wgather", O, {}), ("wgather c128", "wgather", O, {"wgather_chunk": 128}),
+         ("wgather c512", "wgather", O, {"wgather_chunk": 512}), ("wgather c0", "wgather", O, {"wgather_chunk": 0}),
+         ("wgather xl2", "wgather", O, {"vcache_xlane": 2})]
 if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
     cands += [("vcache xl1", "vcache", O, {"vcache_xlane": 1}), ("vcache xl2", "vcache", O, {"vcache_xlane": 2}),
               ("vcache dma", "vcache", O, {"vcache_dma": 1}),
@@ -48,7 +50,6 @@ if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
               ("vcache xl3", "vcache", O, {"vcache_xlane": 3}), ("split xl3", "vcache_split", F, {"vcache_xlane": 3}),
               ("split4", "vcache_split4", F, {}), ("split4 xl2", "vcache_split4", F, {"vcache_xlane": 2}),
               ("split4 dma xl2", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 2}),
-              ("wgather xl2", "wgather", O, {"vcache_xlane": 2}),
               ("split4 xl3", "vcache_split4", F, {"vcache_xlane": 3}),
               ("split4 dma xl3", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 3}),
               ("split4 map", "vcache_split4", F, {"vcache_map": 1}),
@@ -63,8 +64,8 @@ for rnd in range(a.rounds):  # interleaved rounds in one process (methodology ru
     for label, kname, mode, opts in cands:
         try:
             h.set_kernel(kname)
-            for k in ("vcache_dma", "vcache_xlane", "vcache_map"):
-                h.set_option(k, opts.get(k, -1 if k in ("vcache_xlane", "vcache_dma") else 0))
+            for k in ("vcache_dma", "vcache_xlane", "vcache_map", "wgather_chunk"):
+                h.set_option(k, opts.get(k, {"vcache_xlane": -1, "vcache_dma": -1, "wgather_chunk": 256}.get(k, 0)))
             h.exec_device(x, y, beta=0, mode=mode, stream=s)
         except hs.HipSpMVError:
             continue

@@ -1,0 +1,241 @@
+// pf_probe: can scalar-path prefetch waves take the entry stream's HBM latency
+// off the vector L1's request slots?
+//
+// The skeleton of k_vcache's split geometry without its arithmetic: 255
+// workgroups of 1024 threads (one per CU), `steps` barrier-stepped panels.
+//   X: waves 0-2 stage a 32,000-byte x panel per step into LDS by LDS-DMA
+//      (the column part's 2.8 MB, L2-served, like the product kernel);
+//   E: the compute waves load `chunk` entries per step (u32 code + f64 value,
+//      as the vcache layout stores them) through a DE-deep register ring;
+//   P: NPF of the compute waves instead walk the entry lines DP steps ahead
+//      with s_load_dword (one per 128-byte line; the data is discarded), so the
+//      vector loads that follow find the lines in L2.
+// The prefetch role runs as one inline-asm loop: its destination SGPRs are
+// clobbered for the whole loop, and it never waits on lgkmcnt until the end.
+// Prints the time of every variant (HIP events over back-to-back launches).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                               \
+  do {                                                                      \
+    hipError_t e_ = (x);                                                    \
+    if (e_ != hipSuccess) {                                                 \
+      std::printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); \
+      std::exit(1);                                                         \
+    }                                                                       \
+  } while (0)
+
+constexpr int kT = 1024, kNW = 16, kWL = 3, kDE = 4;
+constexpr int kPanel = 4000;             // x columns per step (32,000 B)
+constexpr int kPairs = kPanel / 2;       // 16-byte chunks per panel
+constexpr int kChunk = 1536;             // entries per step: 48 code lines + 96 value lines
+constexpr int kYRows = 12000;            // LDS filler so one workgroup fits a CU (as the y block does)
+
+template <bool X, bool E, int NPF, int EPT>
+__global__ __launch_bounds__(kT) void k_probe(const uint32_t* __restrict__ code, const double* __restrict__ vals,
+                                              const double* __restrict__ x, double* __restrict__ out,
+                                              uint32_t steps, uint32_t part_cols, int dp) {
+  __shared__ double xb[2][kPanel];
+  __shared__ double ylds[kYRows];
+  constexpr int WC = kNW - kWL - NPF, CT = WC * 64;
+  static_assert(!E || EPT * CT >= kChunk, "register window covers a step");
+  static_assert(48 % (NPF ? NPF : 1) == 0, "lines split evenly over the prefetch waves");
+  const int t = threadIdx.x;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+  const uint32_t u = blockIdx.x, h = u % 3;  // column part of this unit
+  const size_t ebase = (size_t)u * steps * kChunk;
+  const uint32_t* cu = code + ebase;
+  const double* vu = vals + ebase;
+  const double* xp = x + (size_t)h * part_cols;
+  const uint32_t npanels = part_cols / kPanel;
+  for (int i = t; i < kYRows; i += kT) ylds[i] = 0.0;
+  __syncthreads();
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  if (w < kWL) {  // ---- x loaders (LDS-DMA, one panel ahead)
+    auto dma = [&](uint32_t s) {
+      if (!X) return;
+      const double* src = xp + (size_t)(s % npanels) * kPanel;
+      double* slot = xb[s & 1];
+#pragma unroll
+      for (int j = 0; j < (kPairs + kWL * 64 - 1) / (kWL * 64); ++j) {
+        const uint32_t c0 = (j * kWL + w) * 64;
+        if (c0 + lane < kPairs)
+          __builtin_amdgcn_global_load_lds((const void*)(src + 2 * (c0 + lane)),
+                                           (__attribute__((address_space(3))) void*)(slot + 2 * c0), 16, 0, 0);
+      }
+    };
+    dma(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    for (uint32_t s = 0; s < steps; ++s) {
+      if (s + 1 < steps) dma(s + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier();
+    }
+  } else if (w < (uint32_t)(kWL + NPF)) {  // ---- scalar prefetch of the entry lines, dp steps ahead
+    const uint32_t k = w - kWL;
+    // this wave's lines: k, k + NPF, ... of each step's 48 code lines and 96 value lines
+    const char* cp = (const char*)cu + (size_t)dp * kChunk * 4 + 128 * k;
+    const char* vp = (const char*)vu + (size_t)dp * kChunk * 8 + 128 * k;
+    uint32_t clo = (uint32_t)(uintptr_t)cp, chi = (uint32_t)((uintptr_t)cp >> 32);
+    uint32_t vlo = (uint32_t)(uintptr_t)vp, vhi = (uint32_t)((uintptr_t)vp >> 32);
+    // steps whose prefetch target lies inside the unit's range; the rest only barrier
+    const uint32_t npf = __builtin_amdgcn_readfirstlane(steps > (uint32_t)dp ? steps - dp : 0u),
+                   nrest = __builtin_amdgcn_readfirstlane(steps - npf);  // + the initial barrier: steps + 1 in all
+    constexpr uint32_t NP1 = NPF ? NPF : 1, ncl = 48 / NP1, nvl = 96 / NP1;
+    // s[84:87]: code / value line pointers of the next prefetch step; s88, s89:
+    // step counters; s[92:93] walking pointer, s94 line counter, s95 the
+    // discarded load destination.  Inputs are copied in; nothing is written
+    // back (the compiler treats asm outputs as divergent).
+    asm volatile(
+        "s_mov_b32 s84, %0\n"
+        "s_mov_b32 s85, %1\n"
+        "s_mov_b32 s86, %2\n"
+        "s_mov_b32 s87, %3\n"
+        "s_mov_b32 s88, %4\n"
+        "s_mov_b32 s89, %5\n"
+        "s_barrier\n"
+        "s_cmp_eq_u32 s88, 0\n"
+        "s_cbranch_scc1 4f\n"
+        "1:\n"
+        "s_mov_b32 s92, s84\n"
+        "s_mov_b32 s93, s85\n"
+        "s_mov_b32 s94, %6\n"
+        "2:\n"
+        "s_load_dword s95, s[92:93], 0x0\n"
+        "s_add_u32 s92, s92, %8\n"
+        "s_addc_u32 s93, s93, 0\n"
+        "s_sub_u32 s94, s94, 1\n"
+        "s_cmp_lg_u32 s94, 0\n"
+        "s_cbranch_scc1 2b\n"
+        "s_mov_b32 s92, s86\n"
+        "s_mov_b32 s93, s87\n"
+        "s_mov_b32 s94, %7\n"
+        "3:\n"
+        "s_load_dword s95, s[92:93], 0x0\n"
+        "s_add_u32 s92, s92, %8\n"
+        "s_addc_u32 s93, s93, 0\n"
+        "s_sub_u32 s94, s94, 1\n"
+        "s_cmp_lg_u32 s94, 0\n"
+        "s_cbranch_scc1 3b\n"
+        "s_barrier\n"
+        "s_add_u32 s84, s84, %9\n"
+        "s_addc_u32 s85, s85, 0\n"
+        "s_add_u32 s86, s86, %10\n"
+        "s_addc_u32 s87, s87, 0\n"
+        "s_sub_u32 s88, s88, 1\n"
+        "s_cmp_lg_u32 s88, 0\n"
+        "s_cbranch_scc1 1b\n"
+        "4:\n"
+        "s_cmp_eq_u32 s89, 0\n"
+        "s_cbranch_scc1 6f\n"
+        "5:\n"
+        "s_barrier\n"
+        "s_sub_u32 s89, s89, 1\n"
+        "s_cmp_lg_u32 s89, 0\n"
+        "s_cbranch_scc1 5b\n"
+        "6:\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        :
+        : "s"(clo), "s"(chi), "s"(vlo), "s"(vhi), "s"(npf), "s"(nrest), "s"(ncl), "s"(nvl), "s"(128 * NPF),
+          "s"(kChunk * 4), "s"(kChunk * 8)
+        : "s84", "s85", "s86", "s87", "s88", "s89", "s92", "s93", "s94", "s95", "scc", "memory");
+  } else {  // ---- compute waves: the entry ring
+    const int ct = t - (kWL + NPF) * 64;
+    const uint32_t last = steps * kChunk - 1;
+    uint32_t C[kDE][EPT];
+    double V[kDE][EPT];
+    auto load = [&](uint32_t s, uint32_t* c, double* v) {
+      if (!E) return;
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        const uint32_t i = min(s * kChunk + min((uint32_t)(ct + j * CT), (uint32_t)kChunk - 1), last);
+        c[j] = cu[i];
+        v[j] = vu[i];
+      }
+    };
+    double acc = 0.0;
+#pragma unroll
+    for (int d = 0; d < kDE; ++d) load(d, C[d], V[d]);
+    barrier();
+    const uint32_t nsteps = (steps + kDE - 1) / kDE * kDE;
+    for (uint32_t b0 = 0; b0 < nsteps; b0 += kDE) {
+#pragma unroll
+      for (int i = 0; i < kDE; ++i) {
+        if (E)
+#pragma unroll
+          for (int j = 0; j < EPT; ++j) acc += (double)C[i][j] * V[i][j] + xb[(b0 + i) & 1][C[i][j] & 2047];
+        load(b0 + i + kDE, C[i], V[i]);
+        if (b0 + i < steps) barrier();
+      }
+    }
+    ylds[ct % kYRows] = acc;
+  }
+  __syncthreads();
+  if (t == 0) out[u] = ylds[0] + ylds[kYRows - 1];
+}
+
+template <bool X, bool E, int NPF, int EPT>
+static float run(const char* name, const uint32_t* code, const double* vals, const double* x, double* out,
+                 uint32_t units, uint32_t steps, uint32_t part_cols, int dp) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto launch = [&] {
+    hipLaunchKernelGGL((k_probe<X, E, NPF, EPT>), dim3(units), dim3(kT), 0, 0, code, vals, x, out, steps,
+                       part_cols, dp);
+  };
+  for (int i = 0; i < 3; ++i) launch();
+  CK(hipGetLastError());
+  const int reps = 30;
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < reps; ++i) launch();
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / reps;
+  const double ebytes = E ? 12.0 * units * steps * kChunk : 0.0;
+  const double xbytes = X ? 8.0 * units * steps * kPanel : 0.0;
+  std::printf("%-34s dp=%2d: %8.2f us  entries %6.0f GB/s  x %6.0f GB/s\n", name, dp, us, ebytes / us / 1e3,
+              xbytes / us / 1e3);
+  std::fflush(stdout);
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return (float)us;
+}
+
+int main() {
+  const uint32_t units = 255, steps = 88, part_cols = 349526 / kPanel * kPanel;  // 87 panels; panel s % 87
+  const size_t n = (size_t)units * steps * kChunk;                           // 34.5 M entries (C3: 33.5 M)
+  uint32_t* code;
+  double *vals, *x, *out;
+  CK(hipMalloc(&code, 4 * n));
+  CK(hipMalloc(&vals, 8 * n));
+  CK(hipMalloc(&x, 8ull * 3 * part_cols));
+  CK(hipMalloc(&out, 8ull * units));
+  CK(hipMemset(code, 1, 4 * n));
+  CK(hipMemset(vals, 0, 8 * n));
+  CK(hipMemset(x, 0, 8ull * 3 * part_cols));
+  for (int rnd = 0; rnd < 2; ++rnd) {
+    std::printf("-- round %d\n", rnd);
+    run<false, true, 0, 2>("E only", code, vals, x, out, units, steps, part_cols, 0);
+    run<true, false, 0, 2>("X only", code, vals, x, out, units, steps, part_cols, 0);
+    run<true, true, 0, 2>("E + X (product skeleton)", code, vals, x, out, units, steps, part_cols, 0);
+    for (int dp : {5, 6, 8, 12}) {
+      run<false, true, 2, 3>("E + P2", code, vals, x, out, units, steps, part_cols, dp);
+      run<true, true, 2, 3>("E + X + P2", code, vals, x, out, units, steps, part_cols, dp);
+      run<true, true, 4, 3>("E + X + P4", code, vals, x, out, units, steps, part_cols, dp);
+    }
+    run<false, false, 4, 3>("P4 only (scalar read rate)", code, vals, x, out, units, steps, part_cols, 0);
+    run<false, false, 12, 3>("P12 only (scalar read rate)", code, vals, x, out, units, steps, part_cols, 0);
+  }
+  return 0;
+}

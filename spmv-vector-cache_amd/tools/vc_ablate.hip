@@ -48,7 +48,7 @@ int main(int argc, char** argv) {
   double* dx = up(x);
   double *dy, *dpart;
   CK(hipMalloc(&dy, 8ull * n));
-  CK(hipMalloc(&dpart, 8ull * 4 * n));  // [split][rows] partials, split <= 4
+  CK(hipMalloc(&dpart, 8ull * 4 * (n + 256 * 16384)));  // [split][nblocks][VRP] partials, split <= 4
   const double alg = 12.0 * a.nnz + 4.0 * (n + 1) + 16.0 * n;
   auto timeit = [&](auto launch) {
     hipEvent_t e0, e1;
@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
   for (VcGeom g : {kVcOrdered, kVcSplit, kVcSplit4}) {
     VcacheLayout L;
     build_vcache(a, g, L);
-    VcacheArgs A{up(L.seg), up(L.code), up(L.vals), dx, dy, dy, dpart, up(std::vector<uint32_t>(L.nblocks, 0)),
+    VcacheArgs A{up(L.seg), up(L.code), up(L.vals), dx, dy, dy, dpart, up(std::vector<uint32_t>(2 * L.nblocks, 0)),
                  a.rows, a.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels, L.npad, a.nnz - 1,
                  g.split, 0};
     std::printf("geometry rows=%d panel=%d split=%d: units=%u npad=%u max_seg=%u\n", g.rows, g.panel, g.split,
@@ -81,8 +81,8 @@ int main(int argc, char** argv) {
     // kernel launched on the split layout's grid): SPLIT is checked here
     // window: entries a CX variant holds in registers per step (0: no limit)
     auto variant = [&](auto kern, int kernel_split, const char* nm, int mask, uint32_t window = 0) {
-      if (kernel_split != g.split || L.rows_per_block > (uint32_t)g.rows ||
-          (uint64_t)L.part_panels * (g.split - 1) >= L.npanels) {
+      if (kernel_split != g.split || !vcache_grid_ok(a.rows, a.cols, L.rows_per_block, L.nblocks, L.npanels,
+                                                     L.part_panels, L.npad, (uint32_t)g.panel, g.split, g)) {
         std::printf("  %-30s SKIPPED: kernel split %d vs layout split %d\n", nm, kernel_split, g.split);
         return;
       }
@@ -124,8 +124,11 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 1, 8, 4, 3, 12>, 1, "no entries/compute", 12);
       variant(k_vcache<double, 1, 8, 4, 3, 15>, 1, "skeleton", 15);
     } else if (g.split == 3) {  // the product FAST geometry (round 2)
-      variant(k_vcache<double, 3, 2, 4, 2, 0, 0, false, 1, 3>, 3, "product (DMA WL2 DE4 EPT2, xlane3)", 0,
-              14 * 64 * 2);
+      variant(k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 3>, 3, "product (DMA WL3 DE4 EPT2, xlane3)", 0,
+              13 * 64 * 2);
+      variant(k_vcache<double, 3, 3, 4, 2, 64, 0, false, 1, 3>, 3, "product without the combine", 64,
+              13 * 64 * 2);
+      variant(k_vcache<double, 3, 2, 4, 2, 0, 0, false, 1, 3>, 3, "DMA WL2 DE4 EPT2, xlane3", 0, 14 * 64 * 2);
       variant(k_vcache<double, 3, 2, 4, 2, 0, 0, false, 1, 0>, 3, "DMA WL2, runs re-read", 0);
       variant(k_vcache<double, 3, 4, 4, 3, 0, 0, false, 1, 3>, 3, "DMA WL4 EPT3 xlane3", 0, 12 * 64 * 3);
       variant(k_vcache<double, 3, 6, 4, 3, 0, 0, false, 0, 3>, 3, "registers WL6 EPT3 xlane3", 0, 10 * 64 * 3);
@@ -135,8 +138,6 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 3, 2, 4, 2, 47, 0, false, 1, 3>, 3, "skeleton without step barriers", 47,
               14 * 64 * 2);
       variant(k_vcache<double, 3, 2, 4, 2, 111, 0, false, 1, 3>, 3, "... and without the combine", 111,
-              14 * 64 * 2);
-      variant(k_vcache<double, 3, 2, 4, 2, 64, 0, false, 1, 3>, 3, "product without the combine", 64,
               14 * 64 * 2);
     } else {
       variant(k_vcache<double, 4>, 4, "default (WL2 DE4 EPT2)", 0);

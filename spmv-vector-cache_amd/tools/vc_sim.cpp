@@ -69,8 +69,10 @@ static double madd(double acc, double a, double b) {
 }
 
 // Replays k_vcache for every unit; returns y.
+// arrival_rev: the column parts of every block arrive in reverse unit order
+// (the combine's result must not depend on the order)
 static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, const Cfg& c, const std::vector<double>& x,
-                                    const std::vector<double>& yin, int beta) {
+                                    const std::vector<double>& yin, int beta, bool arrival_rev = false) {
   const bool gather = c.LD == 2;  // k_wgather: every wave computes, no loader role
   const int VT = 1024, NW = VT / 64, WC = gather ? NW : NW - c.WL, LT = c.WL * 64, CT = WC * 64;
   const uint32_t CMASK = (1u << c.CB) - 1, RMASK = (1u << (30 - c.CB)) - 1;
@@ -82,7 +84,9 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
   Buf<double> vals{"evals", {}}, X{"x", x}, Yin{"y_in", yin}, Y{"y_out", std::vector<double>(rows, NAN)};
   vals.v.resize(L.vals.size());
   std::memcpy(vals.v.data(), L.vals.data(), 8 * L.vals.size());
-  Buf<double> partial{"partial", std::vector<double>((size_t)rows * c.SPLIT, NAN)};
+  // k_vcache's partial layout: part q of block b at (q * nblocks + b) * VRP, VRP = VR rounded up to even
+  const uint32_t VRP = (uint32_t)(c.VR + 1) & ~1u;
+  Buf<double> partial{"partial", std::vector<double>((size_t)VRP * nblocks * c.SPLIT, NAN)};
   std::vector<uint32_t> tickets(nblocks, 0);
   const uint32_t units = nblocks * c.SPLIT;
   std::vector<std::vector<double>> ylds_of(units);
@@ -102,10 +106,10 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
     CHECK(r0 < rows, "unit %u r0 %u >= rows", bid, r0);
     const uint32_t nr = std::min(rpb, rows - r0);
     CHECK(nr <= (uint32_t)c.VR, "nr %u > VR", nr);
-    const uint32_t p0 = h * part;
+    const uint32_t p0 = vc_part_first(h, npanels, c.SPLIT);
     CHECK(p0 < npanels, "p0 %u >= npanels %u", p0, npanels);
-    const uint32_t npu = std::min(part, npanels - p0);
-    CHECK(npu >= 1 && npad + 1 <= (uint32_t)kVcSegMax, "npu %u npad %u", npu, npad);
+    const uint32_t npu = vc_part_first(h + 1, npanels, c.SPLIT) - p0;
+    CHECK(npu >= 1 && npu <= part && npad + 1 <= (uint32_t)kVcSegMax, "npu %u part %u npad %u", npu, part, npad);
     std::vector<uint32_t> segl(kVcSegMax, 0xDEADBEEF);
     for (uint32_t t = 0; t <= npad; ++t) segl[t] = seg.get(((size_t)b * c.SPLIT + h) * (npad + 1) + t);
     std::vector<double> ylds(c.VR, NAN);
@@ -273,19 +277,28 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
     if (c.SPLIT == 1) {
       for (uint32_t i = 0; i < nr; ++i) Y.put(r0 + i, ylds[i]);
     } else {
-      for (uint32_t i = 0; i < nr; ++i) partial.put((size_t)h * rows + r0 + i, ylds[i]);
       ylds_of[bid] = ylds;
     }
   }
-  if (c.SPLIT > 1) {  // every block: the last arriver (any order) writes p0 + p1 (+ p2 + p3)
-    for (uint32_t bid = 0; bid < units; ++bid) {
+  if (c.SPLIT > 1) {
+    // ticket-first combine, arrivals in `order`: the first SPLIT-1 arrivals of a
+    // block publish their partial; the last reads the others' (unwritten ones
+    // are NaN and fail the comparison) and writes p0 + p1 (+ p2 + p3)
+    std::vector<uint32_t> order(units), published(nblocks, 0);
+    for (uint32_t i = 0; i < units; ++i) order[i] = arrival_rev ? units - 1 - i : i;
+    for (uint32_t bid : order) {
       const uint32_t b = b_of[bid], h = h_of[bid];
-      if (++tickets[b] != (uint32_t)c.SPLIT) continue;  // arrival order = unit order here
       const uint32_t r0 = b * rpb, nr = std::min(rpb, rows - r0);
+      if (tickets[b]++ != (uint32_t)c.SPLIT - 1) {
+        for (uint32_t i = 0; i < nr; ++i) partial.put(((size_t)h * nblocks + b) * VRP + i, ylds_of[bid][i]);
+        ++published[b];
+        continue;
+      }
+      CHECK(published[b] == (uint32_t)c.SPLIT - 1, "block %u combined with %u partials published", b, published[b]);
       for (uint32_t i = 0; i < nr; ++i) {
         double acc = 0;
         for (int q = 0; q < c.SPLIT; ++q) {
-          const double v = (uint32_t)q == h ? ylds_of[bid][i] : partial.get((size_t)q * rows + r0 + i);
+          const double v = (uint32_t)q == h ? ylds_of[bid][i] : partial.get(((size_t)q * nblocks + b) * VRP + i);
           acc = q == 0 ? v : acc + v;
         }
         Y.put(r0 + i, acc);
@@ -435,6 +448,9 @@ int main(int argc, char** argv) {
     cases.push_back({"stripe " + std::to_string(n) + "x" + std::to_string(cols), std::move(A)});
   }
   cases.push_back({"random 3000x20001", random_csr(3000, 20001, 0.002, 7, true)});
+  // 4 panels of 4000 for the 3-part split: parts of 1, 1 and 2 panels (a ceil
+  // cut used to leave the last part empty and the geometry ineligible)
+  cases.push_back({"random 2000x14001", random_csr(2000, 14001, 0.003, 17, true)});
   cases.push_back({"random 5000x333", random_csr(5000, 333, 0.12, 9, false)});
   cases.push_back({"random 257x12161 dense rows", random_csr(257, 12161, 0.3, 11, true)});
   cases.push_back({"random 70000x13001", random_csr(70000, 13001, 0.0008, 13, false)});
@@ -549,6 +565,10 @@ int main(int argc, char** argv) {
         const auto y = simulate(cs.A, L, c, x, yin, beta);
         const auto r = reference(cs.A, x, yin, beta);
         size_t bad = 0;
+        if (c.SPLIT > 1) {  // deterministic: the other arrival order gives the same bits
+          const auto y2 = simulate(cs.A, L, c, x, yin, beta, true);
+          bad += std::memcmp(y.data(), y2.data(), 8ull * cs.A.rows) != 0;
+        }
         for (uint32_t i = 0; i < cs.A.rows; ++i) {
           if (c.SPLIT == 1) {
             bad += std::memcmp(&y[i], &r[i], 8) != 0;

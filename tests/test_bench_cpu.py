@@ -47,6 +47,8 @@ class FakeHandle:
         y_out.copy_(torch.from_numpy(y))
 
     def stat(self, key):
+        if key == "setup_ns":
+            return 1000
         assert key == "alg_bytes"
         return 12 * self.nnz + 4 * (self.rows + 1) + 8 * self.cols + 8 * self.rows
 
@@ -110,7 +112,7 @@ def test_bench_json_contract_single(monkeypatch):
     sys.path.insert(0, REPO)
     bench = _patch(monkeypatch)
     out = _run(bench, ["--steps", "2", "--warmup", "1", "--log2-rows", "12", "--log2-cols", "12",
-                       "--cpu-seconds", "0.05"])
+                       "--cpu-seconds", "0.05", "--strong-scale", "12"])
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
                 "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert key in out, key
@@ -133,6 +135,13 @@ def test_bench_json_contract_single(monkeypatch):
     rp = out["rocprof"]
     assert rp["kernel"] == "hipspmv::k_fake" and rp["event_kernel_us"] == rf["kernel_us"]
     assert abs(rp["event_over_rocprof"] - rf["kernel_us"] / 1.0) < 1e-3
+    # per-rank parity (sampled rows of the shard, both modes) and the C4 strong block beside the headline
+    (rp0,) = out["rank_parity"]
+    assert rp0["rank"] == 0 and rp0["fast"].startswith("within FAST bound") and rp0["ordered"].startswith("bit-exact")
+    st = out["strong"]
+    assert st["scaling"] == "strong" and st["nnz_total"] == 32 << 12 and st["rows_per_rank"] == 1 << 12
+    assert st["rank_parity"][0].startswith("within FAST bound") and len(st["rank_kernel_us"]) == 1
+    assert out["gen_s"] >= 0 and out["setup_s"] >= 0 and out["setup_ns_lib"] == 1000
 
 
 FAKE_ROCPROF = """#!/usr/bin/env python3
@@ -263,7 +272,7 @@ def _rank_main(rank, world, store_path, q, extra=()):
         "gloo", init_method=f"file://{store_path}", rank=rank, world_size=world)
     try:
         out = _run(bench, ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--log2-rows", "10",
-                           "--log2-cols", "10", "--no-cpu-baseline", *extra])
+                           "--log2-cols", "10", "--strong-scale", "11", "--parity-rows", "300", *extra])
     except BaseException as e:  # report it to the parent instead of a bare exit code
         q.put((rank, f"ERROR: {type(e).__name__}: {e}"))
         raise
@@ -315,10 +324,24 @@ def test_bench_strong_workloads_gloo(workload, scale):
         assert out["config"]["nnz_total"] == hs_.gen_rmat_csr(scale)[1].size
 
 
+def _check_rank_parity_and_strong(out, world):
+    rp = out["rank_parity"]
+    assert [p["rank"] for p in rp] == list(range(world))
+    assert all(p["fast"].startswith("within FAST bound") and p["ordered"].startswith("bit-exact") for p in rp), rp
+    # the shards tile the rows: rank r owns [r*2^10, (r+1)*2^10)
+    assert [p["rows"] for p in rp] == [[r << 10, (r + 1) << 10] for r in range(world)]
+    st = out["strong"]  # the C4 (here 2^11) matrix cut into `world` row blocks
+    assert st["scaling"] == "strong" and st["nnz_total"] == 32 << 11 and st["rows_per_rank"] == (1 << 11) // world
+    assert len(st["rank_kernel_us"]) == world and len(st["rank_parity"]) == world
+    assert all(p.startswith("within FAST bound") for p in st["rank_parity"]), st["rank_parity"]
+    assert st["x_bcast_us"] > 0 and st["value"] > 0
+
+
 def test_bench_multi_rank_gloo():
     res = _multi_rank([])
     assert res[1] is None  # only rank 0 prints the line
     out = res[0]
+    _check_rank_parity_and_strong(out, 2)
     assert out["n_gpus"] == 2 and out["x_bcast_us"] is not None
     e2e = out["end_to_end"]
     assert e2e["value"] <= out["value"] and abs(e2e["ms_per_step"] - out["ms_per_step"] - out["x_bcast_us"] * 1e-3) < 1e-3
@@ -335,4 +358,5 @@ def test_bench_four_ranks_gloo():
     out = res[0]
     assert all(res[r] is None for r in (1, 2, 3))
     assert out["n_gpus"] == 4 and len(out["rank_kernel_us"]) == 4
+    _check_rank_parity_and_strong(out, 4)
     assert out["config"]["nnz_total"] == 4 * out["config"]["nnz_per_gpu"]

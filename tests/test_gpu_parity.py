@@ -96,7 +96,10 @@ def _random_csc(rows, cols, density, rng, dtype=np.float64, empty_rows=True, lon
     return colptr, rowind, vals
 
 
-@pytest.mark.parametrize("shape", [(1, 1), (1, 300), (300, 1), (257, 1000), (5000, 333), (3000, 20000)])
+# (700, 20001): odd columns over 6 panels of the split geometry (2 per part, the last
+# panel patched); (900, 14001): 4 panels, column parts of 1, 1 and 2 (vc_part_first)
+@pytest.mark.parametrize("shape", [(1, 1), (1, 300), (300, 1), (257, 1000), (5000, 333), (3000, 20000),
+                                   (700, 20001), (900, 14001)])
 @pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
 def test_random_ragged(gpu, shape, kernel):
     rng = np.random.default_rng(shape[0] * 31 + shape[1])
@@ -123,9 +126,10 @@ def test_random_u64_wraparound(gpu, kernel):
 def test_random_duplicates(gpu, kernel):
     # repeated (row, col) entries (5 % of a ragged matrix with a full-width row):
     # ORDERED kernels add each copy in CSC order, bit for bit; FAST within the bound
+    # 20001 columns: enough panels for the three-part split geometry (6), odd width
     rng = np.random.default_rng(11)
-    rows, cols = 2000, 3000
-    colptr, rowind, vals = _random_csc(rows, cols, 0.01, rng, long_rows=[77], dup=True)
+    rows, cols = 2000, 20001
+    colptr, rowind, vals = _random_csc(rows, cols, 0.0015, rng, long_rows=[77], dup=True)
     assert np.any(np.diff(rowind.astype(np.int64)) == 0)  # some entry is repeated
     x = rng.uniform(-1, 1, cols)
     mode = hs.MODE_ORDERED if kernel in ORDERED_KERNELS else hs.MODE_FAST
@@ -558,3 +562,78 @@ def test_exec_device_rejects_bad_tensors(gpu):
         with pytest.raises(ValueError):
             h.exec_device(bad_x, bad_y, beta=0, mode=hs.MODE_ORDERED)
     h.close()
+
+
+def test_split_eligible_at_four_panels(gpu):
+    # 12001-16000 columns give the split geometry 4 panels: parts of 1, 1, 2 (a ceil cut left the
+    # third part empty and the matrix ineligible)
+    rng = np.random.default_rng(3)
+    colptr, rowind, vals = _random_csc(1500, 14001, 0.003, rng)
+    h = hs.Handle.from_csc(colptr, rowind, vals, 1500, 14001)
+    assert h.stat("vcache_split_eligible") == 1
+    x = rng.uniform(-1, 1, 14001)
+    for beta in (0, 1):
+        _check("4 panels", 1500, 14001, colptr, rowind, vals, x, "vcache_split", beta, hs.MODE_FAST)
+
+
+def test_graph_capture_after_eager_launch_on_another_stream(gpu):
+    # A scratch kernel (vcache_split: tickets + partials) launched eagerly on stream A, then captured
+    # on a fresh stream B: the library neither waits on nor records its scratch event inside the
+    # capture, the replays give the eager bits, and eager launches on A resume after it.
+    import torch
+    n = 1 << 16
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    h.set_kernel("vcache_split")
+    xd = torch.from_numpy(hs.gen_vector(n, 3)).cuda()
+    ya, yb = (torch.empty(n, dtype=torch.float64, device="cuda") for _ in range(2))
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    h.exec_device(xd, ya, beta=0, mode=hs.MODE_FAST, stream=sa)
+    torch.cuda.synchronize()
+    ref = ya.cpu().numpy().copy()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=sb):
+        for _ in range(3):
+            h.exec_device(xd, yb, beta=0, mode=hs.MODE_FAST, stream=sb)
+    with torch.cuda.stream(sb):
+        g.replay()
+        g.replay()
+    torch.cuda.synchronize()
+    assert yb.cpu().numpy().tobytes() == ref.tobytes()
+    h.exec_device(xd, ya, beta=0, mode=hs.MODE_FAST, stream=sa)
+    torch.cuda.synchronize()
+    assert ya.cpu().numpy().tobytes() == ref.tobytes()
+
+
+def test_auto_layouts_built_at_create(gpu):
+    # AUTO's layouts (here ORDERED -> sell, FAST -> vcache_split) exist after create and count as
+    # setup; a kernel selected by name builds its layout then, timed in layout_ns and setup_ns
+    n = 1 << 16
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    assert h.kernel_name(hs.MODE_ORDERED) == "sell" and h.kernel_name(hs.MODE_FAST) == "vcache_split"
+    assert h.stat("sell_slices") > 0 and h.stat("auto_fallback") == 0
+    x = hs.gen_vector(n, 3)
+    y_o = h.exec(x, beta=0, mode=hs.MODE_ORDERED)
+    h.exec(x, beta=0, mode=hs.MODE_FAST)
+    assert h.stat("layout_ns") == 0 and h.stat("setup_ns") == h.stat("create_ns") > 0
+    h.set_kernel("vcache")  # the ordered vcache layout: built now, from the device CSR copy
+    assert h.stat("layout_ns") > 0 and h.stat("setup_ns") == h.stat("create_ns") + h.stat("layout_ns")
+    assert h.exec(x, beta=0, mode=hs.MODE_ORDERED).tobytes() == y_o.tobytes()
+
+
+def test_wgather_chunked_launches_bit_identical(gpu):
+    # k_wgather runs its row blocks in launches of `wgather_chunk` (kWgChunk = 256: one per CU);
+    # any chunking gives the single-launch bits, ORDERED == the oracle
+    rows, cols = 1 << 14, 1 << 21
+    rowptr, colind, vals = hs.gen_stripe_csr(0, rows, cols, 32)
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+    assert h.kernel_name(hs.MODE_ORDERED) == "wgather" and h.stat("wgather_chunk") == 256
+    x = hs.gen_vector(cols, 3)
+    colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+    y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=rows)
+    outs = []
+    for chunk in (0, 256, 7, 1):
+        h.set_option("wgather_chunk", chunk)
+        outs.append(h.exec(x, beta=0, mode=hs.MODE_ORDERED).tobytes())
+    assert all(o == y_ref.tobytes() for o in outs)
