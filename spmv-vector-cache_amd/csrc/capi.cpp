@@ -125,12 +125,23 @@ struct hipspmv_handle {
   hipEvent_t scratch_ev = nullptr;
   hipStream_t scratch_stream = nullptr;
   bool scratch_used = false;
+  // option "profile" (DESIGN.md §6.9): vcache / vcache_split launches run with
+  // the kernel's profile stamps; the NewCache state statistics come from them
+  int profile = 0;
+  uint32_t* d_prof = nullptr;  // ordered geometry: kVcProfWords per workgroup (split: inside d_tickets)
+  bool prof_pending = false, prof_valid = false;
+  hipStream_t prof_stream = nullptr;
+  int prof_layout = 0;  // vc[] index of the profiled launch
+  struct Prof {  // means over the workgroups of the last profiled launch, shader cycles
+    uint64_t fill = 0, active = 0, flush = 0, done = 0, loader_work = 0, loader_wait = 0, compute_wait = 0;
+    uint64_t units = 0, span = 0;
+  } prof;
 };
 
 static void release(hipspmv_t* h) {
   if (!h) return;
   DeviceGuard g(h->device);
-  void* ptrs[] = {h->d_rowptr, h->d_colind, h->d_groups, h->d_vals, h->d_x, h->d_y};
+  void* ptrs[] = {h->d_rowptr, h->d_colind, h->d_groups, h->d_vals, h->d_x, h->d_y, h->d_prof};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& v : h->vc) {
@@ -187,8 +198,9 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g) {
   if ((st = dev_upload(&v.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return fail(st);
   if (v.split > 1) {
     // [0, nblocks): arrival tickets, [nblocks, 2 nblocks): published partials
-    // (the ticket-first combine of k_vcache); both self-reset after each launch
-    std::vector<uint32_t> zeros(2ull * v.nblocks, 0u);
+    // (the ticket-first combine of k_vcache); both self-reset after each launch;
+    // then kVcProfWords per unit for the profile stamps (option "profile")
+    std::vector<uint32_t> zeros(2ull * v.nblocks + (uint64_t)kVcProfWords * v.nblocks * v.split, 0u);
     if ((st = dev_upload(&v.d_tickets, zeros.data(), zeros.size(), h->device_bytes))) return fail(st);
     // partials: part q of block b at (q * nblocks + b) * VRP doubles, VRP = the
     // geometry's y block rounded up to even (k_vcache's 16-byte combine)
@@ -490,7 +502,22 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                  v.d_tickets, h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
                  v.npad,      h->nnz - 1, v.split,   beta, h->vcache_dma, (uint32_t)geoms[k].panel,
                  h->vcache_xlane, v.max_seg, h->vcache_map};
-    e = launch_vcache(h->dtype, a, s);
+    h->prof_pending = false;
+    if (h->profile && k < 2) {  // the default configuration with its profile stamps
+      if (k == 0 && !h->d_prof) {
+        const size_t b = 4ull * kVcProfWords * v.nblocks;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&h->d_prof), b));
+        h->device_bytes += b;
+      }
+      if (k == 0) a.partial = h->d_prof;
+      e = launch_vcache_profiled(h->dtype, a, s);
+      h->prof_pending = e == hipSuccess;
+      h->prof_valid = false;
+      h->prof_stream = s;
+      h->prof_layout = k;
+    } else {
+      e = launch_vcache(h->dtype, a, s);
+    }
   } else if (kernel == HIPSPMV_KERNEL_WGATHER) {
     const auto& v = h->vc[3];
     VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    nullptr,
@@ -523,6 +550,46 @@ static int resolve_pending(hipspmv_t* h) {
   HIP_TRY(hipEventElapsedTime(&ms, h->ev[1], h->ev[2]));
   h->kernel_ns = (uint64_t)(ms * 1e6);
   h->pending = false;
+  return HIPSPMV_OK;
+}
+
+// The NewCache state statistics of the last profiled launch, from its stamps
+// (csrc/vcache.hip, AB bit 128): means over the workgroups, converted to
+// shader cycles at the handle's clock (s_memrealtime ticks are 10 ns).
+static int resolve_profile(hipspmv_t* h) {
+  if (!h->prof_pending) return HIPSPMV_OK;
+  DeviceGuard g(h->device);
+  HIP_TRY(hipStreamSynchronize(h->prof_stream));
+  const auto& v = h->vc[h->prof_layout];
+  const uint32_t units = v.nblocks * v.split;
+  std::vector<uint32_t> st((size_t)kVcProfWords * units);
+  const uint32_t* src = h->prof_layout == 0 ? h->d_prof : v.d_tickets + 2ull * v.nblocks;
+  HIP_TRY(hipMemcpy(st.data(), src, 4ull * st.size(), hipMemcpyDeviceToHost));
+  const double cyc_per_tick = h->clock_khz / 1e5;
+  auto at = [&](uint32_t u, int k) { return st[(size_t)kVcProfWords * u + k]; };
+  uint32_t t_end = at(0, 3);
+  for (uint32_t u = 1; u < units; ++u)
+    if ((int32_t)(at(u, 3) - t_end) > 0) t_end = at(u, 3);
+  uint32_t t_beg = at(0, 0);
+  for (uint32_t u = 1; u < units; ++u)
+    if ((int32_t)(at(u, 0) - t_beg) < 0) t_beg = at(u, 0);
+  double fill = 0, active = 0, flush = 0, done = 0, lw = 0, lwait = 0, cwait = 0;
+  for (uint32_t u = 0; u < units; ++u) {
+    fill += (uint32_t)(at(u, 1) - at(u, 0));
+    active += (uint32_t)(at(u, 2) - at(u, 1));
+    flush += (uint32_t)(at(u, 3) - at(u, 2));
+    done += (uint32_t)(t_end - at(u, 3));
+    lw += at(u, 5);
+    lwait += at(u, 6);
+    cwait += at(u, 7);
+  }
+  auto mean_cyc = [&](double ticks) { return (uint64_t)std::llround(ticks / units * cyc_per_tick); };
+  auto mean = [&](double c) { return (uint64_t)std::llround(c / units); };
+  h->prof = hipspmv_handle::Prof{mean_cyc(fill), mean_cyc(active), mean_cyc(flush), mean_cyc(done), mean(lw),
+                                 mean(lwait), mean(cwait), units,
+                                 (uint64_t)std::llround((uint32_t)(t_end - t_beg) * cyc_per_tick)};
+  h->prof_pending = false;
+  h->prof_valid = true;
   return HIPSPMV_OK;
 }
 
@@ -581,6 +648,8 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
     h->mode_opt = (int)value;
   } else if (k == "timing") {
     h->timing = value ? 1 : 0;
+  } else if (k == "profile") {  // NewCache state statistics from the vcache kernels' stamps
+    h->profile = value ? 1 : 0;
   } else {
     return HIPSPMV_ERR_KEY;
   }
@@ -718,6 +787,37 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
       *out = li >= 0 ? (uint64_t)h->vc[li].rows_per_block +
                            (lds_x ? 2ull * (li == 0 ? kVcOrdered.panel : li == 1 ? kVcSplit.panel : kVcSplit4.panel) : 0)
                      : 0;
+  } else if (k == "profile" || k == "profiled" || k == "profile_units" || k == "profile_span_cycles" ||
+             k.rfind("state_", 0) == 0 || k == "no_valid_but_ready" || k == "no_ready_but_valid") {
+    // the reference's cache-FSM state counts and stream-monitor stalls
+    // (HardwareSpMVNewCache.cpp:130-204, NoWMVectorCache.scala:162-292),
+    // measured by the last profiled launch
+    if (int st = resolve_profile(h)) return st;
+    const auto& p = h->prof;
+    const bool ok = h->prof_valid;
+    if (k == "profile") *out = (uint64_t)h->profile;
+    else if (k == "profiled") *out = ok;
+    else if (k == "profile_units") *out = ok ? p.units : 0;
+    else if (k == "profile_span_cycles") *out = ok ? p.span : 0;
+    else if (k == "state_fill") *out = ok ? p.fill : 0;        // y block initialised, first x panel staged
+    else if (k == "state_active") *out = ok ? p.active : 0;    // the panel steps
+    else if (k == "state_flush") *out = ok ? p.flush : 0;      // column-part combine and y written back
+    else if (k == "state_done") *out = ok ? p.done : 0;        // finished, waiting for the launch's last workgroup
+    else if (k == "state_read_miss1") *out = 0;                // no write-before-miss ordering on the GPU
+    else if (k == "state_read_miss2") *out = ok ? p.loader_work : 0;  // fetching x panels (loader wave, per step)
+    else if (k == "state_read_miss3") *out = 0;                // LDS-DMA lands panels without a fill step
+    else if (k == "state_cold_miss") *out = h->last_beta ? 0 : h->rows;  // rows started at +0.0 without a read
+    else if (k == "no_valid_but_ready") *out = ok ? p.compute_wait : 0;  // compute waves waiting on the panel
+    else if (k == "no_ready_but_valid") *out = ok ? p.loader_wait : 0;   // panel ready, compute still busy
+    else return HIPSPMV_ERR_KEY;
+  } else if (k == "issue_window") {  // entries one workgroup keeps in flight (vcache family), else 0
+    const int kn = h->last_kernel;
+    *out = kn == HIPSPMV_KERNEL_VCACHE ? 4ull * 3 * 8 * 64 : kn == HIPSPMV_KERNEL_VCACHE_SPLIT ? 4ull * 2 * 13 * 64 : 0;
+  } else if (k == "capacity_stalls" || k == "cms") {
+    // capacity stalls: no fixed issue window (the hardware analogue is
+    // TCP_PENDING_STALL_CYCLES, tools/cache_stats.py); cms: the kernels mask
+    // the cold-miss-skip bits at create and never use them
+    *out = 0;
   } else if (k == "total_cycles" || k == "active_cycles") {
     int st = resolve_pending(h);
     if (st) return st;

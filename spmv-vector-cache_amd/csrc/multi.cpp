@@ -369,6 +369,22 @@ int hipspmv_multi_stat(hipspmv_multi_t* m, const char* key, uint64_t* out) {
       acc = sum ? acc + v : std::max(acc, v);
     }
     *out = acc;
+  } else if (k.rfind("state_", 0) == 0 || k == "no_valid_but_ready" || k == "no_ready_but_valid" ||
+             k == "profiled" || k == "profile" || k == "profile_units" || k == "profile_span_cycles" ||
+             k == "issue_window" || k == "capacity_stalls" || k == "cms") {
+    // NewCache state statistics: the slowest block's (max); "profiled" only
+    // if every block's last launch was profiled (min); units summed
+    const bool mn = k == "profiled" || k == "profile", sum = k == "profile_units";
+    uint64_t acc = mn ? 1 : 0;
+    bool any = false;
+    for (auto& s : m->shards) {
+      uint64_t v = 0;
+      if (!s.h) continue;
+      if (int st = hipspmv_stat(s.h, key, &v)) return st;
+      acc = mn ? std::min(acc, v) : sum ? acc + v : std::max(acc, v);
+      any = true;
+    }
+    *out = any ? acc : 0;
   } else if (k == "alg_bytes") {
     // per device: its rows' entries + its rowptr + all of x + its y
     uint64_t b = 0;

@@ -57,7 +57,12 @@ struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane
 // AB: ablation mask for the diagnostic build (tools/vc_ablate.hip); the
 // product instantiates AB = 0 and every hook folds away.  Bits: 1 no x loads,
 // 2 no x LDS stores, 4 no entry loads, 8 no compute, 16 x always from panel 0,
-// 32 no per-panel barrier, 64 no column-part combine (wrong results, timing only).
+// 32 no per-panel barrier, 64 no column-part combine (wrong results, timing only),
+// 128 profile stamps, results unchanged (option "profile"): 8 u32
+// per workgroup at tickets + 2 * nblocks + 8 * blockIdx.x (SPLIT 1: at partial):
+// s_memrealtime (100 MHz) at start, main-loop start, main-loop end, exit; the
+// combine ticket; s_memtime cycles summed over the steps: loader wave 0 working,
+// loader wave 0 waiting at the step barrier, first compute wave waiting there.
 template <typename T, int SPLIT, int WL = VcCfg<SPLIT>::WL, int DE = VcCfg<SPLIT>::DE, int EPT = VcCfg<SPLIT>::EPT,
           int AB = 0, int MAP = 0, bool NT = false, int LD = 0, int CX = 0>
 __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restrict__ seg,
@@ -95,6 +100,12 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   const uint32_t r0 = b * rows_per_block;
   if (r0 >= rows) return;  // never with a vcache_grid_ok geometry (workgroup-uniform, before any barrier)
   const uint32_t nr = min(rows_per_block, rows - r0);
+  uint32_t* const sbuf = (SPLIT == 1 ? reinterpret_cast<uint32_t*>(partial) : tickets + 2 * nblocks) + 8 * blockIdx.x;
+  auto stamp = [&](int k, uint32_t v) {
+    if ((AB & 128) && t == 0) sbuf[k] = v;
+  };
+  auto now = [] { return (uint32_t)__builtin_amdgcn_s_memrealtime(); };
+  if (AB & 128) stamp(0, now());
   const uint32_t p0 = vc_part_first(h, npanels, SPLIT);             // first global panel of this unit
   const uint32_t npu = vc_part_first(h + 1, npanels, SPLIT) - p0;   // >= 1 (vcache_grid_ok)
   const uint32_t* sp = seg + ((size_t)b * SPLIT + h) * (npad + 1);
@@ -283,6 +294,19 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
+  // profile (AB & 128): cycles between step barriers (work) and inside them (wait)
+  uint64_t pf_work = 0, pf_wait = 0, pf_mark = 0;
+  auto pbarrier = [&]() {
+    if (AB & 128) {
+      const uint64_t a = __builtin_amdgcn_s_memtime();
+      pf_work += a - pf_mark;
+      barrier();
+      pf_mark = __builtin_amdgcn_s_memtime();
+      pf_wait += pf_mark - a;
+    } else {
+      barrier();
+    }
+  };
   // CX >= 2: both roles run a step count padded to the unroll (extra steps do
   // no work but keep their loads and barrier), so no loop exits mid-group.
   // An early exit inside the unrolled group is what makes hipcc's waitcnt
@@ -300,11 +324,15 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     patch_x(0);
     barrier();
+    if (AB & 128) {
+      stamp(1, now());
+      pf_mark = __builtin_amdgcn_s_memtime();
+    }
     for (uint32_t s = 0; s < nsteps; ++s) {
       if (s + 1 < npu) dma_x(s + 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (s + 1 < npu) patch_x(s + 1);
-      barrier();
+      pbarrier();
     }
   } else if (loader && LD == 2) {
     // same ring, asm loads: storing x(s+1) waits for it with x(s+2)'s NJ
@@ -335,6 +363,10 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     load_x(1, R[1]);
     load_x(2, R[0]);
     barrier();
+    if (AB & 128) {
+      stamp(1, now());
+      pf_mark = __builtin_amdgcn_s_memtime();
+    }
     for (uint32_t base = 0; base < nsteps; base += 2) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -342,7 +374,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
         if (!PAD && s >= npu) break;
         if (s + 1 < npu) store_x(s + 1, R[(i + 1) & 1]);
         load_x(s + 3, R[(i + 1) & 1]);
-        barrier();
+        pbarrier();
       }
     }
   } else {
@@ -351,6 +383,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
 #pragma unroll
     for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i]);
     barrier();
+    if (AB & 128) pf_mark = __builtin_amdgcn_s_memtime();
     for (uint32_t base = 0; base < nsteps; base += DE) {
 #pragma unroll
       for (int i = 0; i < DE; ++i) {
@@ -363,17 +396,28 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
           apply(s, EC[i], EV[i]);
         }
         load_e(s + DE, EC[i], EV[i]);
-        barrier();
+        pbarrier();
       }
     }
     if (CX == 2) vm_wait<0>();  // the clamped prefetches past the last panel
   }
+  if (AB & 128) {
+    if (t == 0) {
+      sbuf[5] = (uint32_t)pf_work;
+      sbuf[6] = (uint32_t)pf_wait;
+    }
+    if (t == LT) sbuf[7] = (uint32_t)pf_wait;
+    __syncthreads();
+    stamp(2, now());
+  }
   if (AB & 64) {  // ablation: no combine, y straight from LDS (timing only)
     for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
+    if (AB & 128) stamp(3, now());
     return;
   }
   if (SPLIT == 1) {
     for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
+    if (AB & 128) stamp(3, now());
     return;
   }
   // ---- combine the column parts, fixed order p0 + p1 + p2 (+ p3), ticket
@@ -408,6 +452,10 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) __hip_atomic_fetch_add(published + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (AB & 128) {
+      stamp(3, now());
+      stamp(4, segl[0]);
+    }
     return;
   }
   if (t == 0) {
@@ -422,6 +470,44 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     __hip_atomic_store(tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  if constexpr (SPLIT == 4) {
+    // four parts: row pairs in chunks of 4 per lane (all 8 at once spilled
+    // past 128 VGPRs), y = p0 + p1 + p2 + p3 in part order
+    static_assert(NP % 4 == 0, "whole chunks");
+#pragma unroll
+    for (int j0 = 0; j0 < NP; j0 += 4) {
+      T acc[4][2];
+#pragma unroll
+      for (int q = 0; q < SPLIT; ++q) {
+        u64x2 v[4];
+        if ((uint32_t)q == h) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = yl2[min((uint32_t)(t + (j0 + j) * VT), VRP / 2 - 1)];
+        } else {
+          const __amdgpu_buffer_rsrc_t src = buf_rsrc(partial + ((size_t)q * nblocks + b) * VRP, 8 * VRP);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = ld_128_sc1(src, 16 * min((uint32_t)(t + (j0 + j) * VT), VRP / 2 - 1));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const T w0 = __builtin_bit_cast(T, (uint64_t)v[j].x), w1 = __builtin_bit_cast(T, (uint64_t)v[j].y);
+          acc[j][0] = q == 0 ? w0 : acc[j][0] + w0;
+          acc[j][1] = q == 0 ? w1 : acc[j][1] + w1;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t p = t + (j0 + j) * VT;
+        if (2 * p < nr) y_out[r0 + 2 * p] = acc[j][0];
+        if (2 * p + 1 < nr) y_out[r0 + 2 * p + 1] = acc[j][1];
+      }
+    }
+    if (AB & 128) {
+      stamp(3, now());
+      stamp(4, segl[0]);
+    }
+    return;
+  }
   // y = p0 + p1 + p2 (+ p3) in part order; part h from LDS, the others loaded
   T acc[NP][2];
 #pragma unroll
@@ -448,6 +534,10 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     if (2 * p < nr) y_out[r0 + 2 * p] = acc[j][0];
     if (2 * p + 1 < nr) y_out[r0 + 2 * p + 1] = acc[j][1];
   }
+  if (AB & 128) {
+    stamp(3, now());
+    stamp(4, segl[0]);
+  }
 }
 
 template <typename T, int SPLIT, int LD, int CX = 0, int MAP = 0>
@@ -460,7 +550,7 @@ static void launch_one(const VcacheArgs& a, hipStream_t s) {
 
 template <typename T, int SPLIT, int MAP = 0>
 static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
-  if constexpr (SPLIT == 3) {  // two loader waves: LDS-DMA only (a register-staged panel would spill)
+  if constexpr (SPLIT == 3) {  // three loader waves: LDS-DMA only (a register-staged panel would spill)
     if (cx == 0)
       launch_one<T, SPLIT, 1, 0, MAP>(a, s);
     else if (cx == 1)
@@ -517,6 +607,38 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
 
 hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s) {
   return dtype ? launch_vcache<uint64_t>(a, s) : launch_vcache<double>(a, s);
+}
+
+template <typename T>
+static hipError_t launch_vcache_profiled_t(const VcacheArgs& a, hipStream_t s) {
+  const VcGeom g = a.split == 1 ? kVcOrdered : kVcSplit;
+  if ((a.split != 1 && a.split != 3) || (a.split == 1 ? !a.partial : !a.tickets) ||
+      !vcache_grid_ok(a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.panel,
+                      a.split, g))
+    return hipErrorInvalidValue;
+  constexpr int P = 128;  // AB: profile stamps only
+  const dim3 grid(a.nblocks * a.split), block(kVcThreads);
+  if (a.split == 1) {
+    hipLaunchKernelGGL((k_vcache<T, 1, VcCfg<1>::WL, VcCfg<1>::DE, VcCfg<1>::EPT, P>), grid, block, 0, s, a.seg,
+                       a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial,
+                       a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad,
+                       a.last, a.beta);
+  } else if (a.max_seg <= (uint32_t)((kVcThreads / 64 - VcCfg<3>::WL) * 64 * VcCfg<3>::EPT)) {
+    hipLaunchKernelGGL((k_vcache<T, 3, VcCfg<3>::WL, VcCfg<3>::DE, VcCfg<3>::EPT, P, 0, false, 1, 3>), grid, block, 0,
+                       s, a.seg, a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out,
+                       (T*)a.partial, a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels,
+                       a.part_panels, a.npad, a.last, a.beta);
+  } else {
+    hipLaunchKernelGGL((k_vcache<T, 3, VcCfg<3>::WL, VcCfg<3>::DE, VcCfg<3>::EPT, P, 0, false, 1, 0>), grid, block, 0,
+                       s, a.seg, a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out,
+                       (T*)a.partial, a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels,
+                       a.part_panels, a.npad, a.last, a.beta);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_vcache_profiled(int dtype, const VcacheArgs& a, hipStream_t s) {
+  return dtype ? launch_vcache_profiled_t<uint64_t>(a, s) : launch_vcache_profiled_t<double>(a, s);
 }
 
 }  // namespace hipspmv

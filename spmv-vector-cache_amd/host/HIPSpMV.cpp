@@ -13,7 +13,7 @@ HIPSpMVRegisterFile* HIPSpMV::registerFile(int device) {
   auto it = files.find(device);
   if (it == files.end())
     it = files.emplace(device, HIPSpMVRegisterFile{kSignature, device, HIPSPMV_MODE_ORDERED, HIPSPMV_KERNEL_AUTO, 1, 0,
-                                                   1, {device}})
+                                                   1, {device}, 0})
              .first;
   return &it->second;
 }
@@ -71,6 +71,9 @@ void HIPSpMV::init() {}
 // reference's busy-wait on doneRegular (HardwareSpMVNewCache.cpp:90-101).
 void HIPSpMV::regular() {
   if (m_status || !(m_h || m_multi)) return;
+  m_status = m_multi ? hipspmv_multi_set_option(m_multi, "profile", regs()->profile)
+                     : hipspmv_set_option(m_h, "profile", regs()->profile);
+  if (m_status) return;
   m_status = m_multi ? hipspmv_multi_exec(m_multi, m_x, m_y, regs()->beta, regs()->mode)
                      : hipspmv_exec(m_h, m_x, m_y, regs()->beta, regs()->mode);
   if (m_status)
@@ -112,8 +115,12 @@ std::vector<std::string> HIPSpMV::statKeys() {
   std::vector<std::string> keys = HardwareSpMV::statKeys();
   for (const char* k : {"kernelTimeUs", "setupTimeUs", "h2dTimeUs", "d2hTimeUs", "algKBytes", "mode", "kernel",
                         "device", "error", "numDevices", "bcastTimeUs", "maxAlive", "maxColSpan", "cmstime",
-                        "maxAliveTime", "maxColSpanTime", "totalCycles", "activeCycles", "readMisses",
-                        "hazardStalls", "ocmDepth"})
+                        "maxAliveTime", "maxColSpanTime"})
+    keys.push_back(k);
+  // HardwareSpMVNewCache::statKeys (HardwareSpMVNewCache.cpp:189-204), same names and order
+  for (const char* k : {"sActive", "sFill", "sFlush", "sDone", "sReadMiss1", "sReadMiss2", "sReadMiss3",
+                        "sColdMiss", "totalCycles", "activeCycles", "readMisses", "ocmDepth", "issueWindow",
+                        "hazardStalls", "capacityStalls", "cms", "noValidButReady", "noReadyButValid"})
     keys.push_back(k);
   return keys;
 }
@@ -161,6 +168,19 @@ unsigned int HIPSpMV::statInt(std::string name) {
   if (name == "readMisses") return (unsigned int)statU64("read_misses");
   if (name == "hazardStalls") return (unsigned int)statU64("hazard_stalls");
   if (name == "ocmDepth") return (unsigned int)statU64("ocm_depth");
+  // the cache-FSM state counts (stateNames, HardwareSpMVNewCache.cpp:6-7) and the
+  // stream-monitor stalls, measured by a profiled launch (register `profile`):
+  // cycles per workgroup (one vector cache), DESIGN.md §6.9
+  static const std::map<std::string, const char*> states = {
+      {"sActive", "state_active"},         {"sFill", "state_fill"},
+      {"sFlush", "state_flush"},           {"sDone", "state_done"},
+      {"sReadMiss1", "state_read_miss1"},  {"sReadMiss2", "state_read_miss2"},
+      {"sReadMiss3", "state_read_miss3"},  {"sColdMiss", "state_cold_miss"},
+      {"issueWindow", "issue_window"},     {"capacityStalls", "capacity_stalls"},
+      {"cms", "cms"},                      {"noValidButReady", "no_valid_but_ready"},
+      {"noReadyButValid", "no_ready_but_valid"}};
+  auto it = states.find(name);
+  if (it != states.end()) return (unsigned int)statU64(it->second);
   if (name == "thresColPtr") return m_thres.colPtr;
   if (name == "thresRowInd") return m_thres.rowInd;
   if (name == "thresNZData") return m_thres.nzData;

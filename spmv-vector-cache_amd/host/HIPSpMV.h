@@ -30,6 +30,10 @@ struct HIPSpMVRegisterFile {
   // (hipspmv_multi_*; x broadcast device to device).  0 or 1: `device` alone.
   int32_t num_devices;
   int32_t devices[16];
+  // 1: vcache-family launches record the NewCache state statistics (sActive,
+  // sFill, ..., noValidButReady) -- the reference's profileSel/profileCount
+  // registers (SpMVAcceleratorNewCache.scala:44,58) read after the run
+  int32_t profile;
 };
 
 class HIPSpMV : public HardwareSpMV {

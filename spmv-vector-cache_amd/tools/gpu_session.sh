@@ -36,6 +36,14 @@ for s in $STEPS; do
     micro) step micro 300 ./spmv-vector-cache_amd/tools/microbench ;;
     exp) HIPSPMV_EXPERIMENTAL=1 step pytest_exp 600 python -m pytest tests/test_gpu_parity.py -m gpu -q -x -p no:cacheprovider -k experimental ;;
     ablate) step ablate 600 ./spmv-vector-cache_amd/lib/vc_ablate ;;
+    stamps) step stamps 300 ./spmv-vector-cache_amd/lib/vc_ablate 20 stamps ;;
+    chain) step chain 120 ./spmv-vector-cache_amd/lib/chain_probe ;;
+    mall) step mall88 300 ./spmv-vector-cache_amd/lib/pf_probe 88 base && step mall44 300 ./spmv-vector-cache_amd/lib/pf_probe 44 base &&
+          step mall22 300 ./spmv-vector-cache_amd/lib/pf_probe 22 base ;;
+    benchtime) step bench_time 900 bash -c 'time python bench.py' ;;
+    mallpol) step mall_policy 300 ./spmv-vector-cache_amd/lib/pf_probe 88 mall ;;
+    sweepc4c) step sweep_c4_chunks 900 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 24 --log2-cols 24 --only "wgather c" --rounds 2 --reps 10 ;;
+    newtests) step pytest_new 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "profile or spmvbench or cache_behaviour" ;;
     sweep) step sweep 600 python spmv-vector-cache_amd/tools/kernel_sweep.py ;;
     sweepx) HIPSPMV_EXPERIMENTAL=1 step sweep_exp 900 python spmv-vector-cache_amd/tools/kernel_sweep.py ;;
     sweeprmat) step sweep_rmat 600 python spmv-vector-cache_amd/tools/kernel_sweep.py --rmat 20 ;;

@@ -39,6 +39,8 @@ cands = [("vcache", "vcache", O, {}), ("csr_lane", "csr_lane", O, {}), ("vcache_
          ("csr_vector", "csr_vector", F, {}), ("sell", "sell", O, {}), ("sell fast", "sell", F, {}),
          ("wgather", "wgather", O, {}), ("wgather c128", "wgather", O, {"wgather_chunk": 128}),
          ("wgather c512", "wgather", O, {"wgather_chunk": 512}), ("wgather c0", "wgather", O, {"wgather_chunk": 0}),
+         ("wgather c192", "wgather", O, {"wgather_chunk": 192}), ("wgather c320", "wgather", O, {"wgather_chunk": 320}),
+         ("wgather c384", "wgather", O, {"wgather_chunk": 384}),
          ("wgather xl2", "wgather", O, {"vcache_xlane": 2})]
 if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
     cands += [("vcache xl1", "vcache", O, {"vcache_xlane": 1}), ("vcache xl2", "vcache", O, {"vcache_xlane": 2}),

@@ -17,6 +17,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                               \
@@ -182,6 +183,66 @@ __global__ __launch_bounds__(kT) void k_probe(const uint32_t* __restrict__ code,
   if (t == 0) out[u] = ylds[0] + ylds[kYRows - 1];
 }
 
+// Infinity-Cache (MALL) residency probe: the units' entry streams (402 MB at
+// 88 steps, more than the 256 MiB MALL) read through buffer loads whose cache
+// policy is AUX for the odd units and the default for the even ones (aux bits,
+// gfx950: 1 sc0, 2 nt, 16 sc1).  If a policy keeps its lines out of the MALL,
+// the even half (201 MB) stays resident across back-to-back launches and the
+// launch gets faster; if not, every policy reads at the streaming rate.
+template <int AUX>
+__global__ __launch_bounds__(kT) void k_mall(const uint32_t* __restrict__ code, const double* __restrict__ vals,
+                                             double* __restrict__ out, uint32_t steps) {
+  const int t = threadIdx.x;
+  const uint32_t u = blockIdx.x;
+  const uint32_t n = steps * kChunk;  // entries of this unit
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(code + (size_t)u * n), (short)0, (int)(4 * n), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(vals + (size_t)u * n), (short)0, (int)(8 * n), 0x00020000);
+  double acc = 0.0;
+  const bool odd = __builtin_amdgcn_readfirstlane(u) & 1;
+  if (odd) {
+#pragma unroll 4
+    for (uint32_t i = t; i < n; i += kT) {
+      const uint32_t c = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)(4 * i), 0, AUX);
+      const uint64_t v = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rv, (int)(8 * i), 0, AUX));
+      acc += (double)c + __builtin_bit_cast(double, v);
+    }
+  } else {
+#pragma unroll 4
+    for (uint32_t i = t; i < n; i += kT) {
+      const uint32_t c = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)(4 * i), 0, 0);
+      const uint64_t v = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rv, (int)(8 * i), 0, 0));
+      acc += (double)c + __builtin_bit_cast(double, v);
+    }
+  }
+  if (acc == 12345.678) out[u] = acc;  // never true on the probe's data; keeps the loads
+}
+
+template <int AUX>
+static void run_mall(const char* name, const uint32_t* code, const double* vals, double* out, uint32_t units,
+                     uint32_t steps) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto launch = [&] { hipLaunchKernelGGL((k_mall<AUX>), dim3(units), dim3(kT), 0, 0, code, vals, out, steps); };
+  for (int i = 0; i < 5; ++i) launch();
+  CK(hipGetLastError());
+  const int reps = 30;
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < reps; ++i) launch();
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / reps, bytes = 12.0 * units * steps * kChunk;
+  std::printf("MALL %-28s steps %3u: %8.2f us  %6.0f GB/s  (%.0f MB of entries)\n", name, steps, us,
+              bytes / us / 1e3, bytes / 1e6);
+  std::fflush(stdout);
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
 template <bool X, bool E, int NPF, int EPT>
 static float run(const char* name, const uint32_t* code, const double* vals, const double* x, double* out,
                  uint32_t units, uint32_t steps, uint32_t part_cols, int dp) {
@@ -212,8 +273,10 @@ static float run(const char* name, const uint32_t* code, const double* vals, con
   return (float)us;
 }
 
-int main() {
-  const uint32_t units = 255, steps = 88, part_cols = 349526 / kPanel * kPanel;  // 87 panels; panel s % 87
+int main(int argc, char** argv) {
+  // steps: 88 = the C3 split unit (402 MB of entries per launch); fewer steps
+  // shrink the entry stream (44: 201 MB, inside the 256 MiB Infinity Cache)
+  const uint32_t units = 255, steps = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 88, part_cols = 349526 / kPanel * kPanel;  // 87 panels; panel s % 87
   const size_t n = (size_t)units * steps * kChunk;                           // 34.5 M entries (C3: 33.5 M)
   uint32_t* code;
   double *vals, *x, *out;
@@ -224,11 +287,24 @@ int main() {
   CK(hipMemset(code, 1, 4 * n));
   CK(hipMemset(vals, 0, 8 * n));
   CK(hipMemset(x, 0, 8ull * 3 * part_cols));
+  if (argc > 2 && std::string(argv[2]) == "mall") {
+    for (int rnd = 0; rnd < 2; ++rnd) {
+      run_mall<0>("all default", code, vals, out, units, steps);
+      run_mall<2>("odd units nt", code, vals, out, units, steps);
+      run_mall<16>("odd units sc1", code, vals, out, units, steps);
+      run_mall<17>("odd units sc0 sc1", code, vals, out, units, steps);
+      run_mall<18>("odd units nt sc1", code, vals, out, units, steps);
+      run_mall<19>("odd units nt sc0 sc1", code, vals, out, units, steps);
+      run_mall<3>("odd units nt sc0", code, vals, out, units, steps);
+    }
+    return 0;
+  }
   for (int rnd = 0; rnd < 2; ++rnd) {
     std::printf("-- round %d\n", rnd);
     run<false, true, 0, 2>("E only", code, vals, x, out, units, steps, part_cols, 0);
     run<true, false, 0, 2>("X only", code, vals, x, out, units, steps, part_cols, 0);
     run<true, true, 0, 2>("E + X (product skeleton)", code, vals, x, out, units, steps, part_cols, 0);
+    if (argc > 2) continue;  // E / X / E+X only
     for (int dp : {5, 6, 8, 12}) {
       run<false, true, 2, 3>("E + P2", code, vals, x, out, units, steps, part_cols, dp);
       run<true, true, 2, 3>("E + X + P2", code, vals, x, out, units, steps, part_cols, dp);

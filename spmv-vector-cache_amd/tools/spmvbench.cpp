@@ -12,7 +12,9 @@
 // microseconds.
 //
 //   spmvbench [--dir D] [--device N] [--mode ordered|fast] [--kernel K] [--reps N]
-//             [--cms 0|1] [--confs hip,sw] matrix...
+//             [--cms 0|1] [--confs hip,sw] [--profile 0|1] matrix...
+// --profile 1: vcache-family launches record the NewCache state statistics
+// (sActive ... noReadyButValid), measured in-kernel.
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
@@ -89,7 +91,7 @@ std::vector<std::string> readList() {
 
 int main(int argc, char** argv) {
   std::string dir = "tests/golden/matrices";
-  int device = 0, mode = HIPSPMV_MODE_ORDERED, kernel = HIPSPMV_KERNEL_AUTO, reps = 1;
+  int device = 0, mode = HIPSPMV_MODE_ORDERED, kernel = HIPSPMV_KERNEL_AUTO, reps = 1, profile = 0;
   bool cms = false, haveCms = false;
   std::vector<std::string> confs, ms;
   for (int i = 1; i < argc; ++i) {
@@ -106,6 +108,7 @@ int main(int argc, char** argv) {
                : k == "csr_vector" ? HIPSPMV_KERNEL_CSR_VECTOR
                : k == "sell" ? HIPSPMV_KERNEL_SELL : HIPSPMV_KERNEL_AUTO;
     } else if (a == "--reps") reps = std::atoi(next().c_str());
+    else if (a == "--profile") profile = std::atoi(next().c_str());
     else if (a == "--cms") { cms = std::atoi(next().c_str()) != 0; haveCms = true; }
     else if (a == "--confs") {
       std::stringstream ss(next());
@@ -132,6 +135,7 @@ int main(int argc, char** argv) {
   regs->mode = mode;
   regs->kernel = kernel;
   regs->beta = 1;  // y += A*x on a zeroed y, as main.cpp does
+  regs->profile = profile;
   const uintptr_t accBase = reinterpret_cast<uintptr_t>(regs);
   const uintptr_t resBase = reinterpret_cast<uintptr_t>(&regs->reset);
   int failures = 0;

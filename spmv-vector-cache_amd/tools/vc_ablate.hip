@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../host/Synthetic.h"
@@ -72,7 +73,9 @@ int main(int argc, char** argv) {
   for (VcGeom g : {kVcOrdered, kVcSplit, kVcSplit4}) {
     VcacheLayout L;
     build_vcache(a, g, L);
-    VcacheArgs A{up(L.seg), up(L.code), up(L.vals), dx, dy, dy, dpart, up(std::vector<uint32_t>(2 * L.nblocks, 0)),
+    // tickets: 2 per block for the combine + 8 stamp words per unit (AB & 128)
+    uint32_t* dtick = up(std::vector<uint32_t>(2 * L.nblocks + 8 * L.nblocks * g.split, 0));
+    VcacheArgs A{up(L.seg), up(L.code), up(L.vals), dx, dy, dy, dpart, dtick,
                  a.rows, a.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels, L.npad, a.nnz - 1,
                  g.split, 0};
     std::printf("geometry rows=%d panel=%d split=%d: units=%u npad=%u max_seg=%u\n", g.rows, g.panel, g.split,
@@ -107,6 +110,64 @@ int main(int argc, char** argv) {
       }
       std::printf("\n");
     };
+    // per-unit timeline of one launch (AB & 128: 8 stamp words per unit, csrc/vcache.hip)
+    auto stamps = [&](auto kern, const char* nm) {
+      const uint32_t units = A.nblocks * A.split;
+      for (int i = 0; i < 20; ++i)
+        hipLaunchKernelGGL(kern, dim3(units), dim3(kVcThreads), 0, nullptr, A.seg, A.code, (const double*)A.vals,
+                           (const double*)A.x, (const double*)A.y_in, (double*)A.y_out, (double*)A.partial,
+                           A.tickets, A.rows, A.cols, A.rows_per_block, A.nblocks, A.npanels, A.part_panels, A.npad,
+                           A.last, A.beta);
+      CK(hipDeviceSynchronize());
+      std::vector<uint32_t> st(8 * units);
+      const uint32_t* src = A.split == 1 ? reinterpret_cast<const uint32_t*>(A.partial) : A.tickets + 2 * A.nblocks;
+      CK(hipMemcpy(st.data(), src, 4ull * st.size(), hipMemcpyDeviceToHost));
+      uint32_t t0 = st[0];
+      for (uint32_t u = 0; u < units; ++u)
+        if ((int32_t)(st[8 * u] - t0) < 0) t0 = st[8 * u];
+      auto us = [&](uint32_t u, int k) { return (int32_t)(st[8 * u + k] - t0) * 0.01; };
+      std::vector<double> start, prolog, loop, tail_last, tail_pub, end, lwork, lwait, cwait;
+      for (uint32_t u = 0; u < units; ++u) {
+        start.push_back(us(u, 0));
+        prolog.push_back(us(u, 1) - us(u, 0));
+        loop.push_back(us(u, 2) - us(u, 1));
+        end.push_back(us(u, 3));
+        (A.split == 1 || st[8 * u + 4] == (uint32_t)A.split - 1 ? tail_last : tail_pub).push_back(us(u, 3) - us(u, 2));
+        lwork.push_back(st[8 * u + 5] / 2400.0);  // s_memtime cycles at a nominal 2.4 GHz
+        lwait.push_back(st[8 * u + 6] / 2400.0);
+        cwait.push_back(st[8 * u + 7] / 2400.0);
+      }
+      auto q = [](std::vector<double> v, const char* what) {
+        if (v.empty()) return;
+        std::sort(v.begin(), v.end());
+        std::printf("    %-26s min %7.2f  p10 %7.2f  median %7.2f  p90 %7.2f  max %7.2f us\n", what, v[0],
+                    v[v.size() / 10], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
+      };
+      std::printf("  stamps: %s (%u units; us from the first start)\n", nm, units);
+      q(start, "start");
+      q(prolog, "prologue");
+      q(loop, "main loop");
+      q(tail_pub, "publish (non-last)");
+      q(tail_last, "combine / write (last)");
+      q(end, "exit");
+      q(lwork, "loader work (2.4 GHz)");
+      q(lwait, "loader barrier wait");
+      q(cwait, "compute barrier wait");
+      for (uint32_t x = 0; x < 8; ++x) {  // by dispatch slot mod 8 (one XCD under round-robin placement)
+        std::vector<double> lx;
+        for (uint32_t u = x; u < units; u += 8) lx.push_back(loop[u]);
+        std::sort(lx.begin(), lx.end());
+        std::printf("    slot%%8=%u main loop median %7.2f max %7.2f\n", x, lx[lx.size() / 2], lx.back());
+      }
+    };
+    if (argc > 2 && std::string(argv[2]) == "stamps") {
+      if (g.split == 3) {
+        stamps(k_vcache<double, 3, 3, 4, 2, 128, 0, false, 1, 3>, "product (split 3)");
+      } else if (g.split == 1) {
+        stamps(k_vcache<double, 1, 8, 4, 3, 128>, "ordered vcache");
+      }
+      continue;
+    }
     // template: <T, SPLIT, WL, DE, EPT, AB, MAP, NT, LD, CX>
     if (g.split == 1) {
       variant(k_vcache<double, 1>, 1, "default (WL8 DE4 EPT3)", 0);

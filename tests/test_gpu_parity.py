@@ -269,6 +269,69 @@ def test_cache_behaviour_stats(gpu):
     h.close()
 
 
+REF_NEWCACHE_KEYS = ["sActive", "sFill", "sFlush", "sDone", "sReadMiss1", "sReadMiss2", "sReadMiss3", "sColdMiss",
+                     "totalCycles", "activeCycles", "readMisses", "ocmDepth", "issueWindow", "hazardStalls",
+                     "capacityStalls", "cms", "noValidButReady", "noReadyButValid"]
+
+
+def test_profile_state_statistics(gpu):
+    """option "profile": the vcache kernels' in-kernel stamps give the NewCache cache-FSM state counts
+    (HardwareSpMVNewCache.cpp:130-204) -- same bits as the unprofiled launch, and the per-workgroup
+    phases (fill + active + flush + done) add up to the launch's span"""
+    n = 1 << 18
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+    x = hs.gen_vector(n, 3)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    assert h.stat("profiled") == 0 and h.stat("state_active") == 0
+    for kernel, mode in [("vcache_split", hs.MODE_FAST), ("vcache", hs.MODE_ORDERED)]:
+        h.set_kernel(kernel)
+        y0 = h.exec(x, beta=0, mode=mode)
+        h.set_option("profile", 1)
+        y1 = h.exec(x, beta=0, mode=mode)
+        assert y1.tobytes() == y0.tobytes(), kernel
+        assert h.stat("profiled") == 1 and h.stat("profile_units") == (
+            h.stat("vcache_split_units") if kernel == "vcache_split" else h.stat("vcache_blocks")), kernel
+        st = {k: h.stat("state_" + k) for k in ("fill", "active", "flush", "done", "read_miss1", "read_miss2",
+                                                "read_miss3", "cold_miss")}
+        span = h.stat("profile_span_cycles")
+        assert st["active"] > 0 and st["fill"] > 0 and st["flush"] > 0 and st["read_miss2"] > 0, (kernel, st)
+        assert st["read_miss1"] == 0 and st["read_miss3"] == 0 and st["cold_miss"] == n, (kernel, st)
+        phases = st["fill"] + st["active"] + st["flush"] + st["done"]
+        assert 0.9 * span <= phases <= 1.01 * span, (kernel, st, span)
+        # the launch's span fits inside the event-timed kernel (a few us of launch overhead around it)
+        assert span <= h.stat("kernel_ns") * h.stat("clock_khz") / 1e6 * 1.05, (kernel, span)
+        assert h.stat("no_valid_but_ready") + h.stat("no_ready_but_valid") > 0, kernel
+        assert h.stat("issue_window") > 0 and h.stat("capacity_stalls") == 0 and h.stat("cms") == 0
+        h.set_option("profile", 0)
+    # a kernel without stamps leaves the last profiled launch's statistics in place
+    h.set_option("profile", 1)
+    h.set_kernel("sell")
+    h.exec(x, beta=0, mode=hs.MODE_ORDERED)
+    assert h.stat("profiled") == 1 and h.stat("issue_window") == 0
+    h.close()
+
+
+def test_plugin_surface_spmvbench_profile(gpu):
+    """spmvbench --profile 1: the CSV carries HardwareSpMVNewCache::statKeys under the reference's names and
+    order, with the state counts measured (vcache kernels)"""
+    import subprocess
+    names = ["circuit204", "row64k"]
+    out = subprocess.run([f"{hs.LIB_DIR}/spmvbench", "--dir", fx.MATRICES, "--confs", "hip", "--cms", "0",
+                          "--kernel", "vcache", "--mode", "ordered", "--profile", "1", *names],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = out.stdout.splitlines()
+    keys = next(l for l in lines if l.startswith("diffFromGolden,")).rstrip(",").split(",")
+    pos = [keys.index(k) for k in REF_NEWCACHE_KEYS]
+    assert pos == sorted(pos), "NewCache keys out of the reference's order"
+    recs = [dict(zip(keys, l.rstrip(",").split(","))) for l in lines if l[:1].isdigit()]
+    assert len(recs) == len(names)
+    for r in recs:
+        assert r["diffFromGolden"] == "0" and r["error"] == "0", r
+        assert int(r["sActive"]) > 0 and int(r["sFill"]) > 0 and int(r["sFlush"]) > 0, r
+        assert int(r["issueWindow"]) > 0 and r["capacityStalls"] == "0" and r["cms"] == "0", r
+
+
 def test_auto_fast_long_row_takes_sell(gpu):
     """AUTO FAST: a row that would outlast the rest in csr_vector (one wave per long row) goes to
     sell's hub pieces; deterministic and within the FAST bound of the oracle."""
