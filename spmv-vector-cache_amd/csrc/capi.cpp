@@ -105,6 +105,13 @@ struct hipspmv_handle {
   // one launch's blocks are all resident at once (2 per CU), so they walk
   // the x windows together and the gathered window stays in L2
   uint32_t wgather_chunk = kWgChunk;
+  // option "vcache_nt": row blocks b >= vcache_nt load their entries
+  // non-temporally; -1 default: every block for the split
+  // geometry, the second half of the blocks for the ordered one
+  int64_t vcache_nt = -1;
+  // option "sell_nt": SELL slices s >= sell_nt load their entries
+  // non-temporally (-1 default: the second half of the slices)
+  int64_t sell_nt = -1;
   void *d_x = nullptr, *d_y = nullptr;
   int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
   // setup_ns: create (transpose, validation, uploads, every layout AUTO uses);
@@ -294,12 +301,19 @@ static int build_vc_layout(hipspmv_t* h, int k, const HostCSR& a) {
 // could not be built falls back to the generic kernel of the mode: csr_lane
 // (ORDERED) or csr_vector (FAST), which need nothing beyond the CSR copy.
 static int auto_pick(const hipspmv_t* h, bool fast_ok, bool built) {
-  auto worth = [&](const hipspmv_handle::Vc& v) {
-    return v.ok && v.max_run <= kVcRunMax &&
+  // each x element a work unit streams feeds enough nonzeros (geometry only:
+  // the ordered layout's entries are built once AUTO wants them)
+  auto worth = [&](const hipspmv_handle::Vc& v, bool eligible) {
+    return eligible && v.max_run <= kVcRunMax &&
            (uint64_t)h->nnz * 16 * v.split >= (uint64_t)v.nblocks * v.split * h->cols;
   };
   const int generic = fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : HIPSPMV_KERNEL_CSR_LANE;
-  if (fast_ok && worth(h->vc[1])) return HIPSPMV_KERNEL_VCACHE_SPLIT;
+  if (fast_ok && worth(h->vc[1], h->vc[1].ok)) return HIPSPMV_KERNEL_VCACHE_SPLIT;
+  // ORDERED: the ordered vector cache with half its row blocks' entries
+  // non-temporal (C3: 181 us against sell's 185 with the same policy, 199 as
+  // round 2 ran it)
+  if (!fast_ok && worth(h->vc[0], h->vc0_eligible))
+    return !built || h->vc[0].ok ? HIPSPMV_KERNEL_VCACHE : h->sell.built ? HIPSPMV_KERNEL_SELL : generic;
   if (!h->vc0_eligible && h->wg_eligible && h->wg_max_run <= kVcRunMax)
     return !built || h->vc[3].ok ? HIPSPMV_KERNEL_WGATHER : generic;
   if (!fast_ok) return !built || h->sell.built ? HIPSPMV_KERNEL_SELL : generic;
@@ -361,6 +375,7 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
     const int k = auto_pick(h, fast_ok, false);
     if (k == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
     else if (k == HIPSPMV_KERNEL_WGATHER) st = build_vc_layout(h, 3, a);
+    else if (k == HIPSPMV_KERNEL_VCACHE) st = build_vc_layout(h, 0, a);
     else st = HIPSPMV_OK;
     if (st == HIPSPMV_ERR_OOM) {
       h->auto_fallback++;
@@ -492,6 +507,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                q.d_hubs,    h->d_rowptr, h->d_colind, h->d_vals, d_x,    d_y_in,
                d_y_out,     q.nslices,   q.nhubs,     beta,    mode == HIPSPMV_MODE_ORDERED ? 1 : 0,
                q.d_pieces,  q.npieces,   q.d_partial, q.d_tickets};
+    a.nt_from = h->sell_nt >= 0 ? (uint32_t)std::min<int64_t>(h->sell_nt, UINT32_MAX) : q.nslices / 2;
     e = launch_sell(h->dtype, a, s);
   } else if (kernel == HIPSPMV_KERNEL_VCACHE || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ||
       kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
@@ -502,6 +518,8 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                  v.d_tickets, h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
                  v.npad,      h->nnz - 1, v.split,   beta, h->vcache_dma, (uint32_t)geoms[k].panel,
                  h->vcache_xlane, v.max_seg, h->vcache_map};
+    a.nt_from = h->vcache_nt >= 0 ? (uint32_t)std::min<int64_t>(h->vcache_nt, UINT32_MAX)
+                : k == 1 ? 0u : k == 0 ? v.nblocks / 2 : ~0u;
     h->prof_pending = false;
     if (h->profile && k < 2) {  // the default configuration with its profile stamps
       if (k == 0 && !h->d_prof) {
@@ -525,6 +543,8 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                  v.npad,      h->nnz - 1, 1,         beta, 0,       (uint32_t)kWgWindow.panel,
                  h->vcache_xlane, v.max_seg};
     a.chunk = h->wgather_chunk;
+    // entries non-temporal unless option vcache_nt > 0 (full C4: 3391 us against 3594)
+    a.nt_from = h->vcache_nt > 0 ? ~0u : 0u;
     e = launch_wgather(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
@@ -640,6 +660,12 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "wgather_chunk") {  // row blocks per k_wgather launch (0: all in one launch)
     if (value < 0 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->wgather_chunk = (uint32_t)value;
+  } else if (k == "sell_nt") {  // first SELL slice whose entries load non-temporally (-1: half)
+    if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
+    h->sell_nt = value;
+  } else if (k == "vcache_nt") {  // first row block whose entries load non-temporally (-1: per geometry)
+    if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
+    h->vcache_nt = value;
   } else if (k == "vcache_xlane") {
     if (value < -1 || value > 3) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_xlane = (int)value;

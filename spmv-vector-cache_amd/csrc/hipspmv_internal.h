@@ -79,6 +79,9 @@ constexpr uint32_t kSellNoRow = 0xFFFFFFFFu;
 // row, first entry (within the row), entries, piece index, pieces of the row,
 // ticket index, 0, 0.
 constexpr uint32_t kSellPiece = 4096;
+// ORDERED f64: a hub row's chain holds kChainG consecutive entries per lane per
+// stage of 64 * kChainG (csrc/sell.hip hub_row_exact; tools/sell_sim.cpp).
+constexpr int kChainG = 8;
 constexpr int kSellPieceWords = 8;
 
 // Column part h of a geometry with `split` parts owns panels

@@ -24,6 +24,7 @@ struct VcacheArgs {
   uint32_t max_seg = 0;  // longest segment of the layout (xlane needs it in the register window)
   int map = 0;           // split 4: XCD-aware unit placement (experimental, option "vcache_map")
   uint32_t chunk = 0;    // k_wgather: row blocks per launch (0: one launch)
+  uint32_t nt_from = ~0u;  // k_vcache: row blocks b >= nt_from load their entries non-temporally
 };
 
 struct CsrArgs {
@@ -59,6 +60,7 @@ struct SellArgs {
   uint32_t npieces = 0;
   void* partial = nullptr;      // [npieces] piece partials
   uint32_t* tickets = nullptr;  // per split row, zero between launches
+  uint32_t nt_from = 0;         // slices s >= nt_from load their entries non-temporally
 };
 
 hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);

@@ -132,12 +132,87 @@ __device__ __forceinline__ T hub_entries(const SellArgs& a, uint32_t base, uint3
   return s;
 }
 
-// ORDERED f64: hub row r in one wave, one chain from y_in (or +0.0).
+// v rotated one lane up the wave: lane l receives lane l-1's value, lane 0
+// lane 63's (DPP wave_ror:1, two 32-bit moves)
 template <typename T>
-__device__ __forceinline__ void hub_row_exact(const SellArgs& a, uint32_t r, int lane) {
-  const uint32_t base = a.rowptr[r], n = a.rowptr[r + 1] - base;
-  const T acc0 = a.beta ? static_cast<const T*>(a.y_in)[r] : T(0);
-  const T acc = hub_entries<T, true>(a, base, n, acc0, lane);
+__device__ __forceinline__ T wave_ror1(T v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, 0x13C, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), 0x13C, 0xF, 0xF, false);
+  return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+}
+
+// ORDERED f64: hub row r in one wave, one chain from y_in (or +0.0) --
+// SoftwareSpMV's own sequence of rounded adds, so it cannot be split; what
+// can be made short is each link.  A stage holds 64 * kChainG consecutive
+// entries, lane l the kChainG entries l*kChainG.. in its registers, their
+// products formed by every lane at once (invalid ones -0.0, which leaves
+// every sum unchanged).  The chain then visits the lanes in order: every
+// lane adds its products to `acc`, and a wave rotation hands the sum of
+// lane l to lane l+1 (lane 63's to lane 0, for the next stage), so only
+// lane l's sum is the chain's at step l.  Per entry one dependent add plus a
+// share of the rotation: chain_probe measured a register-fed add chain at
+// 4.3 cycles per add, and the v_readlane chain this replaces at 20.6.
+// Entries two stages ahead and gathers one stage ahead stay in flight.
+template <typename T>
+__device__ __forceinline__ void hub_row_exact(const SellArgs& a, uint32_t w, int lane) {
+#pragma clang fp contract(off)
+  constexpr int G = kChainG;
+  constexpr uint32_t S = 64 * G;
+  const T* __restrict__ vals = static_cast<const T*>(a.csr_vals);
+  const T* __restrict__ x = static_cast<const T*>(a.x);
+  const uint32_t r = a.hubs[w], base = a.rowptr[r], n = a.rowptr[r + 1] - base;
+  // the chain is latency-bound: the longest hub rows (w: longest first) get
+  // first call on their SIMD's issue slots, over shorter chains and slices
+  if (w < 4)
+    __builtin_amdgcn_s_setprio(3);
+  else if (w < 64)
+    __builtin_amdgcn_s_setprio(2);
+  else
+    __builtin_amdgcn_s_setprio(1);
+  auto load = [&](uint32_t g0, uint32_t* c, T* v) {  // clamped: the copies past the row are never added
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const uint32_t e = min(g0 + (uint32_t)lane * G + j, n - 1);
+      c[j] = nt(a.colind + base + e);
+      v[j] = nt(vals + base + e);
+    }
+  };
+  auto products = [&](uint32_t g0, const T* v, const T* xs, T* p) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) p[j] = g0 + (uint32_t)lane * G + j < n ? v[j] * xs[j] : T(-0.0);
+  };
+  uint32_t cA[G], cB[G];
+  T vA[G], vB[G], xs[G], p[G];
+  load(0, cA, vA);
+#pragma unroll
+  for (int j = 0; j < G; ++j) xs[j] = x[cA[j]];
+  products(0, vA, xs, p);
+  load(S, cA, vA);
+  T acc = a.beta ? static_cast<const T*>(a.y_in)[r] : T(0);  // lane 0's is the chain's
+  for (uint32_t g0 = 0; g0 < n; g0 += S) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) xs[j] = x[cA[j]];  // next stage's gathers
+    load(g0 + 2 * S, cB, vB);                      // and the entries of the one after
+    // the chain touches no memory: keep the scheduler from moving the loads'
+    // consumers (and their waits) into it
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int l = 0; l < 64; ++l) {
+      T s = acc;
+#pragma unroll
+      for (int j = 0; j < G; ++j) s = s + p[j];
+      acc = wave_ror1(s);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    products(g0 + S, vA, xs, p);  // waits for the gathers only (the entry loads are younger)
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      cA[j] = cB[j];
+      vA[j] = vB[j];
+    }
+  }
   if (lane == 0) static_cast<T*>(a.y_out)[r] = acc;
 }
 
@@ -171,8 +246,10 @@ __device__ __forceinline__ void hub_piece(const SellArgs& a, uint32_t pid, int l
   y[r] = a.beta ? static_cast<const T*>(a.y_in)[r] + t : t;
 }
 
-// One slice s: lane `lane` sums rows row[s][j*64 + lane], j = 0..3.
-template <typename T>
+// One slice s: lane `lane` sums rows row[s][j*64 + lane], j = 0..3.  NTL:
+// the slice's entries load non-temporally (the slices s >= nt_from), so the
+// others and x stay in L2 / the Infinity Cache.
+template <typename T, bool NTL>
 __device__ __forceinline__ void slice_rows(const SellArgs& a, uint32_t s, int lane) {
 #pragma clang fp contract(off)
   const T* __restrict__ x = static_cast<const T*>(a.x);
@@ -189,6 +266,12 @@ __device__ __forceinline__ void slice_rows(const SellArgs& a, uint32_t s, int la
   }
   const uint32_t* __restrict__ c = a.col + off + lane;
   const T* __restrict__ v = static_cast<const T*>(a.vals) + off + lane;
+  auto ld = [](const auto* p) {
+    if constexpr (NTL)
+      return nt(p);
+    else
+      return *p;
+  };
   // Software pipeline over pairs of steps (8 entries per lane), two register
   // buffers A/B: gathers of one pair are issued, then the entries of the
   // pair after it, then the products wait for the gathers only (vmcnt counts
@@ -198,8 +281,8 @@ __device__ __forceinline__ void slice_rows(const SellArgs& a, uint32_t s, int la
     const size_t i0 = (size_t)k0 * 4 * 64;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      cc[q] = nt(c + i0 + q * 64);
-      vv[q] = nt(v + i0 + q * 64);
+      cc[q] = ld(c + i0 + q * 64);
+      vv[q] = ld(v + i0 + q * 64);
     }
     // compiler-only barriers (emit nothing): without a possible memory write
     // after these loads, InstCombine folds a loop-carried load into one load
@@ -243,7 +326,7 @@ __device__ __forceinline__ void slice_rows(const SellArgs& a, uint32_t s, int la
     const size_t i0 = (size_t)k * 4 * 64;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const T t = madd(acc[j], nt(v + i0 + j * 64), x[nt(c + i0 + j * 64)]);
+      const T t = madd(acc[j], ld(v + i0 + j * 64), x[ld(c + i0 + j * 64)]);
       acc[j] = k < n[j] ? t : acc[j];
     }
   }
@@ -261,13 +344,18 @@ __global__ __launch_bounds__(256) void k_sell(const SellArgs a) {
   const uint32_t H = EXACT ? a.nhubs : a.npieces;
   if (w < H) {
     if (EXACT)
-      hub_row_exact<T>(a, a.hubs[w], lane);
+      hub_row_exact<T>(a, w, lane);
     else
       hub_piece<T>(a, w, lane);
     return;
   }
   const uint32_t s = w - H;
-  if (s < a.nslices) slice_rows<T>(a, s, lane);
+  if (s < a.nslices) {
+    if (s >= a.nt_from)
+      slice_rows<T, true>(a, s, lane);
+    else
+      slice_rows<T, false>(a, s, lane);
+  }
 }
 
 template <typename T, bool EXACT>

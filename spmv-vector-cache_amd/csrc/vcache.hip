@@ -25,6 +25,8 @@
 // next x panel over.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "device_common.h"
 #include "vc_map.h"
 #include "hipspmv_internal.h"
@@ -63,6 +65,9 @@ struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane
 // s_memrealtime (100 MHz) at start, main-loop start, main-loop end, exit; the
 // combine ticket; s_memtime cycles summed over the steps: loader wave 0 working,
 // loader wave 0 waiting at the step barrier, first compute wave waiting there.
+// 256 / 512 / 1024 / 2048 / 4096: the entries of row blocks b >= nblocks/2,
+// 5/8, 3/8, 1/4, 1/8 loaded
+// non-temporally (Infinity-Cache residency experiment).
 template <typename T, int SPLIT, int WL = VcCfg<SPLIT>::WL, int DE = VcCfg<SPLIT>::DE, int EPT = VcCfg<SPLIT>::EPT,
           int AB = 0, int MAP = 0, bool NT = false, int LD = 0, int CX = 0>
 __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restrict__ seg,
@@ -72,7 +77,8 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
                                                         T* __restrict__ partial, uint32_t* __restrict__ tickets,
                                                         uint32_t rows, uint32_t cols, uint32_t rows_per_block,
                                                         uint32_t nblocks, uint32_t npanels, uint32_t part_panels,
-                                                        uint32_t npad, uint32_t last, int beta) {
+                                                        uint32_t npad, uint32_t last, int beta,
+                                                        uint32_t nt_from) {
 #pragma clang fp contract(off)
   constexpr int VR = VcCfg<SPLIT>::VR, VP = VcCfg<SPLIT>::VP;
   constexpr int VT = kVcThreads, NW = VT / 64, WC = NW - WL;
@@ -169,7 +175,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   // continuation entries (MORE) are read back from memory (rare: several
   // entries of one row inside one panel).
   const int ct = t - LT;
-  auto load_e = [&](uint32_t s, uint32_t* c, T* v) {
+  auto load_e = [&](uint32_t s, uint32_t* c, T* v, auto ntc) {
     if (AB & 4) {
 #pragma unroll
       for (int j = 0; j < EPT; ++j) c[j] = kVcCont;
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       if (CX == 2) {
         c[j] = ald_u32(ecode + i);
         v[j] = ald_64(evals + i);
-      } else if (NT) {  // streamed once: non-temporal, so the entries do not evict x from L2
+      } else if (NT || decltype(ntc)::value) {  // non-temporal: kept out of the Infinity Cache
         c[j] = __builtin_nontemporal_load(ecode + i);
         v[j] = __builtin_nontemporal_load(evals + i);
       } else {
@@ -378,28 +384,43 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       }
     }
   } else {
-    uint32_t EC[DE][EPT];
-    T EV[DE][EPT];
+    // the entry role; ntc: this unit's entries loaded non-temporally -- the
+    // row blocks b >= nt_from (the AB bits 256-4096 fix the threshold instead):
+    // nt entry lines leave L2 and the Infinity Cache to x and to the blocks
+    // below the threshold, whose entries then stay resident across launches
+    // 
+    auto entries = [&](auto ntc) {
+      uint32_t EC[DE][EPT];
+      T EV[DE][EPT];
 #pragma unroll
-    for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i]);
-    barrier();
-    if (AB & 128) pf_mark = __builtin_amdgcn_s_memtime();
-    for (uint32_t base = 0; base < nsteps; base += DE) {
+      for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i], ntc);
+      barrier();
+      if (AB & 128) pf_mark = __builtin_amdgcn_s_memtime();
+      for (uint32_t base = 0; base < nsteps; base += DE) {
 #pragma unroll
-      for (int i = 0; i < DE; ++i) {
-        const uint32_t s = base + i;
-        if (!PAD && s >= npu) break;
-        if (CX == 2) vm_wait<(AB & 4) ? 0 : (DE - 1) * 2 * EPT>();  // slot i landed, DE-1 steps still in flight
-        if (CX) {
-          if (!PAD || s < npu) apply_cx(s, EC[i], EV[i]);
-        } else {
-          apply(s, EC[i], EV[i]);
+        for (int i = 0; i < DE; ++i) {
+          const uint32_t s = base + i;
+          if (!PAD && s >= npu) break;
+          if (CX == 2) vm_wait<(AB & 4) ? 0 : (DE - 1) * 2 * EPT>();  // slot i landed, DE-1 steps still in flight
+          if (CX) {
+            if (!PAD || s < npu) apply_cx(s, EC[i], EV[i]);
+          } else {
+            apply(s, EC[i], EV[i]);
+          }
+          load_e(s + DE, EC[i], EV[i], ntc);
+          pbarrier();
         }
-        load_e(s + DE, EC[i], EV[i]);
-        pbarrier();
       }
-    }
-    if (CX == 2) vm_wait<0>();  // the clamped prefetches past the last panel
+      if (CX == 2) vm_wait<0>();  // the clamped prefetches past the last panel
+    };
+    constexpr int NTAB = AB & (256 | 512 | 1024 | 2048 | 4096);
+    const uint32_t thr = NTAB == 0 ? nt_from
+                       : (AB & 512) ? nblocks * 5 / 8 : (AB & 1024) ? nblocks * 3 / 8
+                       : (AB & 2048) ? nblocks / 4 : (AB & 4096) ? nblocks / 8 : nblocks / 2;
+    if (NT || b >= thr)
+      entries(std::true_type{});
+    else
+      entries(std::false_type{});
   }
   if (AB & 128) {
     if (t == 0) {
@@ -545,7 +566,7 @@ static void launch_one(const VcacheArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((k_vcache<T, SPLIT, VcCfg<SPLIT>::WL, VcCfg<SPLIT>::DE, VcCfg<SPLIT>::EPT, 0, MAP, false, LD, CX>),
                      dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s, a.seg, a.code, (const T*)a.vals,
                      (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets, a.rows, a.cols,
-                     a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta);
+                     a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta, a.nt_from);
 }
 
 template <typename T, int SPLIT, int MAP = 0>
@@ -622,17 +643,17 @@ static hipError_t launch_vcache_profiled_t(const VcacheArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((k_vcache<T, 1, VcCfg<1>::WL, VcCfg<1>::DE, VcCfg<1>::EPT, P>), grid, block, 0, s, a.seg,
                        a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial,
                        a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad,
-                       a.last, a.beta);
+                       a.last, a.beta, a.nt_from);
   } else if (a.max_seg <= (uint32_t)((kVcThreads / 64 - VcCfg<3>::WL) * 64 * VcCfg<3>::EPT)) {
     hipLaunchKernelGGL((k_vcache<T, 3, VcCfg<3>::WL, VcCfg<3>::DE, VcCfg<3>::EPT, P, 0, false, 1, 3>), grid, block, 0,
                        s, a.seg, a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out,
                        (T*)a.partial, a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels,
-                       a.part_panels, a.npad, a.last, a.beta);
+                       a.part_panels, a.npad, a.last, a.beta, a.nt_from);
   } else {
     hipLaunchKernelGGL((k_vcache<T, 3, VcCfg<3>::WL, VcCfg<3>::DE, VcCfg<3>::EPT, P, 0, false, 1, 0>), grid, block, 0,
                        s, a.seg, a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out,
                        (T*)a.partial, a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels,
-                       a.part_panels, a.npad, a.last, a.beta);
+                       a.part_panels, a.npad, a.last, a.beta, a.nt_from);
   }
   return hipGetLastError();
 }

@@ -22,7 +22,7 @@
 
 namespace hipspmv {
 
-template <typename T, int CB, int DE, int EPT>
+template <typename T, int CB, int DE, int EPT, bool NTE = false>
 __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restrict__ seg,
                                                          const uint32_t* __restrict__ ecode,
                                                          const T* __restrict__ evals, const T* __restrict__ x,
@@ -50,8 +50,13 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const uint32_t i = min(beg + t + j * VT, last);  // clamped, validity checked at use
-      c[j] = ecode[i];
-      v[j] = evals[i];
+      if (NTE) {  // streamed once: non-temporal, so the gathered x window keeps L2
+        c[j] = __builtin_nontemporal_load(ecode + i);
+        v[j] = __builtin_nontemporal_load(evals + i);
+      } else {
+        c[j] = ecode[i];
+        v[j] = evals[i];
+      }
     }
   };
   auto run = [&](uint32_t i, uint32_t code, T v, T xv, const T* xs) {
@@ -249,6 +254,10 @@ static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
                          a.npanels, a.npad, a.last, a.beta, b0);
     else if (a.xlane >= 2 && a.max_seg <= 4u * kVcThreads)
       hipLaunchKernelGGL((k_wgather_pipe<T, 17, 4, 4>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
+                         (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
+                         a.npanels, a.npad, a.last, a.beta, b0);
+    else if (a.nt_from == 0)
+      hipLaunchKernelGGL((k_wgather<T, 17, 4, 2, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
                          (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
                          a.npanels, a.npad, a.last, a.beta, b0);
     else

@@ -92,6 +92,36 @@ __global__ __launch_bounds__(64) void k_lds(const double* __restrict__ in, doubl
   if (threadIdx.x == 0) *cyc = t1 - t0;
 }
 
+// dpp: k_sell's ORDERED hub chain (csrc/sell.hip hub_row_exact): 8 products
+// per lane, 64 steps of 8 dependent adds then a DPP wave rotation handing the
+// sum to the next lane
+__device__ __forceinline__ double ror1(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, 0x13C, 0xF, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x13C, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__global__ __launch_bounds__(64) void k_dpp(const double* __restrict__ in, double* out, unsigned long long* cyc) {
+#pragma clang fp contract(off)
+  double p[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) p[j] = in[threadIdx.x * 8 + j];
+  double acc = 0.0;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < kN / 512; ++it) {
+#pragma unroll
+    for (int l = 0; l < 64; ++l) {
+      double s = acc;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s = s + p[j];
+      acc = ror1(s);
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[threadIdx.x] = acc;
+  if (threadIdx.x == 0) *cyc = t1 - t0;
+}
+
 template <typename K>
 static void run(const char* nm, K kern, const double* din, double* dout, unsigned long long* dcyc) {
   unsigned long long best = ~0ull;
@@ -120,5 +150,6 @@ int main() {
   run("reg", k_reg, din, dout, dcyc);
   run("readlane", k_readlane, din, dout, dcyc);
   run("lds", k_lds, din, dout, dcyc);
+  run("dpp8", k_dpp, din, dout, dcyc);
   return 0;
 }

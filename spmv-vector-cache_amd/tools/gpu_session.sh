@@ -43,6 +43,9 @@ for s in $STEPS; do
     benchtime) step bench_time 900 bash -c 'time python bench.py' ;;
     mallpol) step mall_policy 300 ./spmv-vector-cache_amd/lib/pf_probe 88 mall ;;
     sweepc4c) step sweep_c4_chunks 900 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 24 --log2-cols 24 --only "wgather c" --rounds 2 --reps 10 ;;
+    selltests) step pytest_sell 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "sell or rmat or hub or fullsize" ;;
+    sweepc4nt) step sweep_c4_nt 900 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 24 --log2-cols 24 --only "=wgather,=wgather nt" --rounds 2 --reps 10 ;;
+    sweepnt) step sweep_nt 900 python spmv-vector-cache_amd/tools/kernel_sweep.py --only "vcache,sell,split" ;;
     newtests) step pytest_new 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "profile or spmvbench or cache_behaviour" ;;
     sweep) step sweep 600 python spmv-vector-cache_amd/tools/kernel_sweep.py ;;
     sweepx) HIPSPMV_EXPERIMENTAL=1 step sweep_exp 900 python spmv-vector-cache_amd/tools/kernel_sweep.py ;;

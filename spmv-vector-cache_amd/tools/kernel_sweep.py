@@ -41,7 +41,19 @@ cands = [("vcache", "vcache", O, {}), ("csr_lane", "csr_lane", O, {}), ("vcache_
          ("wgather c512", "wgather", O, {"wgather_chunk": 512}), ("wgather c0", "wgather", O, {"wgather_chunk": 0}),
          ("wgather c192", "wgather", O, {"wgather_chunk": 192}), ("wgather c320", "wgather", O, {"wgather_chunk": 320}),
          ("wgather c384", "wgather", O, {"wgather_chunk": 384}),
-         ("wgather xl2", "wgather", O, {"vcache_xlane": 2})]
+         ("wgather xl2", "wgather", O, {"vcache_xlane": 2}),
+         # non-temporal entry loads from a fraction of the row blocks / slices on
+         ("vcache nt all", "vcache", O, {"vcache_nt": 0}), ("vcache nt none", "vcache", O, {"vcache_nt": 1 << 30}),
+         ("vcache nt 1/2", "vcache", O, {"vcache_nt": ("vcache_blocks", 0.5)}),
+         ("vcache nt 1/4", "vcache", O, {"vcache_nt": ("vcache_blocks", 0.25)}),
+         ("split nt none", "vcache_split", F, {"vcache_nt": 1 << 30}),
+         ("split nt 1/4", "vcache_split", F, {"vcache_nt": ("vcache_split_units", 0.25 / 3)}),
+         ("sell nt none", "sell", O, {"sell_nt": 1 << 30}),
+         ("sell nt 3/8", "sell", O, {"sell_nt": ("sell_slices", 0.375)}),
+         ("sell nt 1/2", "sell", O, {"sell_nt": ("sell_slices", 0.5)}),
+         ("sell nt 5/8", "sell", O, {"sell_nt": ("sell_slices", 0.625)}),
+         ("sell fast nt 1/2", "sell", F, {"sell_nt": ("sell_slices", 0.5)}),
+         ("wgather nt", "wgather", O, {"vcache_nt": 0}), ("wgather no nt", "wgather", O, {"vcache_nt": 1 << 30})]
 if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
     cands += [("vcache xl1", "vcache", O, {"vcache_xlane": 1}), ("vcache xl2", "vcache", O, {"vcache_xlane": 2}),
               ("vcache dma", "vcache", O, {"vcache_dma": 1}),
@@ -59,15 +71,21 @@ if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
               ("split4 map xl2", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 2})]
 if a.only:
     keep = a.only.split(",")
-    cands = [c for c in cands if any(k in c[0] for k in keep) or c[0] == "vcache"]
+    # "=label" keeps that label only; anything else keeps the labels containing it
+    cands = [c for c in cands
+             if any((c[0] == k[1:]) if k.startswith("=") else (k in c[0]) for k in keep) or c[0] == "vcache"]
 ref = None
 res, check = {}, {}
 for rnd in range(a.rounds):  # interleaved rounds in one process (methodology rule 24)
     for label, kname, mode, opts in cands:
         try:
             h.set_kernel(kname)
-            for k in ("vcache_dma", "vcache_xlane", "vcache_map", "wgather_chunk"):
-                h.set_option(k, opts.get(k, {"vcache_xlane": -1, "vcache_dma": -1, "wgather_chunk": 256}.get(k, 0)))
+            for k in ("vcache_dma", "vcache_xlane", "vcache_map", "wgather_chunk", "vcache_nt", "sell_nt"):
+                v = opts.get(k, {"vcache_xlane": -1, "vcache_dma": -1, "wgather_chunk": 256, "vcache_nt": -1,
+                                 "sell_nt": -1}.get(k, 0))
+                if isinstance(v, tuple):  # (statistic, fraction): a threshold relative to the layout
+                    v = int(h.stat(v[0]) * v[1])
+                h.set_option(k, v)
             h.exec_device(x, y, beta=0, mode=mode, stream=s)
         except hs.HipSpMVError:
             continue

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "hipspmv_internal.h"
@@ -42,6 +43,14 @@ static T bits(uint64_t u) {
   return t;
 }
 
+template <typename T>
+static T neg_zero() {
+  if constexpr (std::is_floating_point_v<T>)
+    return -0.0;
+  else
+    return T(0);  // u64 never takes the chain (integer sums are order-free)
+}
+
 // The kernel's arithmetic for one element type.  mode: 0 FAST, 1 EXACT (hub chain).
 template <typename T>
 static std::vector<T> replay(const HostCSR& a, const SellLayout& L, const std::vector<T>& x,
@@ -52,6 +61,34 @@ static std::vector<T> replay(const HostCSR& a, const SellLayout& L, const std::v
   // the hub-entry routine (hub_entries): EXACT chain from acc, or lane
   // partials + xor tree; loads at the kernel's clamped indices
   auto hub_entries = [&](uint32_t base, uint32_t n, T acc, bool chain) -> T {
+    if (chain) {  // hub_row_exact: stages of 64 * kChainG, lane l holds entries l*G .. l*G+G-1
+      constexpr uint32_t G = kChainG, S = 64 * G;
+      auto entry = [&](uint32_t g0, int lane, uint32_t j, uint32_t& c, T& v) {
+        const uint32_t e = std::min<uint32_t>(g0 + (uint32_t)lane * G + j, n - 1);
+        c = at(a.colind, (uint64_t)base + e, "hub colind");
+        v = bits<T>(at(a.vals, (uint64_t)base + e, "hub vals"));
+      };
+      for (uint32_t g0 = 0; g0 < n; g0 += S) {
+        for (int lane = 0; lane < 64; ++lane)
+          for (uint32_t j = 0; j < G; ++j) {  // prefetches: entries two stages ahead, gathers one ahead
+            uint32_t c;
+            T v;
+            entry(g0 + 2 * S, lane, j, c, v);
+            entry(g0 + S, lane, j, c, v);
+            (void)xv(c);
+          }
+        // the chain visits the lanes in order; an invalid product is -0.0
+        for (int lane = 0; lane < 64; ++lane)
+          for (uint32_t j = 0; j < G; ++j) {
+            uint32_t c;
+            T v;
+            entry(g0, lane, j, c, v);
+            const T p = g0 + (uint32_t)lane * G + j < n ? v * xv(c) : neg_zero<T>();
+            acc = acc + p;
+          }
+      }
+      return acc;
+    }
     const uint32_t S = 256;
     auto entry = [&](uint32_t g0, int j, int lane, uint32_t& c, T& v) {
       const uint32_t e = std::min<uint32_t>(g0 + j * 64 + lane, n - 1);

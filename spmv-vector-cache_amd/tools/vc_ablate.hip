@@ -97,7 +97,7 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(kern, dim3(A.nblocks * A.split), dim3(kVcThreads), 0, nullptr, A.seg, A.code,
                            (const double*)A.vals, (const double*)A.x, (const double*)A.y_in, (double*)A.y_out,
                            (double*)A.partial, A.tickets, A.rows, A.cols, A.rows_per_block, A.nblocks, A.npanels,
-                           A.part_panels, A.npad, A.last, A.beta);
+                           A.part_panels, A.npad, A.last, A.beta, ~0u);
       });
       std::printf("  %-30s mask %2d %8.2f us  (alg %6.1f GB/s)", nm, mask, us, alg / us * 1e-3);
       if (mask == 0) {  // compare against the first (ordered) result
@@ -117,7 +117,7 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(kern, dim3(units), dim3(kVcThreads), 0, nullptr, A.seg, A.code, (const double*)A.vals,
                            (const double*)A.x, (const double*)A.y_in, (double*)A.y_out, (double*)A.partial,
                            A.tickets, A.rows, A.cols, A.rows_per_block, A.nblocks, A.npanels, A.part_panels, A.npad,
-                           A.last, A.beta);
+                           A.last, A.beta, ~0u);
       CK(hipDeviceSynchronize());
       std::vector<uint32_t> st(8 * units);
       const uint32_t* src = A.split == 1 ? reinterpret_cast<const uint32_t*>(A.partial) : A.tickets + 2 * A.nblocks;
@@ -181,12 +181,33 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 1, 2, 4, 3, 0, 0, false, 1>, 1, "DMA WL2 DE4 EPT3", 0);
       variant(k_vcache<double, 1, 1, 4, 3, 0, 0, false, 1>, 1, "DMA WL1 DE4 EPT3", 0);
       variant(k_vcache<double, 1, 2, 4, 2, 0, 0, false, 1>, 1, "DMA WL2 DE4 EPT2", 0);
+      variant(k_vcache<double, 1, 8, 4, 3, 256>, 1, "default, nt b >= nb/2", 0);
+      variant(k_vcache<double, 1, 8, 4, 3, 1024>, 1, "default, nt b >= 3nb/8", 0);
+      variant(k_vcache<double, 1, 8, 4, 3, 2048>, 1, "default, nt b >= nb/4", 0);
+      variant(k_vcache<double, 1, 8, 4, 3, 512>, 1, "default, nt b >= 5nb/8", 0);
+      variant(k_vcache<double, 1, 8, 4, 3, 0, 0, true>, 1, "default, all nt", 0);
+      variant(k_vcache<double, 1, 8, 4, 3, 256, 0, false, 0, 3>, 1, "xlane3, nt b >= nb/2", 0, 8 * 64 * 3);
+      variant(k_vcache<double, 1, 8, 4, 3, 1024, 0, false, 0, 3>, 1, "xlane3, nt b >= 3nb/8", 0, 8 * 64 * 3);
+      variant(k_vcache<double, 1, 8, 6, 3, 256, 0, false, 2, 2>, 1, "xlane2 DE6, nt b >= nb/2", 0, 8 * 64 * 3);
+      variant(k_vcache<double, 1, 8, 4, 3, 0, 0, true, 0, 3>, 1, "xlane3, all nt", 0, 8 * 64 * 3);
       variant(k_vcache<double, 1, 8, 4, 3, 3>, 1, "no x", 3);
       variant(k_vcache<double, 1, 8, 4, 3, 12>, 1, "no entries/compute", 12);
       variant(k_vcache<double, 1, 8, 4, 3, 15>, 1, "skeleton", 15);
     } else if (g.split == 3) {  // the product FAST geometry (round 2)
       variant(k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 3>, 3, "product (DMA WL3 DE4 EPT2, xlane3)", 0,
               13 * 64 * 2);
+      // Infinity-Cache residency: the entries of the row blocks past a threshold non-temporal
+      variant(k_vcache<double, 3, 3, 4, 2, 256, 0, false, 1, 3>, 3, "product, nt b >= nb/2", 0, 13 * 64 * 2);
+      variant(k_vcache<double, 3, 3, 4, 2, 512, 0, false, 1, 3>, 3, "product, nt b >= 5nb/8", 0, 13 * 64 * 2);
+      variant(k_vcache<double, 3, 3, 4, 2, 1024, 0, false, 1, 3>, 3, "product, nt b >= 3nb/8", 0, 13 * 64 * 2);
+      variant(k_vcache<double, 3, 3, 4, 2, 0, 0, true, 1, 3>, 3, "product, all entries nt", 0, 13 * 64 * 2);
+      variant(k_vcache<double, 3, 3, 4, 2, 2048, 0, false, 1, 3>, 3, "product, nt b >= nb/4", 0, 13 * 64 * 2);
+      variant(k_vcache<double, 3, 3, 4, 2, 4096, 0, false, 1, 3>, 3, "product, nt b >= nb/8", 0, 13 * 64 * 2);
+      variant(k_vcache<double, 3, 3, 4, 2, 0, 0, true, 1, 3>, 3, "product, all entries nt (again)", 0, 13 * 64 * 2);
+      variant(k_vcache<double, 3, 3, 4, 2, 64, 0, true, 1, 3>, 3, "all nt, without the combine", 64, 13 * 64 * 2);
+      variant(k_vcache<double, 3, 2, 4, 2, 0, 0, true, 1, 3>, 3, "all nt, DMA WL2", 0, 14 * 64 * 2);
+      variant(k_vcache<double, 3, 4, 4, 2, 0, 0, true, 1, 3>, 3, "all nt, DMA WL4", 0, 12 * 64 * 2);
+      variant(k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 3>, 3, "product (again)", 0, 13 * 64 * 2);
       variant(k_vcache<double, 3, 3, 4, 2, 64, 0, false, 1, 3>, 3, "product without the combine", 64,
               13 * 64 * 2);
       variant(k_vcache<double, 3, 2, 4, 2, 0, 0, false, 1, 3>, 3, "DMA WL2 DE4 EPT2, xlane3", 0, 14 * 64 * 2);

@@ -161,10 +161,14 @@ def test_synthetic_c3_full_size_ordered(gpu):
     x = hs.gen_vector(n, 3)
     y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=n)
     h = hs.Handle.from_csc(colptr, rowind, cvals, n, n)
-    assert h.kernel_name(hs.MODE_ORDERED) == "sell"  # AUTO's ordered kernel
+    assert h.kernel_name(hs.MODE_ORDERED) == "vcache"  # AUTO's ordered kernel on C3
     y = h.exec(x, beta=0, mode=hs.MODE_ORDERED)
     assert y.tobytes() == y_ref.tobytes()
-    h.set_kernel("vcache")
+    for nt in (0, 1 << 30):  # every / no row block's entries non-temporal: the same bits
+        h.set_option("vcache_nt", nt)
+        assert h.exec(x, beta=0, mode=hs.MODE_ORDERED).tobytes() == y_ref.tobytes()
+    h.set_option("vcache_nt", -1)
+    h.set_kernel("sell")
     assert h.exec(x, beta=0, mode=hs.MODE_ORDERED).tobytes() == y_ref.tobytes()
     h.set_kernel("auto")
     # the CSR entry point gives the same bits
@@ -669,19 +673,20 @@ def test_graph_capture_after_eager_launch_on_another_stream(gpu):
 
 
 def test_auto_layouts_built_at_create(gpu):
-    # AUTO's layouts (here ORDERED -> sell, FAST -> vcache_split) exist after create and count as
+    # AUTO's layouts (here ORDERED -> vcache, FAST -> vcache_split) exist after create and count as
     # setup; a kernel selected by name builds its layout then, timed in layout_ns and setup_ns
     n = 1 << 16
     rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
     h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
-    assert h.kernel_name(hs.MODE_ORDERED) == "sell" and h.kernel_name(hs.MODE_FAST) == "vcache_split"
-    assert h.stat("sell_slices") > 0 and h.stat("auto_fallback") == 0
+    assert h.kernel_name(hs.MODE_ORDERED) == "vcache" and h.kernel_name(hs.MODE_FAST) == "vcache_split"
+    assert h.stat("sell_slices") == 0 and h.stat("auto_fallback") == 0
     x = hs.gen_vector(n, 3)
     y_o = h.exec(x, beta=0, mode=hs.MODE_ORDERED)
     h.exec(x, beta=0, mode=hs.MODE_FAST)
     assert h.stat("layout_ns") == 0 and h.stat("setup_ns") == h.stat("create_ns") > 0
-    h.set_kernel("vcache")  # the ordered vcache layout: built now, from the device CSR copy
+    h.set_kernel("sell")  # the SELL layout: built now, from the device CSR copy
     assert h.stat("layout_ns") > 0 and h.stat("setup_ns") == h.stat("create_ns") + h.stat("layout_ns")
+    assert h.stat("sell_slices") > 0
     assert h.exec(x, beta=0, mode=hs.MODE_ORDERED).tobytes() == y_o.tobytes()
 
 
