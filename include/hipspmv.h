@@ -110,7 +110,12 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
  * L2 serves a quarter of x; experimental), "profile" (1 = VCACHE and
  * VCACHE_SPLIT launches run in their default configuration with in-kernel
  * stamps, and the NewCache state statistics below are measured; results are
- * bit-identical to the unprofiled kernel). */
+ * bit-identical to the unprofiled kernel), "vcache_nt" (row blocks b >=
+ * vcache_nt of VCACHE / VCACHE_SPLIT load their entries non-temporally; -1
+ * default: every block for VCACHE_SPLIT, the second half for VCACHE; WGATHER:
+ * 0 or -1 non-temporal, > 0 the default policy), "sell_nt" (SELL slices s >=
+ * sell_nt likewise; -1 default: the second half).  The cache policy never
+ * changes a result bit. */
 int hipspmv_set_option(hipspmv_t *h, const char *key, int64_t value);
 
 /* Replaces HardwareSpMV::exec()'s reset -> init -> regular -> write sequence

@@ -45,6 +45,8 @@ for s in $STEPS; do
     sweepc4c) step sweep_c4_chunks 900 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 24 --log2-cols 24 --only "wgather c" --rounds 2 --reps 10 ;;
     selltests) step pytest_sell 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "sell or rmat or hub or fullsize" ;;
     sweepc4nt) step sweep_c4_nt 900 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 24 --log2-cols 24 --only "=wgather,=wgather nt" --rounds 2 --reps 10 ;;
+    states) step profile_states 300 python -u spmv-vector-cache_amd/tools/profile_states.py ;;
+    wfast) step wfast_probe 900 python -u spmv-vector-cache_amd/tools/wfast_probe.py ;;
     sweepnt) step sweep_nt 900 python spmv-vector-cache_amd/tools/kernel_sweep.py --only "vcache,sell,split" ;;
     newtests) step pytest_new 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "profile or spmvbench or cache_behaviour" ;;
     sweep) step sweep 600 python spmv-vector-cache_amd/tools/kernel_sweep.py ;;

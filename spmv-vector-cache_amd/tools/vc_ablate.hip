@@ -190,6 +190,14 @@ int main(int argc, char** argv) {
       variant(k_vcache<double, 1, 8, 4, 3, 1024, 0, false, 0, 3>, 1, "xlane3, nt b >= 3nb/8", 0, 8 * 64 * 3);
       variant(k_vcache<double, 1, 8, 6, 3, 256, 0, false, 2, 2>, 1, "xlane2 DE6, nt b >= nb/2", 0, 8 * 64 * 3);
       variant(k_vcache<double, 1, 8, 4, 3, 0, 0, true, 0, 3>, 1, "xlane3, all nt", 0, 8 * 64 * 3);
+      // round 3: loader / compute balance with half the entries nt
+      variant(k_vcache<double, 1, 6, 4, 3, 256>, 1, "WL6, nt b >= nb/2", 0);
+      variant(k_vcache<double, 1, 10, 4, 3, 256>, 1, "WL10, nt b >= nb/2", 0);
+      variant(k_vcache<double, 1, 4, 4, 3, 256, 0, false, 1>, 1, "DMA WL4, nt b >= nb/2", 0);
+      variant(k_vcache<double, 1, 6, 4, 3, 256, 0, false, 1>, 1, "DMA WL6, nt b >= nb/2", 0);
+      variant(k_vcache<double, 1, 8, 6, 3, 256>, 1, "DE6, nt b >= nb/2", 0);
+      variant(k_vcache<double, 1, 8, 4, 3, 256 | 12>, 1, "nt b >= nb/2, x only", 12);
+      variant(k_vcache<double, 1, 8, 4, 3, 256 | 3>, 1, "nt b >= nb/2, no x", 3);
       variant(k_vcache<double, 1, 8, 4, 3, 3>, 1, "no x", 3);
       variant(k_vcache<double, 1, 8, 4, 3, 12>, 1, "no entries/compute", 12);
       variant(k_vcache<double, 1, 8, 4, 3, 15>, 1, "skeleton", 15);
