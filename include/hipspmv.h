@@ -73,6 +73,10 @@ extern "C" {
 #define HIPSPMV_KERNEL_WGATHER 6 /* y block in LDS, x gathered from global in
                                     2^17-column windows (wide x: C4/C5);
                                     ordered; experimental like VCACHE_SPLIT4 */
+#define HIPSPMV_KERNEL_WCSR 8 /* csr_vector over the rows cut at 2^16-column
+                                 windows (window-major), then each row's window
+                                 partials summed in window order; fast,
+                                 deterministic; wide x (C4/C5 shards) */
 #define HIPSPMV_KERNEL_SELL 7 /* SELL-C-sigma: one lane per row over slices of
                                  256 length-sorted rows, coalesced entries; rows
                                  over 256 entries one wave each; ordered in

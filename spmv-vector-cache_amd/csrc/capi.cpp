@@ -98,6 +98,14 @@ struct hipspmv_handle {
     uint32_t nslices = 0, nhubs = 0, npieces = 0;
     uint64_t padding = 0;
   } sell;
+  uint64_t wc_segments = 0;  // segments the wcsr layout would have (counted at create for wide x, else 0)
+  struct Wc {  // wcsr: the column-windowed segment matrix (built when AUTO picks it, else on first selection)
+    bool built = false;
+    uint32_t *d_rowptr = nullptr, *d_colind = nullptr, *d_groups = nullptr, *d_rowseg = nullptr,
+             *d_segidx = nullptr, *d_rgroups = nullptr;
+    uint64_t *d_vals = nullptr, *d_ypart = nullptr;
+    uint32_t nseg = 0, ngroups = 0, rgroups = 0, max_seg = 0, log2w = 0;
+  } wc;
   int vcache_dma = -1;   // option "vcache_dma": LDS-DMA x loader (-1 default: on for the split geometry)
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
   int vcache_map = 0;    // option "vcache_map": XCD-aware part placement, split 4 (experimental)
@@ -161,6 +169,12 @@ static void release(hipspmv_t* h) {
     void* sp[] = {q.d_off, q.d_width, q.d_row, q.d_len, q.d_col, q.d_hubs, q.d_vals, q.d_pieces, q.d_tickets,
                   q.d_partial};
     for (void* p : sp)
+      if (p) (void)hipFree(p);
+  }
+  {
+    auto& w = h->wc;
+    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_vals, w.d_ypart};
+    for (void* p : wp)
       if (p) (void)hipFree(p);
   }
   for (hipEvent_t e : h->ev)
@@ -277,6 +291,51 @@ static int build_sell_layout(hipspmv_t* h, const HostCSR& a) {
   return HIPSPMV_OK;
 }
 
+// The wcsr layout (column-windowed segment matrix) from the CSR `a`.
+static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
+  auto& w = h->wc;
+  if (w.built) return HIPSPMV_OK;
+  DeviceGuard g(h->device);
+  WinLayout L;
+  build_windowed(a, kWcLog2Window, L);
+  std::vector<uint32_t> groups;
+  build_row_groups(L.seg, groups);
+  const uint64_t bytes0 = h->device_bytes;
+  auto fail = [&](int st) {
+    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_vals, w.d_ypart};
+    for (void* p : wp)
+      if (p) (void)hipFree(p);
+    w = hipspmv_handle::Wc{};
+    h->device_bytes = bytes0;
+    return st;
+  };
+  int st;
+  if ((st = dev_upload(&w.d_rowptr, L.seg.rowptr.data(), L.seg.rowptr.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&w.d_colind, L.seg.colind.data(), L.seg.colind.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&w.d_vals, L.seg.vals.data(), L.seg.vals.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&w.d_groups, groups.data(), groups.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&w.d_rowseg, L.rowseg.data(), L.rowseg.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&w.d_segidx, L.segidx.data(), L.segidx.size(), h->device_bytes))) return fail(st);
+  {  // the reduce is a csr_vector over (rowseg, segidx) with ypart as x: its own balanced row groups
+    std::vector<uint32_t> rg;
+    build_row_groups(L.rowseg.data(), a.rows, rg);
+    if ((st = dev_upload(&w.d_rgroups, rg.data(), rg.size(), h->device_bytes))) return fail(st);
+    w.rgroups = (uint32_t)rg.size() - 1;
+  }
+  {
+    const uint64_t b = 8ull * std::max<uint32_t>(L.nseg, 1);
+    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&w.d_ypart), b);
+    if (e != hipSuccess) return fail(hip_fail(e, "hipMalloc(segment partials)"));
+    h->device_bytes += b;
+  }
+  w.nseg = L.nseg;
+  w.ngroups = (uint32_t)groups.size() - 1;
+  w.max_seg = L.max_seg;
+  w.log2w = L.log2w;
+  w.built = true;
+  return HIPSPMV_OK;
+}
+
 // The vcache-family layout k from the CSR `a` (k 0: ordered vcache, 3: wgather).
 static int build_vc_layout(hipspmv_t* h, int k, const HostCSR& a) {
   if (h->vc[k].ok) return HIPSPMV_OK;
@@ -322,6 +381,11 @@ static int auto_pick(const hipspmv_t* h, bool fast_ok, bool built) {
   // bytes), SELL's FAST hub pieces spread it over many waves.  C5 shard 0 of 8
   // (70 k hub rows, longest 238 k): csr_vector 2019 us, sell 496 us; R-MAT s20
   // (longest 39.7 k): csr_vector 253 us, sell 573 us.
+  // x wider than the L2s and rows that keep several entries per column window:
+  // csr_vector over the windowed segments (C5 shards 0 / 7 of 8: 238 / 280 us
+  // against sell 479 / csr_vector 628); C4's uniform rows
+  // (one entry per window) stay on wgather above
+  if (h->wc_segments && h->wc_segments * 2 <= h->nnz) return !built || h->wc.built ? HIPSPMV_KERNEL_WCSR : generic;
   const uint64_t alg = 12ull * h->nnz + 4ull * (h->rows + 1ull) + 8ull * h->cols + 8ull * h->rows;
   if ((uint64_t)h->max_row_len * 4167ull > alg) return !built || h->sell.built ? HIPSPMV_KERNEL_SELL : generic;
   return HIPSPMV_KERNEL_CSR_VECTOR;
@@ -367,6 +431,7 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   if (experimental && vcache_eligible(a, kVcSplit4) && (st = upload_vc(h, 2, a, kVcSplit4))) return st;
   h->wg_eligible = vcache_eligible(a, kWgWindow);
   if (h->wg_eligible) h->wg_max_run = vcache_max_run(a, (uint32_t)kWgWindow.panel);
+  if (a.cols >= kWcMinCols) h->wc_segments = windowed_segments(a, kWcLog2Window);
   // the layouts AUTO will run, built now from the host CSR (no copy back off
   // the device at first use, and their time is setup time); device OOM here
   // leaves AUTO on the generic kernels instead of failing the create
@@ -376,6 +441,7 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
     if (k == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
     else if (k == HIPSPMV_KERNEL_WGATHER) st = build_vc_layout(h, 3, a);
     else if (k == HIPSPMV_KERNEL_VCACHE) st = build_vc_layout(h, 0, a);
+    else if (k == HIPSPMV_KERNEL_WCSR) st = build_wcsr_layout(h, a);
     else st = HIPSPMV_OK;
     if (st == HIPSPMV_ERR_OOM) {
       h->auto_fallback++;
@@ -447,6 +513,8 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
       return HIPSPMV_KERNEL_CSR_LANE;
     case HIPSPMV_KERNEL_SELL:  // ordered: valid in both modes
       return HIPSPMV_KERNEL_SELL;
+    case HIPSPMV_KERNEL_WCSR:  // fast; any matrix, layout built on first selection
+      return fast_ok ? HIPSPMV_KERNEL_WCSR : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_VECTOR:
       return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_AUTO:
@@ -462,7 +530,8 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
 static int ensure_layout(hipspmv_t* h, int kernel) {
   const bool need = (kernel == HIPSPMV_KERNEL_SELL && !h->sell.built) ||
                     (kernel == HIPSPMV_KERNEL_WGATHER && !h->vc[3].ok) ||
-                    (kernel == HIPSPMV_KERNEL_VCACHE && !h->vc[0].ok);
+                    (kernel == HIPSPMV_KERNEL_VCACHE && !h->vc[0].ok) ||
+                    (kernel == HIPSPMV_KERNEL_WCSR && !h->wc.built);
   if (!need) return HIPSPMV_OK;
   const uint64_t t0 = now_ns();
   int st;
@@ -472,6 +541,7 @@ static int ensure_layout(hipspmv_t* h, int kernel) {
     st = download_csr(h, a);
     if (!st) {
       if (kernel == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
+      else if (kernel == HIPSPMV_KERNEL_WCSR) st = build_wcsr_layout(h, a);
       else st = build_vc_layout(h, kernel == HIPSPMV_KERNEL_WGATHER ? 3 : 0, a);
     }
   } catch (const std::bad_alloc&) {
@@ -489,6 +559,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   hipError_t e = hipSuccess;
   if (mode == HIPSPMV_MODE_AUTO) mode = h->mode_opt;
   const bool scratch = kernel == HIPSPMV_KERNEL_VCACHE_SPLIT || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4 ||
+                       kernel == HIPSPMV_KERNEL_WCSR ||
                        (kernel == HIPSPMV_KERNEL_SELL && h->sell.npieces &&
                         (mode != HIPSPMV_MODE_ORDERED || h->dtype == HIPSPMV_U64));
   // Inside a stream capture the handle does not order anything: a graph's
@@ -546,6 +617,11 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     // entries non-temporal unless option vcache_nt > 0 (full C4: 3391 us against 3594)
     a.nt_from = h->vcache_nt > 0 ? ~0u : 0u;
     e = launch_wgather(h->dtype, a, s);
+  } else if (kernel == HIPSPMV_KERNEL_WCSR) {
+    const auto& w = h->wc;
+    WcsrArgs a{w.d_rowptr, w.d_colind, w.d_vals, w.d_groups, w.ngroups, w.d_rowseg, w.d_segidx,
+               w.d_rgroups, w.rgroups,   w.d_ypart, d_x,      d_y_in,     d_y_out,  h->rows, beta};
+    e = launch_wcsr(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
     e = kernel == HIPSPMV_KERNEL_CSR_LANE ? launch_csr_lane(h->dtype, a, s) : launch_csr_vector(h->dtype, a, s);
@@ -647,7 +723,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   if (!h || !key) return HIPSPMV_ERR_INVALID_ARG;
   const std::string k(key);
   if (k == "kernel") {
-    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_SELL) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_WCSR) return HIPSPMV_ERR_INVALID_ARG;
     if (value == HIPSPMV_KERNEL_VCACHE && !h->vc0_eligible) return HIPSPMV_ERR_UNSUPPORTED;
     if (value == HIPSPMV_KERNEL_WGATHER && !h->wg_eligible) return HIPSPMV_ERR_UNSUPPORTED;
     if (int st = ensure_layout(h, (int)value)) return st;
@@ -788,6 +864,9 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "vcache_split_max_run") *out = h->vc[1].max_run;
   else if (k == "wgather_windows") *out = h->vc[3].npanels;
   else if (k == "vcache_split4_x_bytes") *out = h->vc[2].ok ? 8ull * h->vc[2].nblocks * h->cols : 0;
+  else if (k == "wcsr_segments") *out = h->wc.built ? h->wc.nseg : h->wc_segments;
+  else if (k == "wcsr_max_segment") *out = h->wc.max_seg;
+  else if (k == "wcsr_window_log2") *out = h->wc.built ? h->wc.log2w : kWcLog2Window;
   else if (k == "sell_slices") *out = h->sell.nslices;
   else if (k == "sell_hubs") *out = h->sell.nhubs;
   else if (k == "sell_hub_pieces") *out = h->sell.npieces;
@@ -866,6 +945,7 @@ const char* hipspmv_kernel_name(hipspmv_t* h, int mode) {
     case HIPSPMV_KERNEL_CSR_LANE: return "csr_lane";
     case HIPSPMV_KERNEL_CSR_VECTOR: return "csr_vector";
     case HIPSPMV_KERNEL_SELL: return "sell";
+    case HIPSPMV_KERNEL_WCSR: return "wcsr";
     default: return "unsupported";
   }
 }

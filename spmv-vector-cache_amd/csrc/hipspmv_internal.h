@@ -57,6 +57,16 @@ constexpr uint32_t kVcMore = 1u << 31;  // next entry continues this entry's row
 // 0.25 ms in csr_vector, round-2 sweep).
 constexpr uint32_t kVcRunMax = 16;
 
+// ---- wcsr: csr_vector over the column-windowed segment matrix
+// Every row is cut at column windows of 2^kWcLog2Window columns (512 KiB of
+// x); the pieces ("segments", one per (window, row) pair that has
+// entries) form the rows of A', in window-major order.  csr_vector over A'
+// walks x one window at a time; y[r] is the sum of r's segment partials in
+// window order (k_wreduce).
+constexpr uint32_t kWcLog2Window = 16;
+// AUTO considers wcsr from this many columns (x of 16 MiB: four XCD L2s)
+constexpr uint32_t kWcMinCols = 1u << 21;
+
 // ---- csr_vector geometry ---------------------------------------------------
 constexpr int kCvGroupNnz = 256;  // max nnz of a multi-row group (4 per lane)
 constexpr int kCvGroupRows = 64;  // max rows of a multi-row group (1 per lane)
@@ -136,6 +146,13 @@ struct VcacheLayout {
   uint64_t n_cont = 0;   // entries continuing a run (added after another entry of their row in one step)
 };
 
+struct WinLayout {
+  uint32_t log2w = 0, nseg = 0, max_seg = 0;
+  HostCSR seg;                  // A': rows = segments (window-major, then row), cols = the matrix's
+  std::vector<uint32_t> rowseg; // rows + 1: row r's segments are segidx[rowseg[r] .. rowseg[r+1])
+  std::vector<uint32_t> segidx; // nseg: segment ids of each row, in window order
+};
+
 struct SellLayout {
   uint32_t nslices = 0, nhubs = 0;
   std::vector<uint64_t> off;    // nslices + 1: first entry of each slice
@@ -164,8 +181,14 @@ void vcache_geometry(uint32_t rows, uint32_t cols, const VcGeom& g, VcacheLayout
 uint32_t vcache_max_run(const HostCSR& a, uint32_t panel);
 void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out);
 void build_sell(const HostCSR& a, SellLayout& out);
+// The column-windowed segment matrix of `a` (columns sorted within each row:
+// vcache_eligible's condition).  Throws std::bad_alloc on host OOM.
+void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out);
+// Segments build_windowed would make (one pass, no allocation).
+uint64_t windowed_segments(const HostCSR& a, uint32_t log2w);
 // Row groups for csr_vector: group g covers rows [groups[g], groups[g+1]).
 void build_row_groups(const HostCSR& a, std::vector<uint32_t>& groups);
+void build_row_groups(const uint32_t* rowptr, uint32_t rows, std::vector<uint32_t>& groups);
 
 // hipspmv_last_error() text for this thread (capi.cpp).
 void set_last_error(const std::string& what);

@@ -39,6 +39,24 @@ struct CsrArgs {
   int beta;
 };
 
+struct WcsrArgs {  // csr_vector over the column-windowed segment matrix, then k_wreduce
+  const uint32_t* seg_rowptr;
+  const uint32_t* seg_colind;
+  const void* seg_vals;
+  const uint32_t* groups;  // csr_vector row groups of the segment matrix
+  uint32_t ngroups;
+  const uint32_t* rowseg;         // [rows + 1]: row r's segments are segidx[rowseg[r] .. rowseg[r+1])
+  const uint32_t* segidx;         // [nseg]: each row's segment ids, in window order
+  const uint32_t* reduce_groups;  // csr_vector row groups of the (rowseg, segidx) reduce
+  uint32_t rgroups;
+  void* ypart;                    // [nseg] segment partials, in segment order
+  const void* x;
+  const void* y_in;
+  void* y_out;
+  uint32_t rows;
+  int beta;
+};
+
 struct SellArgs {
   const uint64_t* off;    // [nslices + 1]
   const uint32_t* width;  // [nslices]
@@ -72,6 +90,7 @@ hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);
 hipError_t launch_vcache_profiled(int dtype, const VcacheArgs& a, hipStream_t s);
 constexpr int kVcProfWords = 8;
 hipError_t launch_sell(int dtype, const SellArgs& a, hipStream_t s);
+hipError_t launch_wcsr(int dtype, const WcsrArgs& a, hipStream_t s);
 hipError_t launch_wgather(int dtype, const VcacheArgs& a, hipStream_t s);
 hipError_t launch_csr_lane(int dtype, const CsrArgs& a, hipStream_t s);
 hipError_t launch_csr_vector(int dtype, const CsrArgs& a, hipStream_t s);

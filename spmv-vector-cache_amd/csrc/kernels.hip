@@ -74,12 +74,18 @@ __device__ __forceinline__ T wave_segscan(T v, uint32_t f) {
   return v;
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__ rowptr,
-                                                     const uint32_t* __restrict__ colind, const T* __restrict__ vals,
-                                                     const T* __restrict__ x, const T* __restrict__ y_in,
-                                                     T* __restrict__ y_out, const uint32_t* __restrict__ groups,
-                                                     uint32_t ngroups, int beta) {
+// One wave's row group of y = A*x (plus y_in when beta).  KIND 0: plain
+// csr_vector.  KIND 1: the wcsr segment pass -- entry
+// (colind, vals) loads non-temporal, so the streamed entries do not push the
+// current x window out of L2 (§6.10).  KIND 2: the wcsr reduce -- no values,
+// each "entry" adds x[colind[e]] (a segment partial), so the same balanced
+// groups and segmented scan sum every row's partials in a fixed order.
+template <typename T, int KIND>
+__device__ __forceinline__ void csr_vector_group(const uint32_t* __restrict__ rowptr,
+                                                 const uint32_t* __restrict__ colind, const T* __restrict__ vals,
+                                                 const T* __restrict__ x, const T* __restrict__ y_in,
+                                                 T* __restrict__ y_out, const uint32_t* __restrict__ groups,
+                                                 uint32_t ngroups, int beta) {
 #pragma clang fp contract(off)
   __shared__ uint32_t heads[4][kCvGroupNnz / 32];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -87,18 +93,24 @@ __global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__
   if (g >= ngroups) return;  // wave-uniform; no workgroup barriers below
   const uint32_t r0 = groups[g], r1 = groups[g + 1];
   const uint32_t base = rowptr[r0], n = rowptr[r1] - base;
+  auto ci = [&](uint32_t e) { return KIND == 1 ? __builtin_nontemporal_load(colind + e) : colind[e]; };
+  // the e-th term of the group's sums: a rounded product, or a partial
+  auto term = [&](uint32_t e) -> T {
+    if constexpr (KIND == 2) return x[ci(e)];
+    else return (KIND == 1 ? __builtin_nontemporal_load(vals + e) : vals[e]) * x[ci(e)];
+  };
 
   if (r1 - r0 == 1 && n > (uint32_t)kCvGroupNnz) {
     // long row: four interleaved lane accumulators, then a DPP wave reduction
     T a0 = T(0), a1 = T(0), a2 = T(0), a3 = T(0);
     uint32_t e = lane;
     for (; e + 192 < n; e += 256) {
-      a0 = madd(a0, vals[base + e], x[colind[base + e]]);
-      a1 = madd(a1, vals[base + e + 64], x[colind[base + e + 64]]);
-      a2 = madd(a2, vals[base + e + 128], x[colind[base + e + 128]]);
-      a3 = madd(a3, vals[base + e + 192], x[colind[base + e + 192]]);
+      a0 = a0 + term(base + e);
+      a1 = a1 + term(base + e + 64);
+      a2 = a2 + term(base + e + 128);
+      a3 = a3 + term(base + e + 192);
     }
-    for (; e < n; e += 64) a0 = madd(a0, vals[base + e], x[colind[base + e]]);
+    for (; e < n; e += 64) a0 = a0 + term(base + e);
     T s = (a0 + a1) + (a2 + a3);
     s = wave_segscan(s, lane == 0 ? 1u : 0u);  // one segment: lane 63 holds the total
     if (lane == 63) y_out[r0] = beta ? y_in[r0] + s : s;
@@ -124,7 +136,7 @@ __global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__
     T p = T(0);
     uint32_t f = 0;
     if (e < n) {
-      p = vals[base + e] * x[colind[base + e]];
+      p = term(base + e);
       f = (heads[w][e >> 5] >> (e & 31)) & 1u;
     }
     if (lane == 0 && !f) p = carry + p;
@@ -135,6 +147,28 @@ __global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__
     carry = __shfl(p, 63);
   }
   if (own && re == rs) y_out[r0 + lane] = beta ? y_in[r0 + lane] : T(0);
+}
+
+// NTE: the wcsr segment pass (KIND 1 above)
+template <typename T, bool NTE = false>
+__global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__ rowptr,
+                                                     const uint32_t* __restrict__ colind, const T* __restrict__ vals,
+                                                     const T* __restrict__ x, const T* __restrict__ y_in,
+                                                     T* __restrict__ y_out, const uint32_t* __restrict__ groups,
+                                                     uint32_t ngroups, int beta) {
+  csr_vector_group<T, NTE ? 1 : 0>(rowptr, colind, vals, x, y_in, y_out, groups, ngroups, beta);
+}
+
+// k_wreduce (wcsr): y[r] = (y_in[r] +) the sum of row r's segment partials
+// ypart[segidx[k]], k in [rowseg[r], rowseg[r+1]) (window order), over the
+// reduce's own balanced row groups -- a fixed order, so wcsr is
+// deterministic; a row with no segment gets y_in[r] (beta 1) or +0.0.
+template <typename T>
+__global__ __launch_bounds__(256) void k_wreduce(const uint32_t* __restrict__ rowseg,
+                                                  const uint32_t* __restrict__ segidx, const T* __restrict__ ypart,
+                                                  const T* __restrict__ y_in, T* __restrict__ y_out,
+                                                  const uint32_t* __restrict__ groups, uint32_t ngroups, int beta) {
+  csr_vector_group<T, 2>(rowseg, segidx, (const T*)nullptr, ypart, y_in, y_out, groups, ngroups, beta);
 }
 
 // ---------------------------------------------------------------------------
@@ -151,6 +185,21 @@ hipError_t launch_csr_vector(const CsrArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_csr_vector<T>, dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.rowptr, a.colind,
                      (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.groups, a.ngroups, a.beta);
   return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
+  // the segment partials: csr_vector over A', beta 0, entries non-temporal
+  if (a.ngroups)
+    hipLaunchKernelGGL((k_csr_vector<T, true>), dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr,
+                       a.seg_colind, (const T*)a.seg_vals, (const T*)a.x, (const T*)nullptr, (T*)a.ypart,
+                       a.groups, a.ngroups, 0);
+  hipLaunchKernelGGL(k_wreduce<T>, dim3((a.rgroups + 3) / 4), dim3(256), 0, s, a.rowseg, a.segidx,
+                     (const T*)a.ypart, (const T*)a.y_in, (T*)a.y_out, a.reduce_groups, a.rgroups, a.beta);
+  return hipGetLastError();
+}
+hipError_t launch_wcsr(int dtype, const WcsrArgs& a, hipStream_t s) {
+  return dtype ? launch_wcsr<uint64_t>(a, s) : launch_wcsr<double>(a, s);
 }
 
 hipError_t launch_csr_lane(int dtype, const CsrArgs& a, hipStream_t s) {

@@ -269,29 +269,113 @@ void build_sell(const HostCSR& a, SellLayout& out) {
   out.nslices = nslices;
 }
 
+// Column-windowed segment matrix (k_wreduce / wcsr, hipspmv_internal.h):
+// segment (w, r) holds row r's entries with column in window w, in their CSR
+// (ascending column) order; segments are numbered window-major, rows ascending
+// within a window, so a kernel walking them in order gathers from one window
+// of x at a time.  For each row, its segment ids in window order.
+uint64_t windowed_segments(const HostCSR& a, uint32_t log2w) {
+  uint64_t n = 0;
+  for (uint32_t r = 0; r < a.rows; ++r) {
+    uint32_t prev = UINT32_MAX;
+    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+      const uint32_t w = a.colind[e] >> log2w;
+      n += w != prev;
+      prev = w;
+    }
+  }
+  return n;
+}
+
+void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out) {
+  out = WinLayout{};
+  out.log2w = log2w;
+  const uint32_t nwin = (uint32_t)(((uint64_t)a.cols + (1ull << log2w) - 1) >> log2w);
+  // pass 1: segments per window (a row's windows change where its columns cross a boundary)
+  std::vector<uint64_t> wstart((size_t)nwin + 1, 0);
+  out.rowseg.assign((size_t)a.rows + 1, 0);
+  for (uint32_t r = 0; r < a.rows; ++r) {
+    uint32_t prev = UINT32_MAX, n = 0;
+    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+      const uint32_t w = a.colind[e] >> log2w;
+      if (w != prev) {
+        wstart[w + 1]++;
+        ++n;
+        prev = w;
+      }
+    }
+    out.rowseg[r + 1] = out.rowseg[r] + n;
+  }
+  for (uint32_t w = 0; w < nwin; ++w) wstart[w + 1] += wstart[w];
+  out.nseg = (uint32_t)wstart[nwin];
+  // pass 2: each segment's id (rows ascend, so ids ascend within a window) and length
+  std::vector<uint64_t> cursor(wstart.begin(), wstart.end() - 1);
+  std::vector<uint32_t> len(out.nseg, 0);
+  out.segidx.resize(out.nseg);
+  for (uint32_t r = 0; r < a.rows; ++r) {
+    uint32_t prev = UINT32_MAX, k = out.rowseg[r];
+    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+      const uint32_t w = a.colind[e] >> log2w;
+      if (w != prev) {
+        out.segidx[k++] = (uint32_t)cursor[w]++;
+        prev = w;
+      }
+      len[out.segidx[k - 1]]++;
+    }
+  }
+  HostCSR& g = out.seg;
+  g.rows = out.nseg;
+  g.cols = a.cols;
+  g.nnz = a.nnz;
+  g.rowptr.assign((size_t)out.nseg + 1, 0);
+  for (uint32_t i = 0; i < out.nseg; ++i) {
+    g.rowptr[i + 1] = g.rowptr[i] + len[i];
+    out.max_seg = std::max(out.max_seg, len[i]);
+  }
+  // pass 3: copy each row's entries into its segments
+  g.colind.resize(a.nnz);
+  g.vals.resize(a.nnz);
+  for (uint32_t r = 0; r < a.rows; ++r) {
+    uint32_t prev = UINT32_MAX, k = out.rowseg[r], d = 0;
+    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+      const uint32_t w = a.colind[e] >> log2w;
+      if (w != prev) {
+        d = g.rowptr[out.segidx[k++]];
+        prev = w;
+      }
+      g.colind[d] = a.colind[e];
+      g.vals[d] = a.vals[e];
+      ++d;
+    }
+  }
+}
+
 // Greedy row groups: consecutive rows while the group stays within
 // kCvGroupNnz nonzeros and kCvGroupRows rows; a longer row is a group alone.
 // No group crosses a multiple of HIPSPMV_SHARD_ALIGN rows, so the groups of a
 // shard that starts at such a row are exactly the unpartitioned matrix's
 // groups there, and csr_vector's reduction order -- and so its FAST-mode
 // bits -- does not depend on the partition.
-void build_row_groups(const HostCSR& a, std::vector<uint32_t>& groups) {
+void build_row_groups(const uint32_t* rowptr, uint32_t rows, std::vector<uint32_t>& groups) {
   static_assert(kCvGroupRows <= HIPSPMV_SHARD_ALIGN && HIPSPMV_SHARD_ALIGN % kCvGroupRows == 0,
                 "a group fits an aligned window");
   groups.clear();
   uint32_t r = 0;
-  while (r < a.rows) {
+  while (r < rows) {
     groups.push_back(r);
-    const uint32_t start = a.rowptr[r];
+    const uint32_t start = rowptr[r];
     uint32_t n = 0;
-    while (r < a.rows && n < (uint32_t)kCvGroupRows && a.rowptr[r + 1] - start <= (uint32_t)kCvGroupNnz &&
+    while (r < rows && n < (uint32_t)kCvGroupRows && rowptr[r + 1] - start <= (uint32_t)kCvGroupNnz &&
            (n == 0 || r % HIPSPMV_SHARD_ALIGN != 0)) {
       ++r;
       ++n;
     }
     if (n == 0) ++r;  // a long row: its own group
   }
-  groups.push_back(a.rows);
+  groups.push_back(rows);
+}
+void build_row_groups(const HostCSR& a, std::vector<uint32_t>& groups) {
+  build_row_groups(a.rowptr.data(), a.rows, groups);
 }
 
 }  // namespace hipspmv

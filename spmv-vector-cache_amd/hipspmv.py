@@ -33,11 +33,13 @@ F64, U64 = 0, 1
 MODE_AUTO, MODE_ORDERED, MODE_FAST = 0, 1, 2
 KERNEL_AUTO, KERNEL_VCACHE, KERNEL_CSR_LANE, KERNEL_CSR_VECTOR, KERNEL_VCACHE_SPLIT = 0, 1, 2, 3, 4
 KERNEL_VCACHE_SPLIT4, KERNEL_WGATHER = 5, 6  # experimental: never chosen by AUTO
-KERNEL_SELL = 7  # SELL-C-sigma lane per row; selectable, not chosen by AUTO yet
+KERNEL_SELL = 7  # SELL-C-sigma lane per row
+KERNEL_WCSR = 8  # csr_vector over column-windowed row segments + a window-order reduce (FAST)
 SHARD_ALIGN = 64  # HIPSPMV_SHARD_ALIGN: row shards starting at multiples keep every kernel's bits
 KERNELS = {"auto": KERNEL_AUTO, "vcache": KERNEL_VCACHE, "csr_lane": KERNEL_CSR_LANE,
            "csr_vector": KERNEL_CSR_VECTOR, "vcache_split": KERNEL_VCACHE_SPLIT,
-           "vcache_split4": KERNEL_VCACHE_SPLIT4, "wgather": KERNEL_WGATHER, "sell": KERNEL_SELL}
+           "vcache_split4": KERNEL_VCACHE_SPLIT4, "wgather": KERNEL_WGATHER, "sell": KERNEL_SELL,
+           "wcsr": KERNEL_WCSR}
 STATUS = {0: "ok", 1: "invalid argument", 2: "invalid matrix", 3: "HIP error", 4: "out of memory",
           5: "unsupported", 6: "no device", 7: "unknown key"}
 

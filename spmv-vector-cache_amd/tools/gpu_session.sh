@@ -46,7 +46,13 @@ for s in $STEPS; do
     selltests) step pytest_sell 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "sell or rmat or hub or fullsize" ;;
     sweepc4nt) step sweep_c4_nt 900 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 24 --log2-cols 24 --only "=wgather,=wgather nt" --rounds 2 --reps 10 ;;
     states) step profile_states 300 python -u spmv-vector-cache_amd/tools/profile_states.py ;;
+    wcsrtests) step pytest_wcsr 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "wcsr" ;;
+    sweep4) HIPSPMV_EXPERIMENTAL=1 step sweep_split4 900 python spmv-vector-cache_amd/tools/kernel_sweep.py --only "split4,=vcache_split" ;;
+    wcsrshards) step wcsr_shards 900 bash -c 'for s in 0 3 7; do python -u spmv-vector-cache_amd/tools/wfast_probe.py --windows "" --shard $s || exit 1; done' ;;
     wfast) step wfast_probe 900 python -u spmv-vector-cache_amd/tools/wfast_probe.py ;;
+    wfast2) step wfast_probe_s0 600 python -u spmv-vector-cache_amd/tools/wfast_probe.py --windows 14,15,16,17 &&
+            step wfast_probe_s7 600 python -u spmv-vector-cache_amd/tools/wfast_probe.py --shard 7 --windows 15,16,17,19 &&
+            step wfast_probe_c4 600 python -u spmv-vector-cache_amd/tools/wfast_probe.py --c4 --windows 15,17,19 ;;
     sweepnt) step sweep_nt 900 python spmv-vector-cache_amd/tools/kernel_sweep.py --only "vcache,sell,split" ;;
     newtests) step pytest_new 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "profile or spmvbench or cache_behaviour" ;;
     sweep) step sweep 600 python spmv-vector-cache_amd/tools/kernel_sweep.py ;;

@@ -53,6 +53,7 @@ cands = [("vcache", "vcache", O, {}), ("csr_lane", "csr_lane", O, {}), ("vcache_
          ("sell nt 1/2", "sell", O, {"sell_nt": ("sell_slices", 0.5)}),
          ("sell nt 5/8", "sell", O, {"sell_nt": ("sell_slices", 0.625)}),
          ("sell fast nt 1/2", "sell", F, {"sell_nt": ("sell_slices", 0.5)}),
+         ("wcsr", "wcsr", F, {}),
          ("wgather nt", "wgather", O, {"vcache_nt": 0}), ("wgather no nt", "wgather", O, {"vcache_nt": 1 << 30})]
 if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
     cands += [("vcache xl1", "vcache", O, {"vcache_xlane": 1}), ("vcache xl2", "vcache", O, {"vcache_xlane": 2}),
@@ -68,7 +69,10 @@ if os.environ.get("HIPSPMV_EXPERIMENTAL") == "1":
               ("split4 dma xl3", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 3}),
               ("split4 map", "vcache_split4", F, {"vcache_map": 1}),
               ("split4 map xl3", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 3}),
-              ("split4 map xl2", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 2})]
+              ("split4 map xl2", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 2}),
+              ("split4 nt", "vcache_split4", F, {"vcache_nt": 0}),
+              ("split4 dma xl3 nt", "vcache_split4", F, {"vcache_dma": 1, "vcache_xlane": 3, "vcache_nt": 0}),
+              ("split4 map xl3 nt", "vcache_split4", F, {"vcache_map": 1, "vcache_xlane": 3, "vcache_nt": 0})]
 if a.only:
     keep = a.only.split(",")
     # "=label" keeps that label only; anything else keeps the labels containing it

@@ -534,9 +534,46 @@ int main(int argc, char** argv) {
           if (g >= s0 && g <= s1) want.push_back(g - s0);
         shards = shards && sg == want;
       }
-      failures += !(same && tiles && shards);
-      std::printf("%-28s csc_to_csr %s, row groups %s, shard groups %s\n", cs.name.c_str(), same ? "ok" : "FAIL",
-                  tiles ? "ok" : "FAIL", shards ? "ok" : "FAIL");
+      // the wcsr segment matrix (build_windowed): each row's segments, read in
+      // segidx order, are the row's entries in order; a segment lies in one
+      // window; segments run window-major with rows ascending; groups tile it
+      bool wins = true;
+      for (uint32_t lw : {8u, 12u, kWcLog2Window}) {
+        WinLayout W;
+        build_windowed(A, lw, W);
+        const HostCSR& G = W.seg;
+        wins = wins && G.rows == W.nseg && G.nnz == A.nnz && G.rowptr.size() == (size_t)W.nseg + 1 &&
+               G.rowptr[0] == 0 && G.rowptr[W.nseg] == A.nnz && W.rowseg.size() == (size_t)A.rows + 1 &&
+               W.rowseg[A.rows] == W.nseg && W.segidx.size() == W.nseg;
+        if (!wins) break;
+        std::vector<uint32_t> owner(W.nseg, UINT32_MAX);
+        for (uint32_t r = 0; r < A.rows && wins; ++r) {
+          uint32_t e = A.rowptr[r], prevw = 0;
+          for (uint32_t k = W.rowseg[r]; k < W.rowseg[r + 1] && wins; ++k) {
+            const uint32_t sg = W.segidx[k];
+            wins = sg < W.nseg && owner[sg] == UINT32_MAX && G.rowptr[sg] < G.rowptr[sg + 1];
+            if (!wins) break;
+            owner[sg] = r;
+            const uint32_t w = G.colind[G.rowptr[sg]] >> lw;
+            wins = k == W.rowseg[r] || w > prevw;  // a row's segments in ascending windows
+            prevw = w;
+            for (uint32_t d = G.rowptr[sg]; d < G.rowptr[sg + 1] && wins; ++d, ++e)
+              wins = e < A.rowptr[r + 1] && G.colind[d] == A.colind[e] && G.vals[d] == A.vals[e] &&
+                     (G.colind[d] >> lw) == w;
+          }
+          wins = wins && e == A.rowptr[r + 1];
+        }
+        for (uint32_t sg = 1; sg < W.nseg && wins; ++sg) {  // window-major, rows ascending in a window
+          const uint32_t w0 = G.colind[G.rowptr[sg - 1]] >> lw, w1 = G.colind[G.rowptr[sg]] >> lw;
+          wins = w0 < w1 || (w0 == w1 && owner[sg - 1] < owner[sg]);
+        }
+        std::vector<uint32_t> gg;
+        build_row_groups(G, gg);
+        wins = wins && gg.front() == 0 && gg.back() == G.rows;
+      }
+      failures += !(same && tiles && shards && wins);
+      std::printf("%-28s csc_to_csr %s, row groups %s, shard groups %s, windowed segments %s\n", cs.name.c_str(),
+                  same ? "ok" : "FAIL", tiles ? "ok" : "FAIL", shards ? "ok" : "FAIL", wins ? "ok" : "FAIL");
     }
     std::vector<double> x(cs.A.cols), yin(cs.A.rows);
     for (uint32_t i = 0; i < cs.A.cols; ++i) x[i] = uniform11(splitmix64_at(3, i));

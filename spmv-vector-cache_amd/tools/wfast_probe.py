@@ -29,14 +29,19 @@ p = argparse.ArgumentParser()
 p.add_argument("--scale", type=int, default=24)
 p.add_argument("--shard", type=int, default=0)
 p.add_argument("--windows", default="17,19,21")
+p.add_argument("--c4", action="store_true", help="C4 shard (stripe 2^21 x 2^24, 32 nnz/row) instead of R-MAT")
 p.add_argument("--reps", type=int, default=20)
 a = p.parse_args()
 
 t0 = time.time()
-bounds = hs.partition_row_counts(hs.gen_rmat_row_counts(a.scale, 16, 4), 8)
-r0, r1 = int(bounds[a.shard]), int(bounds[a.shard + 1])
-rowptr, colind, vals = hs.gen_rmat_rows(a.scale, r0, r1, 16, 4)
-rows, cols = r1 - r0, 1 << a.scale
+if a.c4:
+    rows, cols = 1 << 21, 1 << a.scale
+    rowptr, colind, vals = hs.gen_stripe_csr(0, rows, cols, 32)
+else:
+    bounds = hs.partition_row_counts(hs.gen_rmat_row_counts(a.scale, 16, 4), 8)
+    r0, r1 = int(bounds[a.shard]), int(bounds[a.shard + 1])
+    rowptr, colind, vals = hs.gen_rmat_rows(a.scale, r0, r1, 16, 4)
+    rows, cols = r1 - r0, 1 << a.scale
 print(f"shard {a.shard}: rows {rows} nnz {colind.size} (gen {time.time() - t0:.1f} s)", flush=True)
 x = torch.from_numpy(hs.gen_vector(cols, 3)).cuda()
 s = torch.cuda.current_stream()
@@ -57,15 +62,18 @@ def timeit(h, mode, yd):
 alg = 12 * colind.size + 4 * (rows + 1) + 8 * cols + 8 * rows
 h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
 y = torch.empty(rows, dtype=torch.float64, device="cuda")
-for k in ("sell", "csr_vector"):
-    h.set_kernel(k)
+for k in ("sell", "csr_vector", "wgather", "wcsr"):
+    try:
+        h.set_kernel(k)
+    except hs.HipSpMVError:
+        continue
     us = timeit(h, hs.MODE_FAST, y)
     print(f"A  {k:10s} FAST {us:8.1f} us  frac8TB={alg / us / 1e3 / 8000:.3f}", flush=True)
 h.close()
 
 lens = np.diff(rowptr.astype(np.int64))
 row_of = np.repeat(np.arange(rows, dtype=np.int64), lens)
-for lw in [int(v) for v in a.windows.split(",")]:
+for lw in [int(v) for v in a.windows.split(",") if v]:
     win = colind.astype(np.int64) >> lw
     key = win * rows + row_of  # window-major, then row; each row's entries stay in column order
     order = np.argsort(key, kind="stable")
@@ -79,7 +87,7 @@ for lw in [int(v) for v in a.windows.split(",")]:
     print(f"W=2^{lw}: {nseg} segments, longest {l2.max()}", flush=True)
     h2 = hs.Handle.from_csr(rp2, c2, v2, nseg, cols)
     y2 = torch.empty(nseg, dtype=torch.float64, device="cuda")
-    for k in ("sell", "csr_vector"):
+    for k in ("csr_vector",):
         h2.set_kernel(k)
         us = timeit(h2, hs.MODE_FAST, y2)
         print(f"A' {k:10s} FAST {us:8.1f} us  frac8TB={alg / us / 1e3 / 8000:.3f} (segment partials only)",

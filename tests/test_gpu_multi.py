@@ -90,3 +90,46 @@ def test_multi_invalid(gpu):
         hs.MultiHandle(colptr, rowind, vals, rows, cols, [])
     with pytest.raises(hs.HipSpMVError):
         hs.MultiHandle(colptr, rowind, vals, rows, cols, [0, 999])
+
+
+_RCCL_CHILD = r'''
+import os, sys, numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+import hipspmv as hs
+torch.cuda.set_device(0)
+dev = torch.device("cuda", 0)
+dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm
+# bench.py's N>1 step on one rank: x generated on rank 0 and broadcast over RCCL, the shard's
+# SpMV, the max-over-ranks kernel time and the y all-gather
+n = 1 << 16
+rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+x = torch.from_numpy(hs.gen_vector(n, 3)).to(dev) if dist.get_rank() == 0 else torch.empty(n, dtype=torch.float64, device=dev)
+dist.broadcast(x, src=0)
+h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+y = torch.empty(n, dtype=torch.float64, device=dev)
+h.exec_device(x, y, beta=0, mode=hs.MODE_FAST, stream=torch.cuda.current_stream())
+t = torch.tensor([1.0], dtype=torch.float64, device=dev)
+dist.all_reduce(t, op=dist.ReduceOp.MAX)
+g = torch.empty(n * dist.get_world_size(), dtype=torch.float64, device=dev)
+dist.all_gather_into_tensor(g, y)
+torch.cuda.synchronize()
+ref = h.exec(hs.gen_vector(n, 3), beta=0, mode=hs.MODE_FAST)
+assert g.cpu().numpy().tobytes() == ref.tobytes() and t.item() == 1.0
+dist.destroy_process_group()
+print("rccl ok", torch.cuda.get_device_name(0))
+'''
+
+
+def test_rccl_collectives_single_rank(gpu, tmp_path):
+    """RCCL ("nccl" in torch.distributed) itself on the GPU box: init, broadcast, all-reduce and
+    all-gather around one SpMV -- bench.py's N>1 step with one rank (two ranks on one device are
+    refused by RCCL, so the N>1 exchange is rehearsed with gloo, tests/test_bench_cpu.py)"""
+    import os
+    import subprocess
+    import sys
+    script = tmp_path / "rccl_child.py"
+    script.write_text(_RCCL_CHILD)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29517", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, str(script), hs.PKG_DIR], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0 and "rccl ok" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]

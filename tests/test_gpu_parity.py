@@ -58,7 +58,7 @@ def _check(name, rows, cols, colptr, rowind, vals, x, kernel, beta, mode=hs.MODE
 
 
 @pytest.mark.parametrize("name", fx.ALL_FIXTURES)
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr"])
 @pytest.mark.parametrize("beta", [0, 1])
 def test_fixtures(gpu, name, kernel, beta):
     rows, cols, colptr, rowind, vals = fx.load(name)
@@ -100,7 +100,7 @@ def _random_csc(rows, cols, density, rng, dtype=np.float64, empty_rows=True, lon
 # panel patched); (900, 14001): 4 panels, column parts of 1, 1 and 2 (vc_part_first)
 @pytest.mark.parametrize("shape", [(1, 1), (1, 300), (300, 1), (257, 1000), (5000, 333), (3000, 20000),
                                    (700, 20001), (900, 14001)])
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr"])
 def test_random_ragged(gpu, shape, kernel):
     rng = np.random.default_rng(shape[0] * 31 + shape[1])
     rows, cols = shape
@@ -112,7 +112,7 @@ def test_random_ragged(gpu, shape, kernel):
         _check(f"rand{shape}", rows, cols, colptr, rowind, vals, x, kernel, beta, mode)
 
 
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr"])
 def test_random_u64_wraparound(gpu, kernel):
     rng = np.random.default_rng(5)
     rows, cols = 4000, 9000
@@ -122,7 +122,7 @@ def test_random_u64_wraparound(gpu, kernel):
         _check("u64", rows, cols, colptr, rowind, vals, x, kernel, beta, hs.MODE_FAST)
 
 
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr"])
 def test_random_duplicates(gpu, kernel):
     # repeated (row, col) entries (5 % of a ragged matrix with a full-width row):
     # ORDERED kernels add each copy in CSC order, bit for bit; FAST within the bound
@@ -135,6 +135,51 @@ def test_random_duplicates(gpu, kernel):
     mode = hs.MODE_ORDERED if kernel in ORDERED_KERNELS else hs.MODE_FAST
     for beta in (0, 1):
         _check("dup", rows, cols, colptr, rowind, vals, x, kernel, beta, mode)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.uint64])
+def test_wcsr_wide_windows(gpu, dtype):
+    # wcsr cuts rows at 2^16-column windows: a wide, skewed matrix (rows spanning many windows, a
+    # full-width row, empty rows, an odd column count) -- FAST within the bound and identical bits
+    # on every run; u64 exact; the segment count matches a CPU recount
+    rng = np.random.default_rng(21)
+    rows, cols = 3000, (1 << 21) + 13
+    want = rng.zipf(1.6, rows).clip(0, 40000)
+    want[rng.integers(0, rows, 300)] = 0
+    want[5] = 60000
+    per_row = [np.unique(rng.integers(0, cols, int(n))) for n in want]  # sorted, distinct
+    lens = np.array([c.size for c in per_row], np.int64)
+    rowptr = np.zeros(rows + 1, np.uint32)
+    rowptr[1:] = np.cumsum(lens)
+    colind = np.concatenate(per_row).astype(np.uint32)
+    if dtype == np.float64:
+        vals, x = rng.uniform(-1, 1, colind.size), rng.uniform(-1, 1, cols)
+    else:
+        vals = rng.integers(0, 2**64, colind.size, dtype=np.uint64)
+        x = rng.integers(0, 2**64, cols, dtype=np.uint64)
+    colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+    assert h.kernel_name(hs.MODE_FAST) == "wcsr"  # AUTO: x wider than the L2s, rows windowable
+    h.set_kernel("wcsr")
+    row_of = np.repeat(np.arange(rows), lens)
+    lw = h.stat("wcsr_window_log2")
+    assert h.stat("wcsr_segments") == np.unique(row_of.astype(np.int64) * 4096 + (colind >> lw)).size
+    y0 = (rng.uniform(-1, 1, rows) if dtype == np.float64 else rng.integers(0, 2**64, rows, dtype=np.uint64))
+    for beta in (0, 1):
+        y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else np.zeros(rows, dtype)), rows=rows)
+        ys = [h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST) for _ in range(2)]
+        assert ys[0].tobytes() == ys[1].tobytes()
+        if dtype == np.uint64:
+            assert ys[0].tobytes() == y_ref.tobytes()
+        else:
+            absprod = np.zeros(rows)
+            np.add.at(absprod, row_of, np.abs(vals * x[colind]))
+            bound = _fast_bound(lens, absprod, y0 if beta else np.zeros(rows))
+            assert np.all(np.abs(ys[0] - y_ref) <= bound)
+    if dtype == np.float64:
+        with pytest.raises(hs.HipSpMVError):  # FAST only
+            h.exec(x, beta=0, mode=hs.MODE_ORDERED)
+    h.close()
 
 
 def test_duplicates_and_cms_bits(gpu):
