@@ -120,6 +120,7 @@ struct hipspmv_handle {
   // option "sell_nt": SELL slices s >= sell_nt load their entries
   // non-temporally (-1 default: the second half of the slices)
   int64_t sell_nt = -1;
+  uint32_t sell_chain_g = 0;  // option "sell_chain" (experimental): ORDERED hub chain 10*G + D
   void *d_x = nullptr, *d_y = nullptr;
   int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
   // setup_ns: create (transpose, validation, uploads, every layout AUTO uses);
@@ -579,6 +580,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                d_y_out,     q.nslices,   q.nhubs,     beta,    mode == HIPSPMV_MODE_ORDERED ? 1 : 0,
                q.d_pieces,  q.npieces,   q.d_partial, q.d_tickets};
     a.nt_from = h->sell_nt >= 0 ? (uint32_t)std::min<int64_t>(h->sell_nt, UINT32_MAX) : q.nslices / 2;
+    a.chain_g = h->sell_chain_g;
     e = launch_sell(h->dtype, a, s);
   } else if (kernel == HIPSPMV_KERNEL_VCACHE || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ||
       kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
@@ -736,6 +738,11 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "wgather_chunk") {  // row blocks per k_wgather launch (0: all in one launch)
     if (value < 0 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->wgather_chunk = (uint32_t)value;
+  } else if (k == "sell_chain") {  // experimental ORDERED hub chain: 10*G + D (0: product)
+    if (value != 0 && value != 82 && value != 121 && value != 122 && value != 161) return HIPSPMV_ERR_INVALID_ARG;
+    const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
+    if (value && !(exp && std::strcmp(exp, "1") == 0)) return HIPSPMV_ERR_UNSUPPORTED;
+    h->sell_chain_g = (uint32_t)value;
   } else if (k == "sell_nt") {  // first SELL slice whose entries load non-temporally (-1: half)
     if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->sell_nt = value;

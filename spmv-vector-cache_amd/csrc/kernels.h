@@ -79,6 +79,7 @@ struct SellArgs {
   void* partial = nullptr;      // [npieces] piece partials
   uint32_t* tickets = nullptr;  // per split row, zero between launches
   uint32_t nt_from = 0;         // slices s >= nt_from load their entries non-temporally
+  uint32_t chain_g = 0;         // exact: 10*G+D runs the experimental k_sell_chain<G, D> (0: product kChainG)
 };
 
 hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);

@@ -28,6 +28,8 @@
 // (row id, length) + 8 B per row of y written; x gathered from L2/MALL.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "device_common.h"
 #include "hipspmv_internal.h"
 #include "kernels.h"
@@ -154,10 +156,9 @@ __device__ __forceinline__ T wave_ror1(T v) {
 // share of the rotation: chain_probe measured a register-fed add chain at
 // 4.3 cycles per add, and the v_readlane chain this replaces at 20.6.
 // Entries two stages ahead and gathers one stage ahead stay in flight.
-template <typename T>
+template <typename T, int G>
 __device__ __forceinline__ void hub_row_exact(const SellArgs& a, uint32_t w, int lane) {
 #pragma clang fp contract(off)
-  constexpr int G = kChainG;
   constexpr uint32_t S = 64 * G;
   const T* __restrict__ vals = static_cast<const T*>(a.csr_vals);
   const T* __restrict__ x = static_cast<const T*>(a.x);
@@ -212,6 +213,76 @@ __device__ __forceinline__ void hub_row_exact(const SellArgs& a, uint32_t w, int
       cA[j] = cB[j];
       vA[j] = vB[j];
     }
+  }
+  if (lane == 0) static_cast<T*>(a.y_out)[r] = acc;
+}
+
+// hub_row_exact with the gathers two stages ahead (experimental): at stage k
+// the products of k are in p, the gathers of k+1 have been in flight since
+// stage k-1, and the gathers of k+2 and the entries of k+3 are issued before
+// k's chain -- two chains of latency cover each gather.  Buffers rotate with
+// period 3 (unrolled, so no register copy waits on a load in flight).  The
+// adds are hub_row_exact's, in the same order: the same bits.
+template <typename T, int G>
+__device__ __forceinline__ void hub_row_exact2(const SellArgs& a, uint32_t w, int lane) {
+#pragma clang fp contract(off)
+  constexpr uint32_t S = 64 * G;
+  const T* __restrict__ vals = static_cast<const T*>(a.csr_vals);
+  const T* __restrict__ x = static_cast<const T*>(a.x);
+  const uint32_t r = a.hubs[w], base = a.rowptr[r], n = a.rowptr[r + 1] - base;
+  if (w < 4)
+    __builtin_amdgcn_s_setprio(3);
+  else if (w < 64)
+    __builtin_amdgcn_s_setprio(2);
+  else
+    __builtin_amdgcn_s_setprio(1);
+  uint32_t c[3][G];
+  T v[3][G], xs[3][G], p[G];
+  auto load = [&](uint32_t g0, uint32_t* cc, T* vv) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const uint32_t e = min(g0 + (uint32_t)lane * G + j, n - 1);
+      cc[j] = nt(a.colind + base + e);
+      vv[j] = nt(vals + base + e);
+    }
+  };
+  auto gather = [&](const uint32_t* cc, T* xx) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) xx[j] = x[cc[j]];
+  };
+  auto products = [&](uint32_t g0, const T* vv, const T* xx) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) p[j] = g0 + (uint32_t)lane * G + j < n ? vv[j] * xx[j] : T(-0.0);
+  };
+  load(0, c[0], v[0]);
+  load(S, c[1], v[1]);
+  gather(c[0], xs[0]);
+  products(0, v[0], xs[0]);
+  gather(c[1], xs[1]);
+  load(2 * S, c[2], v[2]);
+  T acc = a.beta ? static_cast<const T*>(a.y_in)[r] : T(0);
+  auto stage = [&](auto I, uint32_t g0) {
+    constexpr int i = decltype(I)::value, i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+    gather(c[i2], xs[i2]);   // stage k+2's gathers
+    load(g0 + 3 * S, c[i], v[i]);  // stage k+3's entries (buffer i is free: p holds stage k)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int l = 0; l < 64; ++l) {
+      T s = acc;
+#pragma unroll
+      for (int j = 0; j < G; ++j) s = s + p[j];
+      acc = wave_ror1(s);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    products(g0 + S, v[i1], xs[i1]);  // waits for stage k+1's gathers only
+  };
+  for (uint32_t g0 = 0; g0 < n; g0 += 3 * S) {
+    stage(std::integral_constant<int, 0>{}, g0);
+    if (g0 + S >= n) break;
+    stage(std::integral_constant<int, 1>{}, g0 + S);
+    if (g0 + 2 * S >= n) break;
+    stage(std::integral_constant<int, 2>{}, g0 + 2 * S);
   }
   if (lane == 0) static_cast<T*>(a.y_out)[r] = acc;
 }
@@ -336,15 +407,20 @@ __device__ __forceinline__ void slice_rows(const SellArgs& a, uint32_t s, int la
 }
 
 // Waves [0, H) take the hub work -- EXACT: the hub rows (longest first), one
-// wave each; otherwise the hub-row pieces -- and the rest one slice each.
-template <typename T, bool EXACT>
-__global__ __launch_bounds__(256) void k_sell(const SellArgs a) {
+// wave each, G entries per lane per chain stage; otherwise the hub-row pieces
+// -- and the rest one slice each.
+template <typename T, bool EXACT, int G, int D = 1>
+__device__ __forceinline__ void sell_wave(const SellArgs& a) {
   const int lane = threadIdx.x & 63;
   const uint32_t w = blockIdx.x * 4 + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t H = EXACT ? a.nhubs : a.npieces;
   if (w < H) {
-    if (EXACT)
-      hub_row_exact<T>(a, w, lane);
+    if (EXACT) {
+      if constexpr (D == 2)
+        hub_row_exact2<T, G>(a, w, lane);
+      else
+        hub_row_exact<T, G>(a, w, lane);
+    }
     else
       hub_piece<T>(a, w, lane);
     return;
@@ -359,10 +435,32 @@ __global__ __launch_bounds__(256) void k_sell(const SellArgs a) {
 }
 
 template <typename T, bool EXACT>
+__global__ __launch_bounds__(256) void k_sell(const SellArgs a) {
+  sell_wave<T, EXACT, kChainG>(a);
+}
+// experimental (option "sell_chain_g"): the ORDERED hub chain with G entries
+// per lane per stage -- the same adds in the same order, so the same bits
+template <int G, int D>
+__global__ __launch_bounds__(256) void k_sell_chain(const SellArgs a) {
+  sell_wave<double, true, G, D>(a);
+}
+
+template <typename T, bool EXACT>
 hipError_t launch(const SellArgs& a, hipStream_t s) {
   const uint64_t waves = (uint64_t)(EXACT ? a.nhubs : a.npieces) + a.nslices;
   if (waves == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_sell<T, EXACT>), dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+  const dim3 grid((uint32_t)((waves + 3) / 4));
+  if constexpr (EXACT) {
+    // option sell_chain = 10 * G + D (G entries per lane per stage, gathers D stages ahead)
+    switch (a.chain_g) {
+      case 82: hipLaunchKernelGGL((k_sell_chain<8, 2>), grid, dim3(256), 0, s, a); return hipGetLastError();
+      case 121: hipLaunchKernelGGL((k_sell_chain<12, 1>), grid, dim3(256), 0, s, a); return hipGetLastError();
+      case 122: hipLaunchKernelGGL((k_sell_chain<12, 2>), grid, dim3(256), 0, s, a); return hipGetLastError();
+      case 161: hipLaunchKernelGGL((k_sell_chain<16, 1>), grid, dim3(256), 0, s, a); return hipGetLastError();
+      default: break;
+    }
+  }
+  hipLaunchKernelGGL((k_sell<T, EXACT>), grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
