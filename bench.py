@@ -195,7 +195,7 @@ def kernel_stats_summary(path: str):
     return out
 
 
-def kernel_provenance(kname: str, dtype: str = "double", exact: bool = False):
+def kernel_provenance(kname: str, dtype: str = "double", exact: bool = False, iso: bool = False):
     """Machine-code fingerprint of the timed kernel (tools/kernel_isa.py over
     the libhipspmv.so this run loaded) and whether it equals the build that
     last passed `pytest -m gpu` on an MI355X (tests/golden/validated_isa.json)."""
@@ -207,6 +207,8 @@ def kernel_provenance(kname: str, dtype: str = "double", exact: bool = False):
             "wgather": f"void hipspmv::k_wgather<{dtype}, 17, 4, 2, true>",
             "sell": f"void hipspmv::(anonymous namespace)::k_sell<{dtype}, {'true' if exact else 'false'}>",
             "wcsr": f"void hipspmv::k_csr_vector<{dtype}, true>"}
+    if kname == "sell" and exact and iso:  # ORDERED with isolated hub chains (csrc/sell.hip k_sell_iso)
+        want["sell"] = "void hipspmv::(anonymous namespace)::k_sell_iso<12>"
     if kname not in want:
         return {"kernel": kname, "note": "not one of the GPU-validated product kernels"}
     fps = kernel_isa.fingerprints(os.path.join(hs.LIB_DIR, "libhipspmv.so"))
@@ -809,7 +811,8 @@ def main():
             "setup_ns_lib": setup_ns_lib,
         }
         try:  # reported, never fatal
-            out["roofline"]["kernel_provenance"] = kernel_provenance(kname)
+            out["roofline"]["kernel_provenance"] = kernel_provenance(
+                kname, exact=mode == hs.MODE_ORDERED, iso=kname == "sell" and h.stat("sell_iso_hubs") > 0)
         except Exception as e:
             out["roofline"]["kernel_provenance"] = {"error": f"{type(e).__name__}: {e}"}
         if rocprof is not None:

@@ -95,7 +95,7 @@ struct hipspmv_handle {
     uint32_t *d_width = nullptr, *d_row = nullptr, *d_len = nullptr, *d_col = nullptr, *d_hubs = nullptr;
     uint32_t *d_pieces = nullptr, *d_tickets = nullptr;
     uint64_t *d_vals = nullptr, *d_partial = nullptr;
-    uint32_t nslices = 0, nhubs = 0, npieces = 0;
+    uint32_t nslices = 0, nhubs = 0, npieces = 0, niso = 0;
     uint64_t padding = 0;
   } sell;
   uint64_t wc_segments = 0;  // segments the wcsr layout would have (counted at create for wide x, else 0)
@@ -120,7 +120,8 @@ struct hipspmv_handle {
   // option "sell_nt": SELL slices s >= sell_nt load their entries
   // non-temporally (-1 default: the second half of the slices)
   int64_t sell_nt = -1;
-  uint32_t sell_chain_g = 0;  // option "sell_chain" (experimental): ORDERED hub chain 10*G + D
+  int sell_only = 0;          // option "sell_only" (experimental timing probe)
+  uint32_t sell_chain_g = 0;  // option "sell_chain" (experimental): ORDERED hub chain form (0 product)
   void *d_x = nullptr, *d_y = nullptr;
   int kernel_opt = HIPSPMV_KERNEL_AUTO, mode_opt = HIPSPMV_MODE_ORDERED, timing = 0;
   // setup_ns: create (transpose, validation, uploads, every layout AUTO uses);
@@ -287,6 +288,7 @@ static int build_sell_layout(hipspmv_t* h, const HostCSR& a) {
   q.npieces = L.npieces;
   q.nslices = L.nslices;
   q.nhubs = L.nhubs;
+  q.niso = L.niso;
   q.padding = L.padding;
   q.built = true;
   return HIPSPMV_OK;
@@ -581,6 +583,13 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                q.d_pieces,  q.npieces,   q.d_partial, q.d_tickets};
     a.nt_from = h->sell_nt >= 0 ? (uint32_t)std::min<int64_t>(h->sell_nt, UINT32_MAX) : q.nslices / 2;
     a.chain_g = h->sell_chain_g;
+    a.niso = q.niso;
+    if (h->sell_only == 1) a.nslices = 0;  // experimental timing probe: the hub work alone
+    if (h->sell_only == 2) a.nhubs = a.npieces = 0;  // ... or the slices alone (y incomplete)
+    if (h->sell_only == 3)
+      a.nslices = 0, a.nhubs = std::min(a.nhubs, 1u), a.npieces = std::min(a.npieces, 1u),
+      a.niso = std::min(a.niso, 1u);
+    if (h->sell_only == 2) a.niso = 0;
     e = launch_sell(h->dtype, a, s);
   } else if (kernel == HIPSPMV_KERNEL_VCACHE || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ||
       kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
@@ -738,8 +747,13 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "wgather_chunk") {  // row blocks per k_wgather launch (0: all in one launch)
     if (value < 0 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->wgather_chunk = (uint32_t)value;
-  } else if (k == "sell_chain") {  // experimental ORDERED hub chain: 10*G + D (0: product)
-    if (value != 0 && value != 82 && value != 121 && value != 122 && value != 161) return HIPSPMV_ERR_INVALID_ARG;
+  } else if (k == "sell_only") {  // experimental timing probe: 1 hub work only, 2 slices only (y incomplete)
+    const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
+    if (value < 0 || value > 3) return HIPSPMV_ERR_INVALID_ARG;  // 3: the first (longest) hub row alone
+    if (value && !(exp && std::strcmp(exp, "1") == 0)) return HIPSPMV_ERR_UNSUPPORTED;
+    h->sell_only = (int)value;
+  } else if (k == "sell_chain") {  // experimental ORDERED hub chains: 1 none isolated, 2..4 G = 16/24/32
+    if (value < 0 || value > 4) return HIPSPMV_ERR_INVALID_ARG;
     const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
     if (value && !(exp && std::strcmp(exp, "1") == 0)) return HIPSPMV_ERR_UNSUPPORTED;
     h->sell_chain_g = (uint32_t)value;
@@ -876,6 +890,7 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "wcsr_window_log2") *out = h->wc.built ? h->wc.log2w : kWcLog2Window;
   else if (k == "sell_slices") *out = h->sell.nslices;
   else if (k == "sell_hubs") *out = h->sell.nhubs;
+  else if (k == "sell_iso_hubs") *out = h->sell.niso;
   else if (k == "sell_hub_pieces") *out = h->sell.npieces;
   else if (k == "sell_padding") *out = h->sell.padding;
   else if (k == "row_groups") *out = h->ngroups;

@@ -92,6 +92,13 @@ constexpr uint32_t kSellPiece = 4096;
 // ORDERED f64: a hub row's chain holds kChainG consecutive entries per lane per
 // stage of 64 * kChainG (csrc/sell.hip hub_row_exact; tools/sell_sim.cpp).
 constexpr int kChainG = 8;
+// ORDERED f64, k_sell_iso: hub rows of at least kSellIso entries get a
+// 1024-thread workgroup each -- one chain wave alone on its SIMD, fed from
+// LDS by 12 helper waves (csrc/sell.hip hub_row_isolated)
+constexpr uint32_t kSellIso = 8192;
+// products per chain lane per stage there: 12 * 64 = 768, one per helper
+// thread (C5 shard 0 ORDERED: 615.6 us; G = 16 / 24 / 32: 712 / 662 / 660 us)
+constexpr int kIsoG = 12;
 constexpr int kSellPieceWords = 8;
 
 // Column part h of a geometry with `split` parts owns panels
@@ -154,7 +161,7 @@ struct WinLayout {
 };
 
 struct SellLayout {
-  uint32_t nslices = 0, nhubs = 0;
+  uint32_t nslices = 0, nhubs = 0, niso = 0;
   std::vector<uint64_t> off;    // nslices + 1: first entry of each slice
   std::vector<uint32_t> width;  // nslices: longest row of the slice
   std::vector<uint32_t> row;    // nslices * kSellRows: row id (kSellNoRow past the window's rows)

@@ -264,6 +264,8 @@ void build_sell(const HostCSR& a, SellLayout& out) {
     }
   }
   out.npieces = (uint32_t)(out.pieces.size() / kSellPieceWords);
+  out.niso = 0;  // hubs[0, niso): long enough for a workgroup of their own (ORDERED, k_sell_iso)
+  while (out.niso < hubs.size() && a.rowptr[hubs[out.niso] + 1] - a.rowptr[hubs[out.niso]] >= kSellIso) ++out.niso;
   out.hubs = std::move(hubs);
   out.nhubs = (uint32_t)out.hubs.size();
   out.nslices = nslices;

@@ -217,74 +217,111 @@ __device__ __forceinline__ void hub_row_exact(const SellArgs& a, uint32_t w, int
   if (lane == 0) static_cast<T*>(a.y_out)[r] = acc;
 }
 
-// hub_row_exact with the gathers two stages ahead (experimental): at stage k
-// the products of k are in p, the gathers of k+1 have been in flight since
-// stage k-1, and the gathers of k+2 and the entries of k+3 are issued before
-// k's chain -- two chains of latency cover each gather.  Buffers rotate with
-// period 3 (unrolled, so no register copy waits on a load in flight).  The
-// adds are hub_row_exact's, in the same order: the same bits.
+// ORDERED f64, a hub row of at least kSellIso entries in a 1024-thread
+// workgroup of its own (k_sell_iso).  A wave64 f64 add issues over 4 cycles
+// of its SIMD, so a chain sharing its SIMD with other busy waves runs at a
+// fraction of its rate (C5 shard 0: the longest row alone 864 µs, among the
+// other hub waves 1478 µs).  Here wave 0 -- the chain -- is the only wave on
+// its SIMD that issues anything: waves 4, 8, 12 (the same SIMD) only meet the
+// barriers, and the other 12 waves, one product per thread per stage, load
+// the entries 4 stages ahead and gather x 2 stages ahead, and write stage i's
+// products to an LDS ring.  Lane l of the chain owns products l*G..l*G+G-1 of
+// a stage (slot j*64 + l: conflict-free reads) and the lanes hand the sum on
+// by DPP rotation, as hub_row_exact does: the same adds, in the same order,
+// so the same bits.  A 1024-thread workgroup also keeps the CU to itself (at
+// most 16 waves of this kernel fit a CU).
 template <typename T, int G>
-__device__ __forceinline__ void hub_row_exact2(const SellArgs& a, uint32_t w, int lane) {
+__device__ __forceinline__ void hub_row_isolated(const SellArgs& a, uint32_t hub) {
 #pragma clang fp contract(off)
-  constexpr uint32_t S = 64 * G;
+  constexpr int NB = 4, GA = 2;
+  constexpr uint32_t S = 64 * G;                  // products per stage
+  constexpr int PPT = (S + 767) / 768;            // per helper thread (768 helper threads)
+  __shared__ T ring[2][S];
   const T* __restrict__ vals = static_cast<const T*>(a.csr_vals);
   const T* __restrict__ x = static_cast<const T*>(a.x);
-  const uint32_t r = a.hubs[w], base = a.rowptr[r], n = a.rowptr[r + 1] - base;
-  if (w < 4)
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t r = a.hubs[hub], base = a.rowptr[r], n = a.rowptr[r + 1] - base;
+  const uint32_t nst = (n + S - 1) / S;
+  // LDS writes done, then the barrier; global loads stay in flight across it
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  if (wv == 0) {  // ---- the chain: stage i - 1 in iteration i
     __builtin_amdgcn_s_setprio(3);
-  else if (w < 64)
-    __builtin_amdgcn_s_setprio(2);
-  else
-    __builtin_amdgcn_s_setprio(1);
-  uint32_t c[3][G];
-  T v[3][G], xs[3][G], p[G];
-  auto load = [&](uint32_t g0, uint32_t* cc, T* vv) {
+    T acc = a.beta ? static_cast<const T*>(a.y_in)[r] : T(0);
+    barrier();  // iteration 0: the helpers produce stage 0
+    for (uint32_t i = 1; i <= nst; ++i) {
+      const T* slot = ring[(i - 1) & 1];
+      T p[G];
 #pragma unroll
-    for (int j = 0; j < G; ++j) {
-      const uint32_t e = min(g0 + (uint32_t)lane * G + j, n - 1);
-      cc[j] = nt(a.colind + base + e);
-      vv[j] = nt(vals + base + e);
+      for (int j = 0; j < G; ++j) p[j] = slot[j * 64 + lane];
+#pragma unroll
+      for (int l = 0; l < 64; ++l) {
+        T s = acc;
+#pragma unroll
+        for (int j = 0; j < G; ++j) s = s + p[j];
+        acc = wave_ror1(s);
+      }
+      barrier();
+    }
+    if (lane == 0) static_cast<T*>(a.y_out)[r] = acc;
+    return;
+  }
+  if ((wv & 3) == 0) {  // ---- the chain's SIMD: barriers only
+    for (uint32_t i = 0; i <= nst; ++i) barrier();
+    return;
+  }
+  // ---- helpers: thread ht makes products ht, ht + 768, ... (< S) of every stage
+  const uint32_t ht = (uint32_t)(wv - (wv >> 2) - 1) * 64 + lane;  // 12 waves -> [0, 768)
+  uint32_t c[NB][PPT];
+  T v[NB][PPT], xg[NB][PPT];
+  auto load = [&](uint32_t st, int k) {  // clamped: copies past the row are never used
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      const uint32_t e = min(st * S + min(ht + 768u * q, S - 1), n - 1);
+      c[k][q] = nt(a.colind + base + e);
+      v[k][q] = nt(vals + base + e);
     }
   };
-  auto gather = [&](const uint32_t* cc, T* xx) {
+  auto gather = [&](int k) {
 #pragma unroll
-    for (int j = 0; j < G; ++j) xx[j] = x[cc[j]];
+    for (int q = 0; q < PPT; ++q) xg[k][q] = x[c[k][q]];
   };
-  auto products = [&](uint32_t g0, const T* vv, const T* xx) {
 #pragma unroll
-    for (int j = 0; j < G; ++j) p[j] = g0 + (uint32_t)lane * G + j < n ? vv[j] * xx[j] : T(-0.0);
-  };
-  load(0, c[0], v[0]);
-  load(S, c[1], v[1]);
-  gather(c[0], xs[0]);
-  products(0, v[0], xs[0]);
-  gather(c[1], xs[1]);
-  load(2 * S, c[2], v[2]);
-  T acc = a.beta ? static_cast<const T*>(a.y_in)[r] : T(0);
-  auto stage = [&](auto I, uint32_t g0) {
-    constexpr int i = decltype(I)::value, i1 = (i + 1) % 3, i2 = (i + 2) % 3;
-    gather(c[i2], xs[i2]);   // stage k+2's gathers
-    load(g0 + 3 * S, c[i], v[i]);  // stage k+3's entries (buffer i is free: p holds stage k)
+  for (int k = 0; k < NB; ++k) load(k, k);
+#pragma unroll
+  for (int k = 0; k < GA; ++k) gather(k);
+  asm volatile("" ::: "memory");
+  auto iter = [&](auto K, uint32_t i) {
+    constexpr int k = decltype(K)::value, kg = (k + GA) % NB;
+    // stage i: the products (or -0.0 past the row, which leaves every sum as
+    // it is) into the slot of chain lane e / G, position e % G
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      const uint32_t e = ht + 768u * q;
+      if (q == 0 || e < S) ring[i & 1][(e % G) * 64 + e / G] = i * S + e < n ? v[k][q] * xg[k][q] : T(-0.0);
+    }
+    gather(kg);       // stage i + GA's gathers
+    load(i + NB, k);  // stage i + NB's entries
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int l = 0; l < 64; ++l) {
-      T s = acc;
-#pragma unroll
-      for (int j = 0; j < G; ++j) s = s + p[j];
-      acc = wave_ror1(s);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    products(g0 + S, v[i1], xs[i1]);  // waits for stage k+1's gathers only
+    barrier();
   };
-  for (uint32_t g0 = 0; g0 < n; g0 += 3 * S) {
-    stage(std::integral_constant<int, 0>{}, g0);
-    if (g0 + S >= n) break;
-    stage(std::integral_constant<int, 1>{}, g0 + S);
-    if (g0 + 2 * S >= n) break;
-    stage(std::integral_constant<int, 2>{}, g0 + 2 * S);
+  uint32_t i = 0;
+  for (; i + NB <= nst; i += NB) {
+    iter(std::integral_constant<int, 0>{}, i);
+    iter(std::integral_constant<int, 1>{}, i + 1);
+    iter(std::integral_constant<int, 2>{}, i + 2);
+    iter(std::integral_constant<int, 3>{}, i + 3);
   }
-  if (lane == 0) static_cast<T*>(a.y_out)[r] = acc;
+  // the last 0..3 stages (unrolled roles continue from i % NB == 0), then the
+  // chain's last iteration's barrier
+  if (i < nst) iter(std::integral_constant<int, 0>{}, i++);
+  if (i < nst) iter(std::integral_constant<int, 1>{}, i++);
+  if (i < nst) iter(std::integral_constant<int, 2>{}, i++);
+  barrier();
 }
 
 // FAST / u64: one piece of a hub row.  A row in several pieces is finished by
@@ -409,18 +446,14 @@ __device__ __forceinline__ void slice_rows(const SellArgs& a, uint32_t s, int la
 // Waves [0, H) take the hub work -- EXACT: the hub rows (longest first), one
 // wave each, G entries per lane per chain stage; otherwise the hub-row pieces
 // -- and the rest one slice each.
-template <typename T, bool EXACT, int G, int D = 1>
+template <typename T, bool EXACT, int G>
 __device__ __forceinline__ void sell_wave(const SellArgs& a) {
   const int lane = threadIdx.x & 63;
   const uint32_t w = blockIdx.x * 4 + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t H = EXACT ? a.nhubs : a.npieces;
   if (w < H) {
-    if (EXACT) {
-      if constexpr (D == 2)
-        hub_row_exact2<T, G>(a, w, lane);
-      else
-        hub_row_exact<T, G>(a, w, lane);
-    }
+    if (EXACT)
+      hub_row_exact<T, G>(a, w, lane);
     else
       hub_piece<T>(a, w, lane);
     return;
@@ -438,11 +471,35 @@ template <typename T, bool EXACT>
 __global__ __launch_bounds__(256) void k_sell(const SellArgs a) {
   sell_wave<T, EXACT, kChainG>(a);
 }
-// experimental (option "sell_chain_g"): the ORDERED hub chain with G entries
-// per lane per stage -- the same adds in the same order, so the same bits
-template <int G, int D>
-__global__ __launch_bounds__(256) void k_sell_chain(const SellArgs a) {
-  sell_wave<double, true, G, D>(a);
+// ORDERED f64 when some hub row has at least kSellIso entries: those rows
+// isolated (hub_row_isolated), the rest as k_sell does them, in 1024-thread
+// workgroups
+// Blocks: [0, niso) the isolated rows; then the other hub rows, 16 waves
+// (rows) a block; then the slices, 4 a block (waves 4-15 exit at once, so a
+// block's slices spread over as many CUs as k_sell's 256-thread blocks do:
+// 16 latency-bound slices on one CU ran 3.7x slower).
+template <int G>
+__global__ __launch_bounds__(1024) void k_sell_iso(const SellArgs a) {
+  if (blockIdx.x < a.niso) {
+    hub_row_isolated<double, G>(a, blockIdx.x);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t H = a.nhubs - a.niso, hb = (H + 15) / 16, b = blockIdx.x - a.niso;
+  if (b < hb) {
+    const uint32_t w = b * 16 + wv;
+    if (w < H) hub_row_exact<double, kChainG>(a, a.niso + w, lane);
+    return;
+  }
+  if (wv >= 4) return;
+  const uint32_t s = (b - hb) * 4 + wv;
+  if (s < a.nslices) {
+    if (s >= a.nt_from)
+      slice_rows<double, true>(a, s, lane);
+    else
+      slice_rows<double, false>(a, s, lane);
+  }
 }
 
 template <typename T, bool EXACT>
@@ -451,13 +508,19 @@ hipError_t launch(const SellArgs& a, hipStream_t s) {
   if (waves == 0) return hipSuccess;
   const dim3 grid((uint32_t)((waves + 3) / 4));
   if constexpr (EXACT) {
-    // option sell_chain = 10 * G + D (G entries per lane per stage, gathers D stages ahead)
-    switch (a.chain_g) {
-      case 82: hipLaunchKernelGGL((k_sell_chain<8, 2>), grid, dim3(256), 0, s, a); return hipGetLastError();
-      case 121: hipLaunchKernelGGL((k_sell_chain<12, 1>), grid, dim3(256), 0, s, a); return hipGetLastError();
-      case 122: hipLaunchKernelGGL((k_sell_chain<12, 2>), grid, dim3(256), 0, s, a); return hipGetLastError();
-      case 161: hipLaunchKernelGGL((k_sell_chain<16, 1>), grid, dim3(256), 0, s, a); return hipGetLastError();
-      default: break;
+    // isolated chains when some hub row is long enough (option sell_chain 1: never;
+    // 2..4, experimental: stages of G = 16, 24, 32 instead of kIsoG)
+    if (a.niso > 0 && a.chain_g != 1) {
+      const dim3 g((uint32_t)(a.niso + (a.nhubs - a.niso + 15) / 16 + (a.nslices + 3) / 4));
+      if (a.chain_g == 2)
+        hipLaunchKernelGGL(k_sell_iso<16>, g, dim3(1024), 0, s, a);
+      else if (a.chain_g == 3)
+        hipLaunchKernelGGL(k_sell_iso<24>, g, dim3(1024), 0, s, a);
+      else if (a.chain_g == 4)
+        hipLaunchKernelGGL(k_sell_iso<32>, g, dim3(1024), 0, s, a);
+      else
+        hipLaunchKernelGGL(k_sell_iso<kIsoG>, g, dim3(1024), 0, s, a);
+      return hipGetLastError();
     }
   }
   hipLaunchKernelGGL((k_sell<T, EXACT>), grid, dim3(256), 0, s, a);

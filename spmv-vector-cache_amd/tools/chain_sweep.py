@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""ORDERED k_sell on a C5 shard: the product hub chain (kChainG entries per
-lane per stage) against the experimental forms of option "sell_chain" (10 * G + D: G entries per lane
-per stage, gathers D stages ahead)
-(needs HIPSPMV_EXPERIMENTAL=1).  Every form adds the same products in the
-same order, so the bits must match the product's.  Not part of the product.
+"""ORDERED k_sell on a C5 shard: the product (hub rows of >= kSellIso entries
+as isolated chains, k_sell_iso<kIsoG>) against the forms of option
+"sell_chain" (needs HIPSPMV_EXPERIMENTAL=1): 1 no isolated chains (k_sell),
+2..4 isolated chains with G = 16 / 24 / 32 products per lane per stage.
+Every form adds the same products in the same order, so the bits must match
+the product's.  Then the hub rows alone, the longest row alone and the slices
+alone (timing only).  Not part of the product.
 
     HIPSPMV_EXPERIMENTAL=1 python tools/chain_sweep.py [--shard 0]
 """
@@ -33,8 +35,8 @@ alg = 12 * colind.size + 4 * (rows + 1) + 8 * cols + 8 * rows
 h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
 h.set_kernel("sell")
 ref = None
-for rnd in range(2):
-    for g in (0, 82, 121, 122, 161):
+for rnd in range(1):
+    for g in (0, 1, 2, 3, 4):
         h.set_option("sell_chain", g)
         for _ in range(2):
             h.exec_device(x, y, beta=0, mode=hs.MODE_ORDERED, stream=s)
@@ -48,6 +50,24 @@ for rnd in range(2):
         yy = y.cpu().numpy().copy()
         ref = yy if ref is None else ref
         same = yy.tobytes() == ref.tobytes()
-        print(f"round {rnd} shard {a.shard} chain {'G=%d D=%d' % (g // 10, g % 10) if g else 'product G=8 D=1'}: {us:8.1f} us  frac8TB={alg / us / 1e3 / 8000:.4f}"
+        print(f"round {rnd} shard {a.shard} chain {('product (isolated G=12)', 'not isolated (k_sell)', 'isolated G=16', 'isolated G=24', 'isolated G=32')[g]}: {us:8.1f} us  frac8TB={alg / us / 1e3 / 8000:.4f}"
               f"  {'bit-identical to product' if same else 'BITS DIFFER'}", flush=True)
+# where the time goes: the hub chains alone, the slices alone (timing only)
+for only, label in ((1, "hub rows only"), (3, "longest row only"), (2, "slices only")):
+    for g in ((0, 1) if only != 2 else (0,)):
+        h.set_option("sell_chain", g)
+        h.set_option("sell_only", only)
+        for _ in range(2):
+            h.exec_device(x, y, beta=0, mode=hs.MODE_ORDERED, stream=s)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(a.reps):
+            h.exec_device(x, y, beta=0, mode=hs.MODE_ORDERED, stream=s)
+        e1.record(s)
+        torch.cuda.synchronize()
+        print(f"{label:14s} chain {g or 'product'}: {e0.elapsed_time(e1) / a.reps * 1e3:8.1f} us", flush=True)
+    h.set_option("sell_only", 0)
+lens = np.diff(rowptr.astype(np.int64))
+top = np.sort(lens)[::-1][:12]
+print("isolated hub rows:", h.stat("sell_iso_hubs"), "longest rows:", top.tolist(), "rows > 256:", int(np.sum(lens > 256)), "rows > 32768:", int(np.sum(lens > 32768)))
 h.close()

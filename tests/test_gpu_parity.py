@@ -663,6 +663,36 @@ def test_sell_split_hub_rows_fast(gpu):
     hu.close()
 
 
+def test_sell_isolated_hub_chains_ordered(gpu):
+    # ORDERED hub rows of >= 8192 entries (kSellIso) run as isolated chains,
+    # one 1024-thread workgroup each, fed from LDS by helper waves
+    # (hub_row_isolated): the oracle's bits at stage-boundary lengths (the
+    # stages hold 64*G products), just below the threshold, and beside empty
+    # rows and short-row slices
+    rng = np.random.default_rng(29)
+    rows, cols = 900, 120000
+    lens = rng.integers(0, 40, rows)
+    lens[[0, 5, 6, 7, 400, 899]] = [100001, 8191, 8192, 8193, 30720, 20481]
+    lens[[1, 2]] = 0
+    rowptr = np.zeros(rows + 1, np.uint32)
+    rowptr[1:] = np.cumsum(lens)
+    colind = np.concatenate([np.sort(rng.choice(cols, n, replace=False)) for n in lens]).astype(np.uint32)
+    vals = rng.uniform(-1, 1, colind.size)
+    x = rng.uniform(-1, 1, cols)
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+    h.set_kernel("sell")
+    assert h.stat("sell_iso_hubs") == 5
+    colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+    for beta in (0, 1):
+        y0 = rng.uniform(-1, 1, rows)
+        y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else None), rows=rows)
+        for _ in range(2):
+            y = h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_ORDERED)
+            bad = np.nonzero(y.view(np.uint64) != y_ref.view(np.uint64))[0]
+            assert bad.size == 0, (beta, bad[:8], lens[bad[:8]])
+    h.close()
+
+
 def test_exec_device_rejects_bad_tensors(gpu):
     import torch
     rows, cols, colptr, rowind, vals = fx.load("circuit204")
