@@ -102,9 +102,9 @@ struct hipspmv_handle {
   struct Wc {  // wcsr: the column-windowed segment matrix (built when AUTO picks it, else on first selection)
     bool built = false;
     uint32_t *d_rowptr = nullptr, *d_colind = nullptr, *d_groups = nullptr, *d_rowseg = nullptr,
-             *d_segidx = nullptr, *d_rgroups = nullptr;
+             *d_segidx = nullptr, *d_rgroups = nullptr, *d_chunks = nullptr;
     uint64_t *d_vals = nullptr, *d_ypart = nullptr;
-    uint32_t nseg = 0, ngroups = 0, rgroups = 0, max_seg = 0, log2w = 0;
+    uint32_t nseg = 0, ngroups = 0, rgroups = 0, max_seg = 0, log2w = 0, nchunks = 0;
   } wc;
   int vcache_dma = -1;   // option "vcache_dma": LDS-DMA x loader (-1 default: on for the split geometry)
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
@@ -175,7 +175,7 @@ static void release(hipspmv_t* h) {
   }
   {
     auto& w = h->wc;
-    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_vals, w.d_ypart};
+    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart};
     for (void* p : wp)
       if (p) (void)hipFree(p);
   }
@@ -299,13 +299,42 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   auto& w = h->wc;
   if (w.built) return HIPSPMV_OK;
   DeviceGuard g(h->device);
+  // the global-x form (windows of 2^kWcLog2Window), or with HIPSPMV_WCSR_LDS=1
+  // the LDS form (k_wseg: x windows of 2^kWsLog2Window staged in LDS; slower
+  // on every C5 shard measured)
+  const char* lds_env = std::getenv("HIPSPMV_WCSR_LDS");
+  const bool lds = lds_env && std::strcmp(lds_env, "1") == 0;
   WinLayout L;
-  build_windowed(a, kWcLog2Window, L);
-  std::vector<uint32_t> groups;
-  build_row_groups(L.seg, groups);
+  build_windowed(a, lds ? kWsLog2Window : kWcLog2Window, L);
+  std::vector<uint32_t> groups, chunks;
+  if (lds) {  // csr_vector groups inside each window, cut into chunks of <= kWsChunkNnz entries
+    const auto& rp = L.seg.rowptr;
+    for (uint32_t win = 0; win + 1 < L.winseg.size(); ++win) {
+      const uint32_t s0 = L.winseg[win], s1 = L.winseg[win + 1];
+      if (s0 == s1) continue;
+      std::vector<uint32_t> wg;
+      build_row_groups(rp.data() + s0, s1 - s0, wg);
+      uint32_t cg = (uint32_t)groups.size(), cnnz = 0;
+      for (size_t i = 0; i + 1 < wg.size(); ++i) {
+        const uint32_t n = rp[s0 + wg[i + 1]] - rp[s0 + wg[i]];
+        if (cnnz && cnnz + n > kWsChunkNnz) {
+          chunks.insert(chunks.end(), {win, cg, (uint32_t)groups.size()});
+          cg = (uint32_t)groups.size();
+          cnnz = 0;
+        }
+        groups.push_back(s0 + wg[i]);
+        cnnz += n;
+      }
+      chunks.insert(chunks.end(), {win, cg, (uint32_t)groups.size()});
+    }
+    groups.push_back(L.nseg);
+  } else {
+    build_row_groups(L.seg, groups);
+  }
   const uint64_t bytes0 = h->device_bytes;
   auto fail = [&](int st) {
-    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_vals, w.d_ypart};
+    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx,
+                  w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart};
     for (void* p : wp)
       if (p) (void)hipFree(p);
     w = hipspmv_handle::Wc{};
@@ -317,6 +346,9 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   if ((st = dev_upload(&w.d_colind, L.seg.colind.data(), L.seg.colind.size(), h->device_bytes))) return fail(st);
   if ((st = dev_upload(&w.d_vals, L.seg.vals.data(), L.seg.vals.size(), h->device_bytes))) return fail(st);
   if ((st = dev_upload(&w.d_groups, groups.data(), groups.size(), h->device_bytes))) return fail(st);
+  if (!chunks.empty() && (st = dev_upload(&w.d_chunks, chunks.data(), chunks.size(), h->device_bytes)))
+    return fail(st);
+  w.nchunks = (uint32_t)(chunks.size() / 3);
   if ((st = dev_upload(&w.d_rowseg, L.rowseg.data(), L.rowseg.size(), h->device_bytes))) return fail(st);
   if ((st = dev_upload(&w.d_segidx, L.segidx.data(), L.segidx.size(), h->device_bytes))) return fail(st);
   {  // the reduce is a csr_vector over (rowseg, segidx) with ypart as x: its own balanced row groups
@@ -632,6 +664,9 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     const auto& w = h->wc;
     WcsrArgs a{w.d_rowptr, w.d_colind, w.d_vals, w.d_groups, w.ngroups, w.d_rowseg, w.d_segidx,
                w.d_rgroups, w.rgroups,   w.d_ypart, d_x,      d_y_in,     d_y_out,  h->rows, beta};
+    a.chunks = w.d_chunks;
+    a.nchunks = w.nchunks;
+    a.cols = h->cols;
     e = launch_wcsr(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
@@ -888,6 +923,7 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "wcsr_segments") *out = h->wc.built ? h->wc.nseg : h->wc_segments;
   else if (k == "wcsr_max_segment") *out = h->wc.max_seg;
   else if (k == "wcsr_window_log2") *out = h->wc.built ? h->wc.log2w : kWcLog2Window;
+  else if (k == "wcsr_chunks") *out = h->wc.nchunks;
   else if (k == "sell_slices") *out = h->sell.nslices;
   else if (k == "sell_hubs") *out = h->sell.nhubs;
   else if (k == "sell_iso_hubs") *out = h->sell.niso;

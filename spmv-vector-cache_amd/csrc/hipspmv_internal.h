@@ -65,6 +65,11 @@ constexpr uint32_t kVcRunMax = 16;
 // window order (k_wreduce).
 constexpr uint32_t kWcLog2Window = 16;
 // AUTO considers wcsr from this many columns (x of 16 MiB: four XCD L2s)
+// wcsr LDS form (k_wseg, opt-in HIPSPMV_WCSR_LDS=1): x windows of 2^14 f64
+// (128 KiB of LDS), chunks of at most kWsChunkNnz entries of one window per
+// 1024-thread workgroup
+constexpr uint32_t kWsLog2Window = 14;
+constexpr uint32_t kWsChunkNnz = 49152;
 constexpr uint32_t kWcMinCols = 1u << 21;
 
 // ---- csr_vector geometry ---------------------------------------------------
@@ -155,6 +160,7 @@ struct VcacheLayout {
 
 struct WinLayout {
   uint32_t log2w = 0, nseg = 0, max_seg = 0;
+  std::vector<uint32_t> winseg;  // windows + 1: window w's segments are [winseg[w], winseg[w+1])
   HostCSR seg;                  // A': rows = segments (window-major, then row), cols = the matrix's
   std::vector<uint32_t> rowseg; // rows + 1: row r's segments are segidx[rowseg[r] .. rowseg[r+1])
   std::vector<uint32_t> segidx; // nseg: segment ids of each row, in window order

@@ -55,6 +55,9 @@ struct WcsrArgs {  // csr_vector over the column-windowed segment matrix, then k
   void* y_out;
   uint32_t rows;
   int beta;
+  const uint32_t* chunks = nullptr;  // LDS form (k_wseg): (window, first group, end group) per workgroup
+  uint32_t nchunks = 0;
+  uint32_t cols = 0;
 };
 
 struct SellArgs {

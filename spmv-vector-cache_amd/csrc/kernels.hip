@@ -80,24 +80,19 @@ __device__ __forceinline__ T wave_segscan(T v, uint32_t f) {
 // current x window out of L2 (§6.10).  KIND 2: the wcsr reduce -- no values,
 // each "entry" adds x[colind[e]] (a segment partial), so the same balanced
 // groups and segmented scan sum every row's partials in a fixed order.
-template <typename T, int KIND>
-__device__ __forceinline__ void csr_vector_group(const uint32_t* __restrict__ rowptr,
-                                                 const uint32_t* __restrict__ colind, const T* __restrict__ vals,
-                                                 const T* __restrict__ x, const T* __restrict__ y_in,
-                                                 T* __restrict__ y_out, const uint32_t* __restrict__ groups,
-                                                 uint32_t ngroups, int beta) {
+template <typename T, int KIND, typename XF>
+__device__ __forceinline__ void csr_vector_rows(const uint32_t* __restrict__ rowptr,
+                                                const uint32_t* __restrict__ colind, const T* __restrict__ vals,
+                                                XF xv, const T* __restrict__ y_in, T* __restrict__ y_out,
+                                                uint32_t r0, uint32_t r1, int beta, uint32_t* heads) {
 #pragma clang fp contract(off)
-  __shared__ uint32_t heads[4][kCvGroupNnz / 32];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t g = blockIdx.x * 4 + w;
-  if (g >= ngroups) return;  // wave-uniform; no workgroup barriers below
-  const uint32_t r0 = groups[g], r1 = groups[g + 1];
+  const int lane = threadIdx.x & 63;
   const uint32_t base = rowptr[r0], n = rowptr[r1] - base;
-  auto ci = [&](uint32_t e) { return KIND == 1 ? __builtin_nontemporal_load(colind + e) : colind[e]; };
+  auto ci = [&](uint32_t e) { return KIND == 1 || KIND == 3 ? __builtin_nontemporal_load(colind + e) : colind[e]; };
   // the e-th term of the group's sums: a rounded product, or a partial
   auto term = [&](uint32_t e) -> T {
-    if constexpr (KIND == 2) return x[ci(e)];
-    else return (KIND == 1 ? __builtin_nontemporal_load(vals + e) : vals[e]) * x[ci(e)];
+    if constexpr (KIND == 2) return xv(ci(e));
+    else return (KIND == 1 || KIND == 3 ? __builtin_nontemporal_load(vals + e) : vals[e]) * xv(ci(e));
   };
 
   if (r1 - r0 == 1 && n > (uint32_t)kCvGroupNnz) {
@@ -124,10 +119,10 @@ __device__ __forceinline__ void csr_vector_group(const uint32_t* __restrict__ ro
     rs = rowptr[r0 + lane] - base;
     re = rowptr[r0 + lane + 1] - base;
   }
-  if (lane < kCvGroupNnz / 32) heads[w][lane] = 0;
+  if (lane < kCvGroupNnz / 32) heads[lane] = 0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  if (own && re > rs) atomicOr(&heads[w][rs >> 5], 1u << (rs & 31));
+  if (own && re > rs) atomicOr(&heads[rs >> 5], 1u << (rs & 31));
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
   T carry = T(0);
@@ -137,7 +132,7 @@ __device__ __forceinline__ void csr_vector_group(const uint32_t* __restrict__ ro
     uint32_t f = 0;
     if (e < n) {
       p = term(base + e);
-      f = (heads[w][e >> 5] >> (e & 31)) & 1u;
+      f = (heads[e >> 5] >> (e & 31)) & 1u;
     }
     if (lane == 0 && !f) p = carry + p;
     p = wave_segscan(p, f);
@@ -147,6 +142,50 @@ __device__ __forceinline__ void csr_vector_group(const uint32_t* __restrict__ ro
     carry = __shfl(p, 63);
   }
   if (own && re == rs) y_out[r0 + lane] = beta ? y_in[r0 + lane] : T(0);
+}
+
+// One wave's row group of y = A*x (plus y_in when beta).  KIND 0: plain
+// csr_vector.  KIND 1: the wcsr segment pass -- entry
+// (colind, vals) loads non-temporal, so the streamed entries do not push the
+// current x window out of L2 (§6.10).  KIND 2: the wcsr reduce -- no values,
+// each "entry" adds x[colind[e]] (a segment partial), so the same balanced
+// groups and segmented scan sum every row's partials in a fixed order.
+// (KIND 3, k_wseg: entries non-temporal, x from an LDS window.)
+template <typename T, int KIND>
+__device__ __forceinline__ void csr_vector_group(const uint32_t* __restrict__ rowptr,
+                                                 const uint32_t* __restrict__ colind, const T* __restrict__ vals,
+                                                 const T* __restrict__ x, const T* __restrict__ y_in,
+                                                 T* __restrict__ y_out, const uint32_t* __restrict__ groups,
+                                                 uint32_t ngroups, int beta) {
+  __shared__ uint32_t heads[4][kCvGroupNnz / 32];
+  const int w = threadIdx.x >> 6;
+  const uint32_t g = blockIdx.x * 4 + w;
+  if (g >= ngroups) return;  // wave-uniform; no workgroup barriers below
+  csr_vector_rows<T, KIND>(rowptr, colind, vals, [&](uint32_t c) { return x[c]; }, y_in, y_out, groups[g],
+                           groups[g + 1], beta, heads[w]);
+}
+
+// k_wseg (wcsr, LDS form): one chunk of one column window's segments per
+// 1024-thread workgroup.  The window's 2^kWsLog2Window x values are staged in
+// LDS once, then 16 waves run csr_vector groups over the chunk's segments
+// with every gather served from LDS -- no L1/L2 request per gather.
+template <typename T>
+__global__ __launch_bounds__(1024) void k_wseg(const uint32_t* __restrict__ chunks,
+                                               const uint32_t* __restrict__ groups,
+                                               const uint32_t* __restrict__ rowptr,
+                                               const uint32_t* __restrict__ colind, const T* __restrict__ vals,
+                                               const T* __restrict__ x, uint32_t cols, T* __restrict__ ypart) {
+  __shared__ T xw[1u << kWsLog2Window];
+  __shared__ uint32_t heads[16][kCvGroupNnz / 32];
+  const uint32_t* ck = chunks + 3 * (size_t)blockIdx.x;
+  const uint32_t win = ck[0], g0 = ck[1], g1 = ck[2];
+  const uint32_t c0 = win << kWsLog2Window, nc = min(1u << kWsLog2Window, cols - c0);
+  for (uint32_t i = threadIdx.x; i < nc; i += 1024) xw[i] = x[c0 + i];
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  for (uint32_t g = g0 + (uint32_t)w; g < g1; g += 16)
+    csr_vector_rows<T, 3>(rowptr, colind, vals, [&](uint32_t c) { return xw[c - c0]; }, (const T*)nullptr, ypart,
+                          groups[g], groups[g + 1], 0, heads[w]);
 }
 
 // NTE: the wcsr segment pass (KIND 1 above)
@@ -189,8 +228,12 @@ hipError_t launch_csr_vector(const CsrArgs& a, hipStream_t s) {
 
 template <typename T>
 hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
-  // the segment partials: csr_vector over A', beta 0, entries non-temporal
-  if (a.ngroups)
+  // the segment partials: csr_vector over A', beta 0, entries non-temporal;
+  // the LDS form when the layout has window chunks
+  if (a.nchunks)
+    hipLaunchKernelGGL(k_wseg<T>, dim3(a.nchunks), dim3(1024), 0, s, a.chunks, a.groups, a.seg_rowptr, a.seg_colind,
+                       (const T*)a.seg_vals, (const T*)a.x, a.cols, (T*)a.ypart);
+  else if (a.ngroups)
     hipLaunchKernelGGL((k_csr_vector<T, true>), dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr,
                        a.seg_colind, (const T*)a.seg_vals, (const T*)a.x, (const T*)nullptr, (T*)a.ypart,
                        a.groups, a.ngroups, 0);

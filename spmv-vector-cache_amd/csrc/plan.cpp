@@ -310,6 +310,7 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out) {
   }
   for (uint32_t w = 0; w < nwin; ++w) wstart[w + 1] += wstart[w];
   out.nseg = (uint32_t)wstart[nwin];
+  out.winseg.assign(wstart.begin(), wstart.end());
   // pass 2: each segment's id (rows ascend, so ids ascend within a window) and length
   std::vector<uint64_t> cursor(wstart.begin(), wstart.end() - 1);
   std::vector<uint32_t> len(out.nseg, 0);

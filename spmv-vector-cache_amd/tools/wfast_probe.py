@@ -31,6 +31,7 @@ p.add_argument("--shard", type=int, default=0)
 p.add_argument("--windows", default="17,19,21")
 p.add_argument("--c4", action="store_true", help="C4 shard (stripe 2^21 x 2^24, 32 nnz/row) instead of R-MAT")
 p.add_argument("--reps", type=int, default=20)
+p.add_argument("--only-wcsr", action="store_true", help="time the wcsr kernel only")
 a = p.parse_args()
 
 t0 = time.time()
@@ -62,13 +63,15 @@ def timeit(h, mode, yd):
 alg = 12 * colind.size + 4 * (rows + 1) + 8 * cols + 8 * rows
 h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
 y = torch.empty(rows, dtype=torch.float64, device="cuda")
-for k in ("sell", "csr_vector", "wgather", "wcsr"):
+for k in (("wcsr",) if a.only_wcsr else ("sell", "csr_vector", "wgather", "wcsr")):
     try:
         h.set_kernel(k)
     except hs.HipSpMVError:
         continue
     us = timeit(h, hs.MODE_FAST, y)
-    print(f"A  {k:10s} FAST {us:8.1f} us  frac8TB={alg / us / 1e3 / 8000:.3f}", flush=True)
+    extra = (f" (window 2^{h.stat('wcsr_window_log2')}, {h.stat('wcsr_segments')} segments, "
+             f"{h.stat('wcsr_chunks')} LDS chunks)") if k == "wcsr" else ""
+    print(f"A  {k:10s} FAST {us:8.1f} us  frac8TB={alg / us / 1e3 / 8000:.3f}{extra}", flush=True)
 h.close()
 
 lens = np.diff(rowptr.astype(np.int64))
