@@ -126,20 +126,47 @@ __device__ __forceinline__ void csr_vector_rows(const uint32_t* __restrict__ row
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
   T carry = T(0);
-  for (uint32_t pb = 0; pb < n; pb += 64) {
-    const uint32_t e = pb + lane;
-    T p = T(0);
-    uint32_t f = 0;
-    if (e < n) {
-      p = term(base + e);
-      f = (heads[e >> 5] >> (e & 31)) & 1u;
+  if constexpr (KIND == 3) {
+    // k_wseg: every term of the group (<= 256) is loaded before the scans, so
+    // a wave keeps four entry loads in flight instead of one per round trip
+    // (the LDS form 359.7 -> 322.4 us on C5 shard 0; the same in the global
+    // form, KIND 1, measured slower: 264.5 -> 270.8 us)
+    constexpr int Q = kCvGroupNnz / 64;
+    T pv[Q];
+    if (n) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) pv[q] = term(base + min((uint32_t)(q * 64 + lane), n - 1));
     }
-    if (lane == 0 && !f) p = carry + p;
-    p = wave_segscan(p, f);
-    const uint32_t last = re - 1;  // this lane's row's final element (if its row is non-empty)
-    const T tot = __shfl(p, (int)((last - pb) & 63));
-    if (own && re > rs && last >= pb && last < pb + 64) y_out[r0 + lane] = beta ? y_in[r0 + lane] + tot : tot;
-    carry = __shfl(p, 63);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const uint32_t pb = (uint32_t)q * 64;
+      if (pb >= n) break;
+      const uint32_t e = pb + lane;
+      T p = e < n ? pv[q] : T(0);
+      const uint32_t f = e < n ? (heads[e >> 5] >> (e & 31)) & 1u : 0u;
+      if (lane == 0 && !f) p = carry + p;
+      p = wave_segscan(p, f);
+      const uint32_t last = re - 1;
+      const T tot = __shfl(p, (int)((last - pb) & 63));
+      if (own && re > rs && last >= pb && last < pb + 64) y_out[r0 + lane] = beta ? y_in[r0 + lane] + tot : tot;
+      carry = __shfl(p, 63);
+    }
+  } else {
+    for (uint32_t pb = 0; pb < n; pb += 64) {
+      const uint32_t e = pb + lane;
+      T p = T(0);
+      uint32_t f = 0;
+      if (e < n) {
+        p = term(base + e);
+        f = (heads[e >> 5] >> (e & 31)) & 1u;
+      }
+      if (lane == 0 && !f) p = carry + p;
+      p = wave_segscan(p, f);
+      const uint32_t last = re - 1;  // this lane's row's final element (if its row is non-empty)
+      const T tot = __shfl(p, (int)((last - pb) & 63));
+      if (own && re > rs && last >= pb && last < pb + 64) y_out[r0 + lane] = beta ? y_in[r0 + lane] + tot : tot;
+      carry = __shfl(p, 63);
+    }
   }
   if (own && re == rs) y_out[r0 + lane] = beta ? y_in[r0 + lane] : T(0);
 }
