@@ -208,7 +208,7 @@ def kernel_provenance(kname: str, dtype: str = "double", exact: bool = False, is
             "sell": f"void hipspmv::(anonymous namespace)::k_sell<{dtype}, {'true' if exact else 'false'}>",
             "wcsr": f"void hipspmv::k_csr_vector<{dtype}, true>"}
     if kname == "sell" and exact and iso:  # ORDERED with isolated hub chains (csrc/sell.hip k_sell_iso)
-        want["sell"] = "void hipspmv::(anonymous namespace)::k_sell_iso<12>"
+        want["sell"] = "void hipspmv::(anonymous namespace)::k_sell_iso<45>"
     if kname not in want:
         return {"kernel": kname, "note": "not one of the GPU-validated product kernels"}
     fps = kernel_isa.fingerprints(os.path.join(hs.LIB_DIR, "libhipspmv.so"))

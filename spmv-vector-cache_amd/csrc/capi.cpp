@@ -787,8 +787,8 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
     if (value < 0 || value > 3) return HIPSPMV_ERR_INVALID_ARG;  // 3: the first (longest) hub row alone
     if (value && !(exp && std::strcmp(exp, "1") == 0)) return HIPSPMV_ERR_UNSUPPORTED;
     h->sell_only = (int)value;
-  } else if (k == "sell_chain") {  // experimental ORDERED hub chains: 1 none isolated, 2..4 G = 16/24/32
-    if (value < 0 || value > 4) return HIPSPMV_ERR_INVALID_ARG;
+  } else if (k == "sell_chain") {  // experimental ORDERED hub chains: 1 none isolated, 2 / 3: G = 12 / 30
+    if (value < 0 || value > 3) return HIPSPMV_ERR_INVALID_ARG;
     const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
     if (value && !(exp && std::strcmp(exp, "1") == 0)) return HIPSPMV_ERR_UNSUPPORTED;
     h->sell_chain_g = (uint32_t)value;

@@ -101,9 +101,11 @@ constexpr int kChainG = 8;
 // 1024-thread workgroup each -- one chain wave alone on its SIMD, fed from
 // LDS by 12 helper waves (csrc/sell.hip hub_row_isolated)
 constexpr uint32_t kSellIso = 8192;
-// products per chain lane per stage there: 12 * 64 = 768, one per helper
-// thread (C5 shard 0 ORDERED: 615.6 us; G = 16 / 24 / 32: 712 / 662 / 660 us)
-constexpr int kIsoG = 12;
+// products per chain lane per stage there: 45 * 64 = 2880, three per
+// helper thread (all 15 other waves help; C5 shard 0 ORDERED 461 us, the
+// longest row's chain at 4.6 cycles per add; G = 12 with 12 helper waves:
+// 579-616 us)
+constexpr int kIsoG = 45;
 constexpr int kSellPieceWords = 8;
 
 // Column part h of a geometry with `split` parts owns panels

@@ -83,7 +83,7 @@ struct SellArgs {
   uint32_t* tickets = nullptr;  // per split row, zero between launches
   uint32_t nt_from = 0;         // slices s >= nt_from load their entries non-temporally
   uint32_t niso = 0;            // hubs[0, niso): isolated chains (k_sell_iso)
-  uint32_t chain_g = 0;         // exact: 0 product; 1 no isolated chains; 2..4 isolated stages of G = 16/24/32 (experimental)
+  uint32_t chain_g = 0;         // exact: 0 product; 1 no isolated chains; 2 / 3 isolated stages of G = 12 / 30 (experimental)
 };
 
 hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);

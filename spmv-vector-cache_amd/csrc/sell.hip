@@ -221,22 +221,29 @@ __device__ __forceinline__ void hub_row_exact(const SellArgs& a, uint32_t w, int
 // workgroup of its own (k_sell_iso).  A wave64 f64 add issues over 4 cycles
 // of its SIMD, so a chain sharing its SIMD with other busy waves runs at a
 // fraction of its rate (C5 shard 0: the longest row alone 864 µs, among the
-// other hub waves 1478 µs).  Here wave 0 -- the chain -- is the only wave on
-// its SIMD that issues anything: waves 4, 8, 12 (the same SIMD) only meet the
-// barriers, and the other 12 waves, one product per thread per stage, load
-// the entries 4 stages ahead and gather x 2 stages ahead, and write stage i's
-// products to an LDS ring.  Lane l of the chain owns products l*G..l*G+G-1 of
-// a stage (slot j*64 + l: conflict-free reads) and the lanes hand the sum on
-// by DPP rotation, as hub_row_exact does: the same adds, in the same order,
-// so the same bits.  A 1024-thread workgroup also keeps the CU to itself (at
-// most 16 waves of this kernel fit a CU).
+// other hub waves 1478 µs).  Here wave 0 runs the chain and nothing else;
+// the helper waves -- all 15 others when G is a multiple of 15 (the product,
+// kIsoG = 45), else the 12 off the chain's SIMD while waves 4, 8, 12 only
+// meet the barriers -- load the entries NB stages ahead, gather x two stages
+// ahead and write stage i's products to an LDS ring.  Lane l of the chain
+// owns products l*G..l*G+G-1 of a stage (slot j*65 + l: conflict-free reads,
+// and the padding spreads the helpers' writes over the banks) and the lanes
+// hand the sum on by DPP rotation, as hub_row_exact does: the same adds, in
+// the same order, so the same bits.  At most 20 waves of this kernel fit a
+// CU, so a 1024-thread workgroup keeps its CU to itself.
 template <typename T, int G>
 __device__ __forceinline__ void hub_row_isolated(const SellArgs& a, uint32_t hub) {
 #pragma clang fp contract(off)
-  constexpr int NB = 4, GA = 2;
+  constexpr int GA = 2;
   constexpr uint32_t S = 64 * G;                  // products per stage
-  constexpr int PPT = (S + 767) / 768;            // per helper thread (768 helper threads)
-  __shared__ T ring[2][S];
+  // helper threads: waves off the chain's SIMD (768), or with G a multiple
+  // of 15 (experimental) every wave but the chain (960)
+  constexpr bool ALL = G % 15 == 0;
+  constexpr uint32_t NH = ALL ? 960u : 768u;
+  constexpr int PPT = (S + NH - 1) / NH;          // products per helper thread
+  constexpr int NB = PPT >= 3 ? 3 : 4;            // entry buffers: loads NB stages ahead
+  constexpr uint32_t RS = 65;                     // ring row stride: lane l's j-th product at j*65 + l
+  __shared__ T ring[2][RS * G];
   const T* __restrict__ vals = static_cast<const T*>(a.csr_vals);
   const T* __restrict__ x = static_cast<const T*>(a.x);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -256,7 +263,7 @@ __device__ __forceinline__ void hub_row_isolated(const SellArgs& a, uint32_t hub
       const T* slot = ring[(i - 1) & 1];
       T p[G];
 #pragma unroll
-      for (int j = 0; j < G; ++j) p[j] = slot[j * 64 + lane];
+      for (int j = 0; j < G; ++j) p[j] = slot[j * RS + lane];
 #pragma unroll
       for (int l = 0; l < 64; ++l) {
         T s = acc;
@@ -269,18 +276,18 @@ __device__ __forceinline__ void hub_row_isolated(const SellArgs& a, uint32_t hub
     if (lane == 0) static_cast<T*>(a.y_out)[r] = acc;
     return;
   }
-  if ((wv & 3) == 0) {  // ---- the chain's SIMD: barriers only
+  if (!ALL && (wv & 3) == 0) {  // ---- the chain's SIMD: barriers only
     for (uint32_t i = 0; i <= nst; ++i) barrier();
     return;
   }
-  // ---- helpers: thread ht makes products ht, ht + 768, ... (< S) of every stage
-  const uint32_t ht = (uint32_t)(wv - (wv >> 2) - 1) * 64 + lane;  // 12 waves -> [0, 768)
+  // ---- helpers: thread ht makes products ht, ht + NH, ... (< S) of every stage
+  const uint32_t ht = (uint32_t)(ALL ? wv - 1 : wv - (wv >> 2) - 1) * 64 + lane;  // -> [0, NH)
   uint32_t c[NB][PPT];
   T v[NB][PPT], xg[NB][PPT];
   auto load = [&](uint32_t st, int k) {  // clamped: copies past the row are never used
 #pragma unroll
     for (int q = 0; q < PPT; ++q) {
-      const uint32_t e = min(st * S + min(ht + 768u * q, S - 1), n - 1);
+      const uint32_t e = min(st * S + min(ht + NH * q, S - 1), n - 1);
       c[k][q] = nt(a.colind + base + e);
       v[k][q] = nt(vals + base + e);
     }
@@ -300,8 +307,8 @@ __device__ __forceinline__ void hub_row_isolated(const SellArgs& a, uint32_t hub
     // it is) into the slot of chain lane e / G, position e % G
 #pragma unroll
     for (int q = 0; q < PPT; ++q) {
-      const uint32_t e = ht + 768u * q;
-      if (q == 0 || e < S) ring[i & 1][(e % G) * 64 + e / G] = i * S + e < n ? v[k][q] * xg[k][q] : T(-0.0);
+      const uint32_t e = ht + NH * q;
+      if (q == 0 || e < S) ring[i & 1][(e % G) * RS + e / G] = i * S + e < n ? v[k][q] * xg[k][q] : T(-0.0);
     }
     gather(kg);       // stage i + GA's gathers
     load(i + NB, k);  // stage i + NB's entries
@@ -314,13 +321,14 @@ __device__ __forceinline__ void hub_row_isolated(const SellArgs& a, uint32_t hub
     iter(std::integral_constant<int, 0>{}, i);
     iter(std::integral_constant<int, 1>{}, i + 1);
     iter(std::integral_constant<int, 2>{}, i + 2);
-    iter(std::integral_constant<int, 3>{}, i + 3);
+    if constexpr (NB == 4) iter(std::integral_constant<int, NB - 1>{}, i + 3);
   }
-  // the last 0..3 stages (unrolled roles continue from i % NB == 0), then the
-  // chain's last iteration's barrier
+  // the last 0..NB-1 stages (unrolled roles continue from i % NB == 0), then
+  // the chain's last iteration's barrier
   if (i < nst) iter(std::integral_constant<int, 0>{}, i++);
   if (i < nst) iter(std::integral_constant<int, 1>{}, i++);
-  if (i < nst) iter(std::integral_constant<int, 2>{}, i++);
+  if constexpr (NB == 4)
+    if (i < nst) iter(std::integral_constant<int, 2>{}, i++);
   barrier();
 }
 
@@ -474,10 +482,12 @@ __global__ __launch_bounds__(256) void k_sell(const SellArgs a) {
 // ORDERED f64 when some hub row has at least kSellIso entries: those rows
 // isolated (hub_row_isolated), the rest as k_sell does them, in 1024-thread
 // workgroups
-// Blocks: [0, niso) the isolated rows; then the other hub rows, 16 waves
-// (rows) a block; then the slices, 4 a block (waves 4-15 exit at once, so a
-// block's slices spread over as many CUs as k_sell's 256-thread blocks do:
-// 16 latency-bound slices on one CU ran 3.7x slower).
+// Blocks: [0, niso) the isolated rows; then the slices, 4 a block (waves
+// 4-15 exit at once, so a block's slices spread over as many CUs as k_sell's
+// 256-thread blocks do: 16 latency-bound slices on one CU ran 3.7x slower);
+// then the other hub rows, 16 waves (rows) a block.  The slices go before
+// the hub blocks: dispatched after them, their long-latency waves started
+// only once the ~1000 hub blocks had drained and ended the launch.
 template <int G>
 __global__ __launch_bounds__(1024) void k_sell_iso(const SellArgs a) {
   if (blockIdx.x < a.niso) {
@@ -486,20 +496,20 @@ __global__ __launch_bounds__(1024) void k_sell_iso(const SellArgs a) {
   }
   const int lane = threadIdx.x & 63;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t H = a.nhubs - a.niso, hb = (H + 15) / 16, b = blockIdx.x - a.niso;
-  if (b < hb) {
-    const uint32_t w = b * 16 + wv;
-    if (w < H) hub_row_exact<double, kChainG>(a, a.niso + w, lane);
+  const uint32_t H = a.nhubs - a.niso, sb = (a.nslices + 3) / 4, b = blockIdx.x - a.niso;
+  if (b < sb) {
+    if (wv >= 4) return;
+    const uint32_t s = b * 4 + wv;
+    if (s < a.nslices) {
+      if (s >= a.nt_from)
+        slice_rows<double, true>(a, s, lane);
+      else
+        slice_rows<double, false>(a, s, lane);
+    }
     return;
   }
-  if (wv >= 4) return;
-  const uint32_t s = (b - hb) * 4 + wv;
-  if (s < a.nslices) {
-    if (s >= a.nt_from)
-      slice_rows<double, true>(a, s, lane);
-    else
-      slice_rows<double, false>(a, s, lane);
-  }
+  const uint32_t w = (b - sb) * 16 + wv;
+  if (w < H) hub_row_exact<double, kChainG>(a, a.niso + w, lane);
 }
 
 template <typename T, bool EXACT>
@@ -509,15 +519,13 @@ hipError_t launch(const SellArgs& a, hipStream_t s) {
   const dim3 grid((uint32_t)((waves + 3) / 4));
   if constexpr (EXACT) {
     // isolated chains when some hub row is long enough (option sell_chain 1: never;
-    // 2..4, experimental: stages of G = 16, 24, 32 instead of kIsoG)
+    // 2, 3 (experimental): stages of G = 12 (12 helper waves) or 30)
     if (a.niso > 0 && a.chain_g != 1) {
       const dim3 g((uint32_t)(a.niso + (a.nhubs - a.niso + 15) / 16 + (a.nslices + 3) / 4));
       if (a.chain_g == 2)
-        hipLaunchKernelGGL(k_sell_iso<16>, g, dim3(1024), 0, s, a);
+        hipLaunchKernelGGL(k_sell_iso<12>, g, dim3(1024), 0, s, a);
       else if (a.chain_g == 3)
-        hipLaunchKernelGGL(k_sell_iso<24>, g, dim3(1024), 0, s, a);
-      else if (a.chain_g == 4)
-        hipLaunchKernelGGL(k_sell_iso<32>, g, dim3(1024), 0, s, a);
+        hipLaunchKernelGGL(k_sell_iso<30>, g, dim3(1024), 0, s, a);
       else
         hipLaunchKernelGGL(k_sell_iso<kIsoG>, g, dim3(1024), 0, s, a);
       return hipGetLastError();

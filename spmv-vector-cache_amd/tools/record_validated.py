@@ -24,7 +24,7 @@ PRODUCT = [f"void hipspmv::k_{k}<{t}{a}>" for t in ("double", "unsigned long")
                         ("csr_lane", ""), ("csr_vector", ", false"), ("wgather", ", 17, 4, 2, true"))] + \
           [f"void hipspmv::(anonymous namespace)::k_sell<{a}>" for a in
            ("double, true", "double, false", "unsigned long, false")] + \
-          ["void hipspmv::(anonymous namespace)::k_sell_iso<12>"] + \
+          ["void hipspmv::(anonymous namespace)::k_sell_iso<45>"] + \
           [f"void hipspmv::k_{k}" for t in ("double", "unsigned long")
            for k in (f"csr_vector<{t}, true>", f"wreduce<{t}>")]
 

@@ -156,4 +156,4 @@ def test_compiled_rings_pass_the_dataflow_check(tmp_path):
         out = subprocess.run([sys.executable, os.path.join(hs.PKG_DIR, "tools", "vmcnt_check.py"), str(asm)],
                              capture_output=True, text=True)
         assert out.returncode == 0, out.stdout
-        assert out.stdout.count(": 0 violations") >= {"vcache.hip": 40, "wgather.hip": 6, "sell.hip": 7}[src], out.stdout
+        assert out.stdout.count(": 0 violations") >= {"vcache.hip": 40, "wgather.hip": 6, "sell.hip": 6}[src], out.stdout
