@@ -304,8 +304,18 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   // on every C5 shard measured)
   const char* lds_env = std::getenv("HIPSPMV_WCSR_LDS");
   const bool lds = lds_env && std::strcmp(lds_env, "1") == 0;
+  // windows of 2^16 columns, or 2^17 when rows are short enough that 2^16
+  // leaves more than one segment per five entries (C5 shards 3 / 7: 342.8 /
+  // 436.4 -> 312.7 / 410.2 us; shard 0, 0.12 segments per entry, stays at
+  // 2^16: 268.6 against 275.4 us)
+  const uint64_t seg16 = h->wc_segments ? h->wc_segments : windowed_segments(a, kWcLog2Window);
+  uint32_t log2w = lds ? kWsLog2Window : (seg16 * 5 > a.nnz ? kWcLog2Window + 1 : kWcLog2Window);
+  if (const char* e = std::getenv("HIPSPMV_WCSR_LOG2W"); e && !lds) {  // probe: another window width
+    const int v = std::atoi(e);
+    if (v >= 10 && v <= 24) log2w = (uint32_t)v;
+  }
   WinLayout L;
-  build_windowed(a, lds ? kWsLog2Window : kWcLog2Window, L);
+  build_windowed(a, log2w, L);
   std::vector<uint32_t> groups, chunks;
   if (lds) {  // csr_vector groups inside each window, cut into chunks of <= kWsChunkNnz entries
     const auto& rp = L.seg.rowptr;
