@@ -74,14 +74,16 @@ extern "C" {
                                     2^17-column windows (wide x: C4/C5);
                                     ordered; experimental like VCACHE_SPLIT4 */
 #define HIPSPMV_KERNEL_WCSR 8 /* csr_vector over the rows cut at 2^16-column
-                                 windows (window-major), then each row's window
-                                 partials summed in window order; fast,
-                                 deterministic; wide x (C4/C5 shards) */
+                                 windows (2^17 for short rows; window-major),
+                                 then each row's window partials summed in a
+                                 fixed order; fast, deterministic; wide, skewed
+                                 x (C5 shards) */
 #define HIPSPMV_KERNEL_SELL 7 /* SELL-C-sigma: one lane per row over slices of
                                  256 length-sorted rows, coalesced entries; rows
-                                 over 256 entries one wave each; ordered in
-                                 ORDERED mode (FAST: long rows tree-summed); any
-                                 matrix; layout built when first selected */
+                                 over 256 entries one wave each (ORDERED: rows of
+                                 8192+ entries as isolated chains, a 1024-thread
+                                 workgroup each); ordered in ORDERED mode (FAST:
+                                 long rows cut into pieces); any matrix */
 
 typedef struct hipspmv_handle hipspmv_t;
 
@@ -119,7 +121,10 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
  * default: every block for VCACHE_SPLIT, the second half for VCACHE; WGATHER:
  * 0 or -1 non-temporal, > 0 the default policy), "sell_nt" (SELL slices s >=
  * sell_nt likewise; -1 default: the second half).  The cache policy never
- * changes a result bit. */
+ * changes a result bit.  Experimental (HIPSPMV_EXPERIMENTAL=1): "sell_chain"
+ * (ORDERED hub chains: 1 = no isolated chains, 2 / 3 = isolated stages of 12 /
+ * 30 products per lane instead of 45; the same bits), "sell_only" (timing
+ * probe, y incomplete: 1 hub rows only, 2 slices only, 3 the longest row). */
 int hipspmv_set_option(hipspmv_t *h, const char *key, int64_t value);
 
 /* Replaces HardwareSpMV::exec()'s reset -> init -> regular -> write sequence
@@ -151,7 +156,9 @@ int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void 
  * "vcache_split_x_bytes" (x bytes one launch streams into LDS)
  * "vcache_split4_eligible" "vcache_split4_x_bytes" "wgather_eligible"
  * "wgather_windows" "row_groups" "sell_slices" "sell_hubs" "sell_hub_pieces"
- * "sell_padding" (SELL layout, 0 until the sell kernel is selected)
+ * "sell_padding" "sell_iso_hubs" (SELL layout, 0 until the sell kernel is
+ * selected) "wcsr_segments" "wcsr_max_segment" "wcsr_window_log2"
+ * "wcsr_chunks" (wcsr layout)
  * "max_row_len" "empty_rows" "execs"; the reference accelerator's cache
  * statistics for the last launch: "total_cycles" "active_cycles" "read_misses"
  * "hazard_stalls" "ocm_depth" "issue_window" "capacity_stalls" "cms"; measured
