@@ -314,8 +314,10 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
     const int v = std::atoi(e);
     if (v >= 10 && v <= 24) log2w = (uint32_t)v;
   }
+  uint32_t cap = UINT32_MAX;  // probe: segments of at most this many entries
+  if (const char* e = std::getenv("HIPSPMV_WCSR_MAXSEG")) cap = std::max(64, std::atoi(e));
   WinLayout L;
-  build_windowed(a, log2w, L);
+  build_windowed(a, log2w, L, cap);
   std::vector<uint32_t> groups, chunks;
   if (lds) {  // csr_vector groups inside each window, cut into chunks of <= kWsChunkNnz entries
     const auto& rp = L.seg.rowptr;

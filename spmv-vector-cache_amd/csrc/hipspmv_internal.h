@@ -198,7 +198,7 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out);
 void build_sell(const HostCSR& a, SellLayout& out);
 // The column-windowed segment matrix of `a` (columns sorted within each row:
 // vcache_eligible's condition).  Throws std::bad_alloc on host OOM.
-void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out);
+void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t cap = UINT32_MAX);
 // Segments build_windowed would make (one pass, no allocation).
 uint64_t windowed_segments(const HostCSR& a, uint32_t log2w);
 // Row groups for csr_vector: group g covers rows [groups[g], groups[g+1]).

@@ -289,7 +289,7 @@ uint64_t windowed_segments(const HostCSR& a, uint32_t log2w) {
   return n;
 }
 
-void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out) {
+void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t cap) {
   out = WinLayout{};
   out.log2w = log2w;
   const uint32_t nwin = (uint32_t)(((uint64_t)a.cols + (1ull << log2w) - 1) >> log2w);
@@ -297,13 +297,14 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out) {
   std::vector<uint64_t> wstart((size_t)nwin + 1, 0);
   out.rowseg.assign((size_t)a.rows + 1, 0);
   for (uint32_t r = 0; r < a.rows; ++r) {
-    uint32_t prev = UINT32_MAX, n = 0;
-    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+    uint32_t prev = UINT32_MAX, n = 0, run = 0;
+    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
       const uint32_t w = a.colind[e] >> log2w;
-      if (w != prev) {
+      if (w != prev || run == cap) {  // a new window, or the segment is full
         wstart[w + 1]++;
         ++n;
         prev = w;
+        run = 0;
       }
     }
     out.rowseg[r + 1] = out.rowseg[r] + n;
@@ -316,12 +317,13 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out) {
   std::vector<uint32_t> len(out.nseg, 0);
   out.segidx.resize(out.nseg);
   for (uint32_t r = 0; r < a.rows; ++r) {
-    uint32_t prev = UINT32_MAX, k = out.rowseg[r];
-    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+    uint32_t prev = UINT32_MAX, k = out.rowseg[r], run = 0;
+    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
       const uint32_t w = a.colind[e] >> log2w;
-      if (w != prev) {
+      if (w != prev || run == cap) {
         out.segidx[k++] = (uint32_t)cursor[w]++;
         prev = w;
+        run = 0;
       }
       len[out.segidx[k - 1]]++;
     }
@@ -339,12 +341,13 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out) {
   g.colind.resize(a.nnz);
   g.vals.resize(a.nnz);
   for (uint32_t r = 0; r < a.rows; ++r) {
-    uint32_t prev = UINT32_MAX, k = out.rowseg[r], d = 0;
-    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+    uint32_t prev = UINT32_MAX, k = out.rowseg[r], d = 0, run = 0;
+    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
       const uint32_t w = a.colind[e] >> log2w;
-      if (w != prev) {
+      if (w != prev || run == cap) {
         d = g.rowptr[out.segidx[k++]];
         prev = w;
+        run = 0;
       }
       g.colind[d] = a.colind[e];
       g.vals[d] = a.vals[e];

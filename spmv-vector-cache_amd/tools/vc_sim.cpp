@@ -538,9 +538,13 @@ int main(int argc, char** argv) {
       // segidx order, are the row's entries in order; a segment lies in one
       // window; segments run window-major with rows ascending; groups tile it
       bool wins = true;
-      for (uint32_t lw : {8u, 12u, kWcLog2Window}) {
+      // (and with a segment length cap: a row's pieces of one window are
+      // consecutive, every piece but its last holds exactly cap entries)
+      const std::pair<uint32_t, uint32_t> forms[] = {
+          {8u, UINT32_MAX}, {12u, UINT32_MAX}, {kWcLog2Window, UINT32_MAX}, {8u, 3u}, {12u, 5u}};
+      for (const auto& [lw, cap] : forms) {
         WinLayout W;
-        build_windowed(A, lw, W);
+        build_windowed(A, lw, W, cap);
         const HostCSR& G = W.seg;
         wins = wins && G.rows == W.nseg && G.nnz == A.nnz && G.rowptr.size() == (size_t)W.nseg + 1 &&
                G.rowptr[0] == 0 && G.rowptr[W.nseg] == A.nnz && W.rowseg.size() == (size_t)A.rows + 1 &&
@@ -555,7 +559,10 @@ int main(int argc, char** argv) {
             if (!wins) break;
             owner[sg] = r;
             const uint32_t w = G.colind[G.rowptr[sg]] >> lw;
-            wins = k == W.rowseg[r] || w > prevw;  // a row's segments in ascending windows
+            const uint32_t prevlen = k == W.rowseg[r] ? 0 : G.rowptr[W.segidx[k - 1] + 1] - G.rowptr[W.segidx[k - 1]];
+            // a row's segments in ascending windows (a full piece may continue in its window)
+            wins = (k == W.rowseg[r] || w > prevw || (w == prevw && prevlen == cap)) &&
+                   G.rowptr[sg + 1] - G.rowptr[sg] <= cap;
             prevw = w;
             for (uint32_t d = G.rowptr[sg]; d < G.rowptr[sg + 1] && wins; ++d, ++e)
               wins = e < A.rowptr[r + 1] && G.colind[d] == A.colind[e] && G.vals[d] == A.vals[e] &&
@@ -565,7 +572,8 @@ int main(int argc, char** argv) {
         }
         for (uint32_t sg = 1; sg < W.nseg && wins; ++sg) {  // window-major, rows ascending in a window
           const uint32_t w0 = G.colind[G.rowptr[sg - 1]] >> lw, w1 = G.colind[G.rowptr[sg]] >> lw;
-          wins = w0 < w1 || (w0 == w1 && owner[sg - 1] < owner[sg]);
+          wins = w0 < w1 || (w0 == w1 && (owner[sg - 1] < owner[sg] ||
+                                           (cap != UINT32_MAX && owner[sg - 1] == owner[sg])));
         }
         std::vector<uint32_t> gg;
         build_row_groups(G, gg);
