@@ -314,8 +314,11 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
     const int v = std::atoi(e);
     if (v >= 10 && v <= 24) log2w = (uint32_t)v;
   }
-  uint32_t cap = UINT32_MAX;  // probe: segments of at most this many entries
-  if (const char* e = std::getenv("HIPSPMV_WCSR_MAXSEG")) cap = std::max(64, std::atoi(e));
+  // segments of at most kCvGroupNnz entries, so every segment-pass group is a
+  // balanced multi-row group (C5 shard 0 / 3: 264.1 / 314.2 -> 257.2 / 306.5
+  // us); HIPSPMV_WCSR_MAXSEG overrides (probe)
+  uint32_t cap = (uint32_t)kCvGroupNnz;
+  if (const char* e = std::getenv("HIPSPMV_WCSR_MAXSEG")) cap = (uint32_t)std::max(64, std::atoi(e));
   WinLayout L;
   build_windowed(a, log2w, L, cap);
   std::vector<uint32_t> groups, chunks;

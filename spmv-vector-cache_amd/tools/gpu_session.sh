@@ -53,7 +53,7 @@ for s in $STEPS; do
       HIPSPMV_WCSR_LDS=1 step wcsr_shards_lds 900 bash -c 'for s in 0 3 7; do python -u spmv-vector-cache_amd/tools/wfast_probe.py --windows "" --only-wcsr --shard $s || exit 1; done' ;;
     wcsrwin) for w in 15 17; do HIPSPMV_WCSR_LOG2W=$w step wcsr_shards_w$w 900 bash -c 'for s in 0 3 7; do python -u spmv-vector-cache_amd/tools/wfast_probe.py --windows "" --only-wcsr --shard $s || exit 1; done' || break; done &&
       step wcsr_shards_w16 900 bash -c 'for s in 0 3 7; do python -u spmv-vector-cache_amd/tools/wfast_probe.py --windows "" --only-wcsr --shard $s || exit 1; done' ;;
-    wcsrcap) for c in 1024 4096; do HIPSPMV_WCSR_MAXSEG=$c step wcsr_shards_cap$c 900 bash -c 'for s in 0 3; do python -u spmv-vector-cache_amd/tools/wfast_probe.py --windows "" --only-wcsr --shard $s || exit 1; done' || break; done &&
+    wcsrcap) for c in ${CAPS:-1024 4096}; do HIPSPMV_WCSR_MAXSEG=$c step wcsr_shards_cap$c 900 bash -c 'for s in 0 3; do python -u spmv-vector-cache_amd/tools/wfast_probe.py --windows "" --only-wcsr --shard $s || exit 1; done' || break; done &&
       step wcsr_shards_nocap 900 bash -c 'for s in 0 3; do python -u spmv-vector-cache_amd/tools/wfast_probe.py --windows "" --only-wcsr --shard $s || exit 1; done' ;;
     wfast) step wfast_probe 900 python -u spmv-vector-cache_amd/tools/wfast_probe.py ;;
     wfast2) step wfast_probe_s0 600 python -u spmv-vector-cache_amd/tools/wfast_probe.py --windows 14,15,16,17 &&
