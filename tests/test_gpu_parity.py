@@ -163,7 +163,9 @@ def test_wcsr_wide_windows(gpu, dtype):
     h.set_kernel("wcsr")
     row_of = np.repeat(np.arange(rows), lens)
     lw = h.stat("wcsr_window_log2")
-    assert h.stat("wcsr_segments") == np.unique(row_of.astype(np.int64) * 4096 + (colind >> lw)).size
+    # segments: each row's run in one window, cut into pieces of <= 256 entries (the layout's cap)
+    _, runs = np.unique(row_of.astype(np.int64) * 4096 + (colind >> lw), return_counts=True)
+    assert h.stat("wcsr_segments") == int(np.sum((runs + 255) // 256))
     y0 = (rng.uniform(-1, 1, rows) if dtype == np.float64 else rng.integers(0, 2**64, rows, dtype=np.uint64))
     for beta in (0, 1):
         y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else np.zeros(rows, dtype)), rows=rows)
