@@ -126,11 +126,11 @@ __device__ __forceinline__ void csr_vector_rows(const uint32_t* __restrict__ row
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
   T carry = T(0);
-  if constexpr (KIND == 3) {
-    // k_wseg: every term of the group (<= 256) is loaded before the scans, so
-    // a wave keeps four entry loads in flight instead of one per round trip
-    // (the LDS form 359.7 -> 322.4 us on C5 shard 0; the same in the global
-    // form, KIND 1, measured slower: 264.5 -> 270.8 us)
+  if constexpr (KIND == 2 || KIND == 3) {
+    // the wcsr reduce and k_wseg: every term of the group (<= 256) is loaded
+    // before the scans, so a wave keeps four loads in flight instead of one
+    // per round trip (k_wseg on C5 shard 0: 359.7 -> 322.4 us; the same in
+    // the global segment pass, KIND 1, measured slower: 264.5 -> 270.8 us)
     constexpr int Q = kCvGroupNnz / 64;
     T pv[Q];
     if (n) {
