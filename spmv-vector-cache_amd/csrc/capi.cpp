@@ -236,6 +236,40 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g) {
   return HIPSPMV_OK;
 }
 
+// Frees whatever a layout build that threw (host std::bad_alloc) had already
+// uploaded: the half-built SELL / wcsr / vcache-family layouts, so a later
+// build starts from nothing and nothing stays allocated behind a failed one.
+static void drop_partial_layouts(hipspmv_t* h) {
+  DeviceGuard g(h->device);
+  if (!h->sell.built) {
+    auto& q = h->sell;
+    void* sp[] = {q.d_off, q.d_width, q.d_row, q.d_len, q.d_col, q.d_hubs, q.d_vals, q.d_pieces, q.d_tickets,
+                  q.d_partial};
+    for (void* p : sp)
+      if (p) (void)hipFree(p);
+    q = hipspmv_handle::Sell{};
+  }
+  if (!h->wc.built) {
+    auto& w = h->wc;
+    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart};
+    for (void* p : wp)
+      if (p) (void)hipFree(p);
+    w = hipspmv_handle::Wc{};
+  }
+  for (int k = 0; k < 4; ++k)
+    if (!h->vc[k].ok && (h->vc[k].d_seg || h->vc[k].d_code || h->vc[k].d_vals)) {
+      const auto keep = h->vc[k];  // the ordered geometry is known before its entries exist
+      free_vc(h, k);
+      h->vc[k].split = keep.split;
+      h->vc[k].rows_per_block = keep.rows_per_block;
+      h->vc[k].nblocks = keep.nblocks;
+      h->vc[k].npanels = keep.npanels;
+      h->vc[k].part_panels = keep.part_panels;
+      h->vc[k].npad = keep.npad;
+      h->vc[k].max_run = keep.max_run;
+    }
+}
+
 // The device CSR copy back on the host (the host CSR is gone after create):
 // the source of the layouts built on first selection by name.
 static int download_csr(hipspmv_t* h, HostCSR& a) {
@@ -488,11 +522,16 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   const bool exact_any = h->dtype == HIPSPMV_U64;
   for (const bool fast_ok : {exact_any, true}) {
     const int k = auto_pick(h, fast_ok, false);
-    if (k == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
-    else if (k == HIPSPMV_KERNEL_WGATHER) st = build_vc_layout(h, 3, a);
-    else if (k == HIPSPMV_KERNEL_VCACHE) st = build_vc_layout(h, 0, a);
-    else if (k == HIPSPMV_KERNEL_WCSR) st = build_wcsr_layout(h, a);
-    else st = HIPSPMV_OK;
+    try {  // a host allocation failure in a layout build is an OOM like a device one
+      if (k == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
+      else if (k == HIPSPMV_KERNEL_WGATHER) st = build_vc_layout(h, 3, a);
+      else if (k == HIPSPMV_KERNEL_VCACHE) st = build_vc_layout(h, 0, a);
+      else if (k == HIPSPMV_KERNEL_WCSR) st = build_wcsr_layout(h, a);
+      else st = HIPSPMV_OK;
+    } catch (const std::bad_alloc&) {
+      drop_partial_layouts(h);
+      st = HIPSPMV_ERR_OOM;
+    }
     if (st == HIPSPMV_ERR_OOM) {
       h->auto_fallback++;
       (void)hipGetLastError();  // the failed allocation must not leak into a later check
@@ -532,7 +571,12 @@ static int create_common(uint32_t rows, uint32_t cols, uint32_t nnz, int dtype, 
   h->cols = cols;
   h->nnz = nnz;
   if (hipDeviceGetAttribute(&h->clock_khz, hipDeviceAttributeClockRate, device) != hipSuccess) h->clock_khz = 0;
-  st = finish_create(h, a);
+  try {
+    st = finish_create(h, a);
+  } catch (...) {  // nothing uploaded so far may leak past a throw
+    release(h);
+    throw;
+  }
   if (st) {
     release(h);
     return st;
@@ -595,8 +639,10 @@ static int ensure_layout(hipspmv_t* h, int kernel) {
       else st = build_vc_layout(h, kernel == HIPSPMV_KERNEL_WGATHER ? 3 : 0, a);
     }
   } catch (const std::bad_alloc&) {
+    drop_partial_layouts(h);
     st = HIPSPMV_ERR_OOM;
   } catch (...) {  // e.g. std::system_error from the layout builder's threads
+    drop_partial_layouts(h);
     g_last_error = "layout build failed";
     st = HIPSPMV_ERR_HIP;
   }
@@ -649,12 +695,19 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                  h->vcache_xlane, v.max_seg, h->vcache_map};
     a.nt_from = h->vcache_nt >= 0 ? (uint32_t)std::min<int64_t>(h->vcache_nt, UINT32_MAX)
                 : k == 1 ? 0u : k == 0 ? v.nblocks / 2 : ~0u;
-    h->prof_pending = false;
+    // an unprofiled launch leaves an unread profile of an earlier launch readable
+    // (it writes no stamps); d_prof is allocated when the option is set, never
+    // here, so a profiled launch is legal only outside a capture (checked below)
     if (h->profile && k < 2) {  // the default configuration with its profile stamps
+      hipStreamCaptureStatus pc = hipStreamCaptureStatusNone;
+      HIP_TRY(hipStreamIsCapturing(s, &pc));
+      if (pc != hipStreamCaptureStatusNone) {
+        set_last_error("option profile: profiled launches cannot be captured into a graph");
+        return HIPSPMV_ERR_UNSUPPORTED;
+      }
       if (k == 0 && !h->d_prof) {
-        const size_t b = 4ull * kVcProfWords * v.nblocks;
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&h->d_prof), b));
-        h->device_bytes += b;
+        set_last_error("option profile: no stamp buffer for the ordered geometry");
+        return HIPSPMV_ERR_UNSUPPORTED;
       }
       if (k == 0) a.partial = h->d_prof;
       e = launch_vcache_profiled(h->dtype, a, s);
@@ -822,6 +875,12 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "timing") {
     h->timing = value ? 1 : 0;
   } else if (k == "profile") {  // NewCache state statistics from the vcache kernels' stamps
+    if (value && h->vc0_eligible && !h->d_prof) {  // the ordered geometry's stamp buffer, allocated here
+      DeviceGuard g(h->device);
+      const size_t b = 4ull * kVcProfWords * h->vc[0].nblocks;
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&h->d_prof), b));
+      h->device_bytes += b;
+    }
     h->profile = value ? 1 : 0;
   } else {
     return HIPSPMV_ERR_KEY;

@@ -33,6 +33,7 @@ for s in $STEPS; do
     prof) export TMPDIR=/tmp; step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-rocprof ;;
     pmc) export TMPDIR=/tmp; step pmc 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-rocprof &&
          step pmc2 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-rocprof ;;
+    pmc4) step pmc4 400 bash spmv-vector-cache_amd/tools/gpurun_pmc.sh ;;
     micro) step micro 300 ./spmv-vector-cache_amd/tools/microbench ;;
     exp) HIPSPMV_EXPERIMENTAL=1 step pytest_exp 600 python -m pytest tests/test_gpu_parity.py -m gpu -q -x -p no:cacheprovider -k experimental ;;
     ablate) step ablate 600 ./spmv-vector-cache_amd/lib/vc_ablate ;;
