@@ -84,6 +84,8 @@ def parse():
                    help="LDS-DMA x loader (-1: the library default, on for the split geometry)")
     p.add_argument("--vcache-map", type=int, default=0, choices=[0, 1],
                    help="experimental XCD-aware placement of vcache_split4's column parts")
+    p.add_argument("--vquad-variant", type=int, default=-1,
+                   help="vcache_split4 (k_vquad) configuration (-1: the library default)")
     p.add_argument("--traffic-csv", default=None,
                    help="rocprofv3 --pmc counter CSV (FETCH_SIZE, WRITE_SIZE) of this workload, for roofline.traffic")
     p.add_argument("--no-rocprof", action="store_true",
@@ -227,7 +229,8 @@ def _bench_child(a, steps: int, warmup: int):
             "--steps", str(steps), "--warmup", str(warmup), "--workload", a.workload, "--scale", str(a.scale),
             "--log2-rows", str(a.log2_rows), "--log2-cols", str(a.log2_cols), "--nnz-per-row", str(a.nnz_per_row),
             "--kernel", a.kernel, "--mode", a.mode, "--vcache-xlane", str(a.vcache_xlane),
-            "--vcache-dma", str(a.vcache_dma), "--vcache-map", str(a.vcache_map), "--no-strong"] + \
+            "--vcache-dma", str(a.vcache_dma), "--vcache-map", str(a.vcache_map), "--no-strong",
+            "--vquad-variant", str(getattr(a, "vquad_variant", -1))] + \
         (["--shard", a.shard] if getattr(a, "shard", "") else [])
 
 
@@ -596,6 +599,8 @@ def main():
     h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols, device=local)
     if a.kernel != "auto":
         h.set_kernel(a.kernel)
+    if a.vquad_variant >= 0:
+        h.set_option("vquad_variant", a.vquad_variant)
     if a.vcache_xlane != -1 or a.vcache_dma != -1 or a.vcache_map:
         h.set_option("vcache_map", a.vcache_map)
         h.set_option("vcache_xlane", a.vcache_xlane)
@@ -686,7 +691,7 @@ def main():
             y_other = None
 
     traffic, traffic_src = None, None
-    ksub = ("k_vcache" if "vcache" in kname else ["k_csr_vector<double, true>", "k_wreduce"] if kname == "wcsr"
+    ksub = ("k_vquad" if kname == "vcache_split4" else "k_vcache" if "vcache" in kname else ["k_csr_vector<double, true>", "k_wreduce"] if kname == "wcsr"
             else "k_" + kname)
     if a.traffic_csv and os.path.exists(a.traffic_csv):
         traffic, traffic_src = traffic_from_csv(a.traffic_csv, ksub), a.traffic_csv

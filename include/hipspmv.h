@@ -73,11 +73,10 @@ extern "C" {
 #define HIPSPMV_KERNEL_WGATHER 6 /* y block in LDS, x gathered from global in
                                     2^17-column windows (wide x: C4/C5);
                                     ordered; experimental like VCACHE_SPLIT4 */
-#define HIPSPMV_KERNEL_WCSR 8 /* csr_vector over the rows cut at 2^16-column
-                                 windows (2^17 for short rows; window-major),
-                                 then each row's window partials summed in a
-                                 fixed order; fast, deterministic; wide, skewed
-                                 x (C5 shards) */
+#define HIPSPMV_KERNEL_WCSR 8 /* csr_vector over the rows cut at 2^17-column
+                                 windows (window-major), then each row's window
+                                 partials summed in a fixed order; fast,
+                                 deterministic; wide, skewed x (C5 shards) */
 #define HIPSPMV_KERNEL_SELL 7 /* SELL-C-sigma: one lane per row over slices of
                                  256 length-sorted rows, coalesced entries; rows
                                  over 256 entries one wave each (ORDERED: rows of
@@ -209,8 +208,13 @@ int hipspmv_mark_row_starts(const uint32_t *rowind, uint32_t *rowind_out, uint32
  * when the block starts at a multiple of HIPSPMV_SHARD_ALIGN rows and runs
  * the same kernel (the FAST csr_vector kernel groups rows within aligned
  * 64-row windows; every other kernel is position-independent; ORDERED is
- * kernel-independent, FAST AUTO may choose by shard shape).  hipspmv_multi_create and the host
- * partition helpers cut at such rows. */
+ * kernel-independent, FAST AUTO may choose by shard shape).  One exception:
+ * WCSR in FAST f64 -- its segment pass groups the window-major segments of
+ * all the shard's rows, so a row's partials depend on which other rows share
+ * its windows; a shard's rows stay within the FAST bound but may differ in
+ * the last bits from the unpartitioned run (u64 is exact either way; the
+ * window width is the same for every matrix).  hipspmv_multi_create and the
+ * host partition helpers cut at such rows. */
 #define HIPSPMV_SHARD_ALIGN 64
 
 /* ---- several devices of one process ---------------------------------------

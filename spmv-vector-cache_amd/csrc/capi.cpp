@@ -108,7 +108,11 @@ struct hipspmv_handle {
   } wc;
   int vcache_dma = -1;   // option "vcache_dma": LDS-DMA x loader (-1 default: on for the split geometry)
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
-  int vcache_map = 0;    // option "vcache_map": XCD-aware part placement, split 4 (experimental)
+  int vcache_map = 0;    // option "vcache_map": XCD-aware part placement (unused since k_vquad; kept as an option)
+  int vquad_variant = 0;  // option "vquad_variant": k_vquad configuration (csrc/vquad.hip launch_vquad_t)
+  // bit 0: a k_vquad combine hand-off wait timed out (never observed; the
+  // launch's y is then wrong and the scratch counters need a reset)
+  uint32_t* d_status = nullptr;
   // option "wgather_chunk": row blocks per k_wgather launch:
   // one launch's blocks are all resident at once (2 per CU), so they walk
   // the x windows together and the gathered window stays in L2
@@ -158,7 +162,7 @@ struct hipspmv_handle {
 static void release(hipspmv_t* h) {
   if (!h) return;
   DeviceGuard g(h->device);
-  void* ptrs[] = {h->d_rowptr, h->d_colind, h->d_groups, h->d_vals, h->d_x, h->d_y, h->d_prof};
+  void* ptrs[] = {h->d_rowptr, h->d_colind, h->d_groups, h->d_vals, h->d_x, h->d_y, h->d_prof, h->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& v : h->vc) {
@@ -338,12 +342,10 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   // on every C5 shard measured)
   const char* lds_env = std::getenv("HIPSPMV_WCSR_LDS");
   const bool lds = lds_env && std::strcmp(lds_env, "1") == 0;
-  // windows of 2^16 columns, or 2^17 when rows are short enough that 2^16
-  // leaves more than one segment per five entries (C5 shards 3 / 7: 342.8 /
-  // 436.4 -> 312.7 / 410.2 us; shard 0, 0.12 segments per entry, stays at
-  // 2^16: 268.6 against 275.4 us)
-  const uint64_t seg16 = h->wc_segments ? h->wc_segments : windowed_segments(a, kWcLog2Window);
-  uint32_t log2w = lds ? kWsLog2Window : (seg16 * 5 > a.nnz ? kWcLog2Window + 1 : kWcLog2Window);
+  // windows of 2^kWcLog2Window columns for every matrix (a width that does
+  // not depend on the matrix keeps a row's segments the same in every row
+  // partition of it)
+  uint32_t log2w = lds ? kWsLog2Window : kWcLog2Window;
   if (const char* e = std::getenv("HIPSPMV_WCSR_LOG2W"); e && !lds) {  // probe: another window width
     const int v = std::atoi(e);
     if (v >= 10 && v <= 24) log2w = (uint32_t)v;
@@ -511,8 +513,17 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
     v.npad = G.npad;
     v.max_run = vcache_max_run(a, (uint32_t)kVcOrdered.panel);
   }
+  {
+    const uint32_t zero = 0;
+    if ((st = dev_upload(&h->d_status, &zero, 1, h->device_bytes))) return st;
+  }
   if (vcache_eligible(a, kVcSplit) && (st = upload_vc(h, 1, a, kVcSplit))) return st;
-  if (experimental && vcache_eligible(a, kVcSplit4) && (st = upload_vc(h, 2, a, kVcSplit4))) return st;
+  // the four-part layout (k_vquad) wherever eligible and every segment fits
+  // the kernel's register window (k_vquad has no slow path for longer ones)
+  if (vcache_eligible(a, kVcSplit4)) {
+    if ((st = upload_vc(h, 2, a, kVcSplit4))) return st;
+    if (h->vc[2].max_seg > vquad_max_window(0)) free_vc(h, 2);
+  }
   h->wg_eligible = vcache_eligible(a, kWgWindow);
   if (h->wg_eligible) h->wg_max_run = vcache_max_run(a, (uint32_t)kWgWindow.panel);
   if (a.cols >= kWcMinCols) h->wc_segments = windowed_segments(a, kWcLog2Window);
@@ -715,6 +726,10 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
       h->prof_valid = false;
       h->prof_stream = s;
       h->prof_layout = k;
+    } else if (k == 2) {
+      a.status = h->d_status;
+      a.variant = h->vquad_variant;
+      e = launch_vquad(h->dtype, a, s);
     } else {
       e = launch_vcache(h->dtype, a, s);
     }
@@ -749,6 +764,22 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   h->last_kernel = kernel;
   h->last_beta = beta;
   h->execs++;
+  return HIPSPMV_OK;
+}
+
+// k_vquad's combine status (bit 0: a hand-off wait timed out, the launch's y
+// is wrong): read after a synchronous exec and by the stat key
+// "handoff_timeouts"; a set bit resets the scratch counters and the word.
+static int read_status(hipspmv_t* h, uint32_t* out) {
+  *out = 0;
+  if (!h->d_status) return HIPSPMV_OK;
+  DeviceGuard g(h->device);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, h->d_status, 4, hipMemcpyDeviceToHost));
+  if (*out) {
+    if (h->vc[2].d_tickets) HIP_TRY(hipMemset(h->vc[2].d_tickets, 0, 8ull * h->vc[2].nblocks));
+    HIP_TRY(hipMemset(h->d_status, 0, 4));
+  }
   return HIPSPMV_OK;
 }
 
@@ -847,6 +878,10 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
     h->vcache_dma = (int)value;
   } else if (k == "vcache_map") {
     h->vcache_map = value ? 1 : 0;
+  } else if (k == "vquad_variant") {  // k_vquad configuration (csrc/vquad.hip)
+    if (value < 0 || value > 16) return HIPSPMV_ERR_INVALID_ARG;
+    if (h->vc[2].ok && h->vc[2].max_seg > vquad_max_window((int)value)) return HIPSPMV_ERR_UNSUPPORTED;
+    h->vquad_variant = (int)value;
   } else if (k == "wgather_chunk") {  // row blocks per k_wgather launch (0: all in one launch)
     if (value < 0 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->wgather_chunk = (uint32_t)value;
@@ -923,6 +958,14 @@ int hipspmv_exec(hipspmv_t* h, const void* x, void* y, int beta, int mode) {
     HIP_TRY(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
     h->d2h_ns = (uint64_t)(ms * 1e6);
     h->pending = false;
+    if (kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
+      uint32_t bad = 0;
+      if (int st2 = read_status(h, &bad)) return st2;
+      if (bad) {
+        set_last_error("k_vquad: a column-part hand-off timed out; this exec's y is wrong (scratch reset)");
+        return HIPSPMV_ERR_HIP;
+      }
+    }
     return HIPSPMV_OK;
   } catch (const std::bad_alloc&) {
     return HIPSPMV_ERR_OOM;
@@ -1007,6 +1050,13 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "max_row_len") *out = h->max_row_len;
   else if (k == "empty_rows") *out = h->empty_rows;
   else if (k == "execs") *out = h->execs;
+  else if (k == "handoff_timeouts") {  // k_vquad combine waits that timed out since the last read (0)
+    uint32_t v = 0;
+    if (int st = read_status(h, &v)) return st;
+    *out = v;
+  }
+  else if (k == "vquad_variant") *out = (uint64_t)h->vquad_variant;
+  else if (k == "vcache_split4_max_segment") *out = h->vc[2].max_seg;
   else if (k == "clock_khz") *out = (uint64_t)h->clock_khz;
   // The reference accelerator's cache statistics (HardwareSpMVNewCache.cpp:
   // 189-204), restated for the last kernel's layout:

@@ -58,12 +58,16 @@ constexpr uint32_t kVcMore = 1u << 31;  // next entry continues this entry's row
 constexpr uint32_t kVcRunMax = 16;
 
 // ---- wcsr: csr_vector over the column-windowed segment matrix
-// Every row is cut at column windows of 2^kWcLog2Window columns (512 KiB of
+// Every row is cut at column windows of 2^kWcLog2Window columns (1 MiB of
 // x); the pieces ("segments", one per (window, row) pair that has
 // entries) form the rows of A', in window-major order.  csr_vector over A'
 // walks x one window at a time; y[r] is the sum of r's segment partials in
-// window order (k_wreduce).
-constexpr uint32_t kWcLog2Window = 16;
+// window order (k_wreduce).  One width for every matrix (round 4): the
+// round-3 rule (2^16 unless that left more than one segment per five
+// entries) chose by the shard's own row lengths, so two shards of one matrix
+// could cut a row differently; 2^17 measured 275 / 313 / 410 us on C5 shards
+// 0 / 3 / 7 against 269 / 343 / 436 at 2^16.
+constexpr uint32_t kWcLog2Window = 17;
 // AUTO considers wcsr from this many columns (x of 16 MiB: four XCD L2s)
 // wcsr LDS form (k_wseg, opt-in HIPSPMV_WCSR_LDS=1): x windows of 2^14 f64
 // (128 KiB of LDS), chunks of at most kWsChunkNnz entries of one window per

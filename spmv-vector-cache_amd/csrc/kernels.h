@@ -25,6 +25,8 @@ struct VcacheArgs {
   int map = 0;           // split 4: XCD-aware unit placement (experimental, option "vcache_map")
   uint32_t chunk = 0;    // k_wgather: row blocks per launch (0: one launch)
   uint32_t nt_from = ~0u;  // k_vcache: row blocks b >= nt_from load their entries non-temporally
+  uint32_t* status = nullptr;  // k_vquad: bit 0 set when a combine hand-off wait timed out
+  int variant = 0;             // k_vquad: configuration (loader waves, x / entry ring depths)
 };
 
 struct CsrArgs {
@@ -94,6 +96,11 @@ hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);
 // the default kernel's bits.  Split 4: hipErrorInvalidValue.
 hipError_t launch_vcache_profiled(int dtype, const VcacheArgs& a, hipStream_t s);
 constexpr int kVcProfWords = 8;
+// k_vquad (csrc/vquad.hip): the four-part vector cache over the kVcSplit4
+// layout, x panels DX deep in registers; needs a.status and max_seg within
+// vquad_max_window(a.variant).
+hipError_t launch_vquad(int dtype, const VcacheArgs& a, hipStream_t s);
+uint32_t vquad_max_window(int variant);
 hipError_t launch_sell(int dtype, const SellArgs& a, hipStream_t s);
 hipError_t launch_wcsr(int dtype, const WcsrArgs& a, hipStream_t s);
 hipError_t launch_wgather(int dtype, const VcacheArgs& a, hipStream_t s);

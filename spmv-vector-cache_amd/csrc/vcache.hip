@@ -619,10 +619,8 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
     dispatch<T, 1>(a, s, ld, cx);
   else if (a.split == 3)
     dispatch<T, 3>(a, s, ld, cx);
-  else if (a.map)  // experimental: XCD-aware placement of the four column parts
-    dispatch<T, 4, 1>(a, s, ld, cx);
-  else
-    dispatch<T, 4>(a, s, ld, cx);
+  else  // four parts: k_vquad (csrc/vquad.hip) runs that layout
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -1,0 +1,428 @@
+// k_vquad: the four-part LDS vector cache (HIPSPMV_KERNEL_VCACHE_SPLIT4,
+// DESIGN.md §6.12) -- the round-4 FAST kernel for C3-like matrices.
+//
+// Why four parts.  A work unit keeps the y accumulators of R rows in LDS and
+// streams its column part of x through LDS, so every CU moves 8 * cols / S
+// bytes of x per launch besides its share of the entries.  Round 4's overlap
+// probe (tools/overlap_probe.hip, profiles/r04) measured that the two streams
+// do not overlap inside a CU -- their times add -- so the x bytes per CU are
+// the lever: R = 16384 rows (128 KiB of y, the most LDS holds beside an x
+// ring), S = 4 parts, 64 blocks x 4 = 256 units: 2 MiB of x per CU against
+// 2.7 MiB for three parts of 12352 rows (free-running skeletons: 83 against
+// 94 us).  What kept the round-2 four-part kernel slow (137 us) was its
+// x ring: 1984-column panels with one panel in flight, waited for at every
+// step.  Here the loader waves keep DX panels in flight in registers (asm
+// loads, exact vmcnt waits) and only the store into LDS happens per step, so
+// an x panel has DX steps to arrive.
+//
+// Work unit (b, h): rows [b*R, b*R + R), panels [vc_part_first(h), ...) of the
+// kVcSplit4 layout (csrc/plan.cpp build_vcache: per (block, panel) segment,
+// entries in (row, column) order, code = col_local | row_local << 16 | CONT |
+// MORE).  The parts of a block run in dispatch slots i, i+8, i+16, i+24 (one
+// XCD under round-robin placement: the combine's hand-off stays in one L2;
+// speed only).
+//
+// Roles: waves [0, WL) stage x panels (LDS slot s & 1 holds panel s); waves
+// [WL, 16) stream the unit's entries DE steps ahead (asm loads, exact waits)
+// and apply them: every valid lane forms its rounded product from the LDS
+// panel, a run head (first entry of its row in the segment) adds the
+// products of its run's other entries from the next lanes (DPP-free
+// __shfl_down; a run that crosses into the next wave finishes with scalar
+// loads) and updates its y row in LDS.  No two lanes own one row in a step,
+// and the step barrier orders the steps.  One s_barrier per panel.
+//
+// Combine (fixed order y = p0 + p1 + p2 + p3, deterministic): ticket first --
+// the workgroups that are not last publish their partial with write-through
+// (sc1) 16-byte stores, drain, and count it; the last arriver polls that count
+// (sc1), reads the three partials (sc1) and writes y (MI355X_MICROARCH.md,
+// Valid forms, table row 1).  The publishers took their tickets before the
+// last arriver did, so they run and publish: the wait is bounded by their
+// work.  A wait that still exceeds ~0.3 s of polls sets bit 0 of *status and
+// leaves the counters alone (the host reports the launch failed and resets
+// the scratch) instead of reading partials that may be unpublished.
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "hipspmv_internal.h"
+#include "kernels.h"
+
+namespace hipspmv {
+
+namespace {
+
+constexpr int VR = kVcSplit4.rows, VP = kVcSplit4.panel, SPLIT = 4;
+
+// an asm-load ring value may be read (or its register reused) only after the
+// wait that retired its load: the wait is followed by an empty asm that takes
+// the value in and out, so no use moves above the wait and the register stays
+// owned by the value until then (tools/vmcnt_check.py checks the build)
+template <typename R>
+__device__ __forceinline__ void tie(R& r) {
+  asm volatile("" : "+v"(r));
+}
+__device__ __forceinline__ void tie(u64x2& r) {
+  asm volatile("" : "+v"(r));
+}
+__device__ __forceinline__ uint32_t ald_u32_nt(const uint32_t* p) {
+  uint32_t r;
+  asm volatile("global_load_dword %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ T ald_64_nt(const T* p) {
+  uint64_t r;
+  asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
+  return __builtin_bit_cast(T, r);
+}
+
+constexpr uint32_t gcd_u(uint32_t a, uint32_t b) { return b ? gcd_u(b, a % b) : a; }
+constexpr uint32_t lcm_u(uint32_t a, uint32_t b) { return a / gcd_u(a, b) * b; }
+
+}  // namespace
+
+// AB: ablation mask (timing probes only; results wrong unless 0): 1 no apply,
+// 2 no x stores into LDS, 4 no combine (each part writes its own rows), 8 no
+// step barrier, 16 x loads by LDS-DMA into the slots (timing only: DX > 1
+// panels in flight overwrite each other), 32 no x loads, 64 no entry loads
+template <typename T, int WL, int DX, int DE, int EPT, bool NOFB = false, int AB = 0>
+__global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict__ seg,
+                                                       const uint32_t* __restrict__ ecode,
+                                                       const T* __restrict__ evals, const T* __restrict__ x,
+                                                       const T* __restrict__ y_in, T* __restrict__ y_out,
+                                                       T* __restrict__ partial, uint32_t* __restrict__ tickets,
+                                                       uint32_t* __restrict__ status, uint32_t rows, uint32_t cols,
+                                                       uint32_t rows_per_block, uint32_t nblocks, uint32_t npanels,
+                                                       uint32_t npad, uint32_t last, int beta) {
+#pragma clang fp contract(off)
+  constexpr int VT = kVcThreads, NW = VT / 64, WC = NW - WL;
+  constexpr int LT = WL * 64, CT = WC * 64;
+  constexpr uint32_t PAIRS = VP / 2;         // 16-byte pairs per panel
+  constexpr int NJ = (PAIRS + LT - 1) / LT;  // pairs per loader lane per panel
+  static_assert(VR * 8 + 2 * VP * 8 + kVcSegMax * 4 <= 163840, "LDS budget");
+  static_assert(WL > 0 && WC > 0 && DX >= 2 && DE >= 2, "roles and rings");
+  static_assert((DX - 1) * NJ < 64 && (DE - 1) * 2 * EPT < 64, "vmcnt field");
+  __shared__ alignas(16) T ylds[VR];
+  __shared__ alignas(16) T xb[2][VP];
+  __shared__ uint32_t segl[kVcSegMax];
+
+  const int t = threadIdx.x;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool loader = wv < (uint32_t)WL;  // wave-uniform role
+  // unit i -> (b, h): the parts of a block are 8 dispatch slots apart
+  const uint32_t g8 = blockIdx.x / (8 * SPLIT), rem = blockIdx.x % (8 * SPLIT);
+  const uint32_t nbg = min(8u, nblocks - g8 * 8);
+  const uint32_t h = rem / nbg, b = g8 * 8 + rem % nbg;
+  const uint32_t r0 = b * rows_per_block;
+  if (r0 >= rows) return;  // never with a vcache_grid_ok geometry (workgroup-uniform, before any barrier)
+  const uint32_t nr = min(rows_per_block, rows - r0);
+  const uint32_t p0 = vc_part_first(h, npanels, SPLIT);            // first global panel of this unit
+  const uint32_t npu = vc_part_first(h + 1, npanels, SPLIT) - p0;  // >= 1 (vcache_grid_ok)
+  const uint32_t* sp = seg + ((size_t)b * SPLIT + h) * (npad + 1);
+  if ((uint32_t)t <= npad) segl[t] = sp[t];
+  for (uint32_t i = t; i < nr; i += VT) ylds[i] = (beta && h == 0) ? y_in[r0 + i] : T(0);
+  __syncthreads();  // segl visible; then each role's prologue, one barrier, the steps
+
+  // every role runs the same padded step count (one barrier per step, no
+  // early exit inside an unrolled group: the ring waits stay exact); in
+  // barrier terms step s of both roles lies between the same two barriers
+  constexpr uint32_t PER = lcm_u(DX, DE);
+  const uint32_t nsteps = (npu + PER - 1) / PER * PER;
+
+  auto barrier = [] {
+    if (AB & 8) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+
+  if (loader) {
+    // ---- x panels: NJ 16-byte pairs per lane per panel, clamped in bounds
+    // (branch-free), DX panels in flight in registers; in step s the panel
+    // s + 1 is stored into slot (s + 1) & 1 (read last in step s - 1, closed
+    // by that step's barrier) and panel s + 1 + DX is issued into its registers
+    const uint32_t cmax = (cols - 2) & ~1u;
+    const T xlast = __builtin_bit_cast(T, sld_64(x + cols - 1));  // scalar: no vmcnt slot in the ring
+    u64x2 R[DX][NJ];
+    auto issue = [&](uint32_t s, u64x2* r) {
+      if (AB & 32) return;
+      const uint32_t base = (p0 + min(s, npu - 1)) * VP;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const T* src = x + min(base + 2 * (t + j * LT), cmax);
+        if (AB & 16) {
+          const uint32_t c0 = (uint32_t)(j * LT) + wv * 64;  // this wave's 64 pairs of instruction j
+          __builtin_amdgcn_global_load_lds((const void*)src,
+                                           (__attribute__((address_space(3))) void*)(xb[s & 1] + 2 * min(c0, PAIRS - 64)),
+                                           16, 0, 0);
+        } else {
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[j]) : "v"(src) : "memory");
+        }
+      }
+    };
+    auto store = [&](uint32_t s, u64x2* r) {  // panel s into slot s & 1
+      T* dst = xb[s & 1];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        if ((j + 1) * LT <= (int)PAIRS || (uint32_t)(t + j * LT) < PAIRS)
+          *reinterpret_cast<u64x2*>(&dst[2 * (t + j * LT)]) = r[j];
+      if ((cols & 1) && p0 + s == npanels - 1) {  // odd cols: the last element from a scalar load
+        const uint32_t sl = cols - 1 - (p0 + s) * VP;
+        if ((uint32_t)t == (sl >> 1) % LT) dst[sl] = xlast;
+      }
+    };
+    auto wait_slot = [&](u64x2* r) {  // the oldest panel of the ring landed, (DX - 1) * NJ loads younger
+      if (AB & 32) return;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DX - 1) * NJ) : "memory");
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) tie(r[j]);
+    };
+#pragma unroll
+    for (int d = 0; d < DX; ++d) issue(d, R[d]);
+    wait_slot(R[0]);
+    store(0, R[0]);
+    issue(DX, R[0]);
+    barrier();
+    for (uint32_t base = 0; base < nsteps; base += DX) {
+#pragma unroll
+      for (int i = 0; i < DX; ++i) {
+        const uint32_t s = base + i;  // ring slot of panel s + 1: (s + 1) % DX == (i + 1) % DX
+        u64x2* r = R[(i + 1) % DX];
+        wait_slot(r);
+        if (!(AB & 2) && s + 1 < npu) store(s + 1, r);
+        issue(s + 1 + DX, r);
+        barrier();
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped loads past the last panel
+#pragma unroll
+    for (int d = 0; d < DX; ++d)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) tie(R[d][j]);
+  } else {
+    // ---- entries: EPT per lane per step at clamped indices, DE steps in flight
+    const int ct = t - LT;
+    const uint32_t lw = t & 63;
+    uint32_t EC[DE][EPT];
+    T EV[DE][EPT];
+    auto issue = [&](uint32_t s, uint32_t* c, T* v) {
+      if (AB & 64) return;
+      const uint32_t beg = segl[min(s, npad)];
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        const uint32_t q = min(beg + ct + j * CT, last);
+        c[j] = ald_u32_nt(ecode + q);
+        v[j] = ald_64_nt(evals + q);
+      }
+    };
+    auto sload32 = [](const uint32_t* p) {
+      uint32_t r;
+      asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
+      return r;
+    };
+    auto sload64 = [](const T* p) {
+      uint64_t r;
+      asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
+      return __builtin_bit_cast(T, r);
+    };
+    // step s: products from LDS panel s & 1; a run head sums its run across
+    // the following lanes (the layout keeps a row's entries of one segment
+    // adjacent) and updates its y row; requires max_seg <= EPT * CT
+    auto apply = [&](uint32_t s, const uint32_t* c, const T* v) {
+      const T* xs = xb[s & 1];
+      const uint32_t beg = segl[s], end = segl[s + 1];
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        const uint32_t q = beg + ct + j * CT;
+        const uint32_t code = c[j];
+        const bool valid = q < end;
+        const T p = valid ? v[j] * xs[code & 0xFFFF] : T(0);  // rounded product (contract off)
+        const bool own = valid && !(code & kVcCont);
+        const uint32_t row = (code >> 16) & 0x3FFF;
+        T acc = own ? ylds[row] + p : T(0);
+        bool more = own && (code & kVcMore);
+        bool fb = false;
+        uint32_t fbi = 0;
+        for (uint32_t k = 1; __builtin_amdgcn_ballot_w64(more) != 0; ++k) {  // wave-uniform trip count
+          const T pk = __shfl_down(p, k);
+          const uint32_t ck = __shfl_down(code, k);
+          if (more) {
+            if (lw + k < 64) {
+              acc = acc + pk;
+              more = (ck & kVcMore) != 0;
+            } else {  // the run continues in the next wave's lanes
+              fb = true;
+              fbi = q + k;
+              more = false;
+            }
+          }
+        }
+        for (uint64_t m = NOFB ? 0 : __builtin_amdgcn_ballot_w64(fb); m; m &= m - 1) {  // rare
+          const uint32_t l = (uint32_t)__builtin_ctzll(m);
+          uint32_t i = __builtin_amdgcn_readlane(fbi, l);
+          const uint64_t ab = __builtin_bit_cast(uint64_t, acc);
+          T a = __builtin_bit_cast(T, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)ab, l) |
+                                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(ab >> 32), l)
+                                           << 32));
+          uint32_t cd;
+          do {
+            cd = sload32(ecode + i);
+            const T pv = sload64(evals + i) * xs[cd & 0xFFFF];
+            a = a + pv;
+            ++i;
+          } while (cd & kVcMore);
+          if (lw == l) acc = a;
+        }
+        if (own) ylds[row] = acc;
+      }
+    };
+#pragma unroll
+    for (int d = 0; d < DE; ++d) issue(d, EC[d], EV[d]);
+    barrier();
+    for (uint32_t base = 0; base < nsteps; base += DE) {
+#pragma unroll
+      for (int i = 0; i < DE; ++i) {
+        const uint32_t s = base + i;
+        if (!(AB & 64)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DE - 1) * 2 * EPT) : "memory");  // step s landed
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+          tie(EC[i][j]);
+          tie(EV[i][j]);
+        }
+        // apply before the slot's reload: the old values die first, so the
+        // reload reuses their registers and the loop carries no copy of a
+        // register whose load is in flight (vmcnt_check: a copy there reads it)
+        if (!(AB & 1) && s < npu) apply(s, EC[i], EV[i]);
+        issue(s + DE, EC[i], EV[i]);
+        barrier();
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int d = 0; d < DE; ++d)
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        tie(EC[d][j]);
+        tie(EV[d][j]);
+      }
+  }
+  if (AB & 4) {
+    __syncthreads();
+    for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
+    return;
+  }
+  // ---- combine: ticket first (header comment)
+  constexpr uint32_t VRP = (VR + 1) & ~1u;
+  constexpr int NP = (VRP / 2 + VT - 1) / VT;  // row pairs per lane
+  static_assert(NP % 4 == 0, "whole chunks");
+  uint32_t* const published = tickets + nblocks;
+  if (t == 0) segl[0] = __hip_atomic_fetch_add(tickets + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const u64x2* const yl2 = reinterpret_cast<const u64x2*>(ylds);
+  const uint32_t npairs = (nr + 1) / 2;
+  if (segl[0] != (uint32_t)SPLIT - 1) {
+    const __amdgpu_buffer_rsrc_t mine = buf_rsrc(partial + ((size_t)h * nblocks + b) * VRP, 8 * VRP);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const uint32_t p = t + j * VT;
+      if (p < npairs) st_128_sc1(mine, 16 * p, yl2[p]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) __hip_atomic_fetch_add(published + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (t == 0) {
+    bool ok = false;
+    for (uint32_t spin = 0; spin < (1u << 18); ++spin) {
+      if (__hip_atomic_load(published + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)SPLIT - 1) {
+        ok = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (ok) {  // both counters back to zero for the next launch (every add of this one is in)
+      __hip_atomic_store(published + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {  // never observed: report it, and leave the counters for the host to reset
+      __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  __syncthreads();
+  // y = p0 + p1 + p2 + p3 in part order, row pairs in chunks of 4 per lane
+#pragma unroll
+  for (int j0 = 0; j0 < NP; j0 += 4) {
+    T acc[4][2];
+#pragma unroll
+    for (int q = 0; q < SPLIT; ++q) {
+      u64x2 v[4];
+      if ((uint32_t)q == h) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = yl2[min((uint32_t)(t + (j0 + j) * VT), VRP / 2 - 1)];
+      } else {
+        const __amdgpu_buffer_rsrc_t src = buf_rsrc(partial + ((size_t)q * nblocks + b) * VRP, 8 * VRP);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = ld_128_sc1(src, 16 * min((uint32_t)(t + (j0 + j) * VT), VRP / 2 - 1));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const T w0 = __builtin_bit_cast(T, (uint64_t)v[j].x), w1 = __builtin_bit_cast(T, (uint64_t)v[j].y);
+        acc[j][0] = q == 0 ? w0 : acc[j][0] + w0;
+        acc[j][1] = q == 0 ? w1 : acc[j][1] + w1;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t p = t + (j0 + j) * VT;
+      if (2 * p < nr) y_out[r0 + 2 * p] = acc[j][0];
+      if (2 * p + 1 < nr) y_out[r0 + 2 * p + 1] = acc[j][1];
+    }
+  }
+}
+
+template <typename T, int WL, int DX, int DE, bool NOFB = false, int AB = 0>
+static void launch_cfg(const VcacheArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((k_vquad<T, WL, DX, DE, 2, NOFB, AB>), dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s, a.seg, a.code,
+                     (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets,
+                     a.status, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.npad, a.last, a.beta);
+}
+
+// the register window (entries one step holds) of configuration v
+static uint32_t vquad_window(int v) { return (uint32_t)((16 - (v == 2 || v == 3 ? 4 : 3)) * 64 * 2); }
+
+template <typename T>
+static hipError_t launch_vquad_t(const VcacheArgs& a, hipStream_t s) {
+  if (!vcache_grid_ok(a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.panel,
+                      a.split, kVcSplit4) ||
+      !a.status || a.max_seg > vquad_window(a.variant))
+    return hipErrorInvalidValue;
+  switch (a.variant) {  // (loader waves, x panels in flight, entry steps in flight)
+    case 1: launch_cfg<T, 3, 4, 6>(a, s); break;
+    case 2: launch_cfg<T, 4, 4, 6>(a, s); break;
+    case 3: launch_cfg<T, 4, 6, 6>(a, s); break;
+    case 4: launch_cfg<T, 3, 3, 8>(a, s); break;
+    case 5: launch_cfg<T, 3, 3, 6, true>(a, s); break;  // timing probe: runs past a wave left unfinished (wrong y)
+    // ablations (timing probes, wrong y): 6 no apply, 7 no x stores, 8 no combine,
+    // 9 no apply and no x stores, 10 no step barriers (races), 11 skeleton (1|2|4)
+    case 6: launch_cfg<T, 3, 3, 6, false, 1>(a, s); break;
+    case 7: launch_cfg<T, 3, 3, 6, false, 2>(a, s); break;
+    case 8: launch_cfg<T, 3, 3, 6, false, 4>(a, s); break;
+    case 9: launch_cfg<T, 3, 3, 6, false, 3>(a, s); break;
+    case 10: launch_cfg<T, 3, 3, 6, false, 8>(a, s); break;
+    case 11: launch_cfg<T, 3, 3, 6, false, 7>(a, s); break;
+    case 12: launch_cfg<T, 3, 3, 6, false, 7 | 32>(a, s); break;   // skeleton, entries only
+    case 13: launch_cfg<T, 3, 3, 6, false, 7 | 64>(a, s); break;   // skeleton, x only
+    case 14: launch_cfg<T, 3, 3, 6, false, 7 | 16>(a, s); break;   // skeleton, x by LDS-DMA
+    case 15: launch_cfg<T, 3, 3, 6, false, 7 | 8>(a, s); break;    // skeleton without step barriers
+    case 16: launch_cfg<T, 3, 3, 6, false, 7 | 8 | 16>(a, s); break;  // ... and x by LDS-DMA
+    default: launch_cfg<T, 3, 3, 6>(a, s); break;
+  }
+  return hipGetLastError();
+}
+
+uint32_t vquad_max_window(int variant) { return vquad_window(variant); }
+
+hipError_t launch_vquad(int dtype, const VcacheArgs& a, hipStream_t s) {
+  return dtype ? launch_vquad_t<uint64_t>(a, s) : launch_vquad_t<double>(a, s);
+}
+
+}  // namespace hipspmv

@@ -68,9 +68,25 @@ __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt field");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// the same wait, tying the registers it makes valid: the compiler cannot
+// read them before it, nor hand their registers to another value while the
+// loads may still write them (an asm-load result it thought dead was reused
+// while the load was in flight: the round-4 probe's GPU fault)
+template <typename R>
+__device__ __forceinline__ void tie(R& r) {  // volatile asms keep their order: a tie after a wait stays after it
+  asm volatile("" : "+v"(r));
+}
+template <int N, typename... R>
+__device__ __forceinline__ void vm_wait_tie(R&... r) {
+  vm_wait<N>();
+  (tie(r), ...);
+}
 
 // ---- E / X / EX: free-running roles
-template <bool E, bool X, int WL, int P>
+// MAP 1: unit u's column part is (u mod 8) mod S, so with S = 4 each XCD
+// (round-robin dispatch: u mod 8) streams one 2 MiB part (its L2 holds it).
+// C11: the entry stream as 11-byte entries (u16 column, u8 row step, f64 value).
+template <bool E, bool X, int WL, int P, int MAP = 0, bool C11 = false>
 __global__ __launch_bounds__(kT) void k_free(const uint32_t* __restrict__ code, const double* __restrict__ vals,
                                              const double* __restrict__ x, double* __restrict__ out,
                                              uint32_t part_cols, int S) {
@@ -79,7 +95,7 @@ __global__ __launch_bounds__(kT) void k_free(const uint32_t* __restrict__ code, 
   constexpr int WC = kNW - WL, CT = WC * 64, EPT = 2, DE = 4;
   const int t = threadIdx.x;
   const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
-  const uint32_t u = blockIdx.x, h = (u / 8) % (uint32_t)S;
+  const uint32_t u = blockIdx.x, h = MAP ? (u & 7) % (uint32_t)S : (u / 8) % (uint32_t)S;
   const double* xp = x + (size_t)h * part_cols;
   double acc = 0.0;
   if (w < WL) {
@@ -107,11 +123,16 @@ __global__ __launch_bounds__(kT) void k_free(const uint32_t* __restrict__ code, 
     const uint32_t nsteps = (kNE + STEP - 1) / STEP;
     uint32_t C[DE][EPT];
     double V[DE][EPT];
+    const uint16_t* cu16 = reinterpret_cast<const uint16_t*>(code) + (size_t)u * kNE;
+    const uint8_t* du8 = reinterpret_cast<const uint8_t*>(code) + (size_t)kNE * 256 * 2 + (size_t)u * kNE;
     auto load = [&](uint32_t s, uint32_t* c, double* v) {
 #pragma unroll
       for (int j = 0; j < EPT; ++j) {
         const uint32_t i = min(s * STEP + j * CT + ct, kNE - 1);
-        c[j] = __builtin_nontemporal_load(cu + i);
+        if (C11)
+          c[j] = (uint32_t)__builtin_nontemporal_load(cu16 + i) | (uint32_t)__builtin_nontemporal_load(du8 + i) << 16;
+        else
+          c[j] = __builtin_nontemporal_load(cu + i);
         v[j] = __builtin_nontemporal_load(vu + i);
       }
     };
@@ -132,12 +153,81 @@ __global__ __launch_bounds__(kT) void k_free(const uint32_t* __restrict__ code, 
   if (t == 0) out[u] = pad[5] + pad[999];
 }
 
+// ---- EW: the entry stream with 16-byte loads (each lane four consecutive
+// entries: one dwordx4 of codes, two of values), free-running, beside the
+// free-running x loaders (X) of k_free
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+template <bool X, int WL, int P, int MAP, int DE>
+__global__ __launch_bounds__(kT) void k_wide(const uint32_t* __restrict__ code, const double* __restrict__ vals,
+                                             const double* __restrict__ x, double* __restrict__ out,
+                                             uint32_t part_cols, int S) {
+  __shared__ double xb[2][P];
+  __shared__ double pad[12000];
+  constexpr int WC = kNW - WL, CT = WC * 64;
+  const int t = threadIdx.x;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+  const uint32_t u = blockIdx.x, h = MAP ? (u & 7) % (uint32_t)S : (u / 8) % (uint32_t)S;
+  const double* xp = x + (size_t)h * part_cols;
+  double acc = 0.0;
+  if (w < WL) {
+    if constexpr (X && WL > 0) {
+      constexpr uint32_t PAIRS = P / 2, ND = (PAIRS + WL * 64 - 1) / (WL * 64);
+      const uint32_t npan = part_cols / P;
+      for (uint32_t p = 0; p < npan; ++p) {
+        double* slot = xb[p & 1];
+#pragma unroll
+        for (uint32_t j = 0; j < ND; ++j) {
+          const uint32_t c0 = (j * WL + w) * 64;
+          if (c0 + lane < PAIRS)
+            __builtin_amdgcn_global_load_lds((const void*)(xp + (size_t)p * P + 2 * (c0 + lane)),
+                                             (lds_void*)(slot + 2 * c0), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ND) : "memory");
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else {
+    const int ct = t - WL * 64;
+    const uint32_t* cu = code + (size_t)u * kNE;
+    const double* vu = vals + (size_t)u * kNE;
+    constexpr uint32_t STEP = 4 * CT;  // entries per step
+    constexpr uint32_t NSTEPS = (kNE + STEP - 1) / STEP;
+    u32x4v C[DE];
+    double V[DE][4];
+    auto load = [&](uint32_t s, int i) {
+      const uint32_t e = min(s * STEP + 4 * ct, kNE - 4);  // 4 consecutive entries, 16-B aligned
+      C[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(cu + e));
+      const u32x4v v0 = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(vu + e));
+      const u32x4v v1 = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(vu + e + 2));
+      V[i][0] = __builtin_bit_cast(double, (uint64_t)v0.x | (uint64_t)v0.y << 32);
+      V[i][1] = __builtin_bit_cast(double, (uint64_t)v0.z | (uint64_t)v0.w << 32);
+      V[i][2] = __builtin_bit_cast(double, (uint64_t)v1.x | (uint64_t)v1.y << 32);
+      V[i][3] = __builtin_bit_cast(double, (uint64_t)v1.z | (uint64_t)v1.w << 32);
+    };
+#pragma unroll
+    for (int d = 0; d < DE; ++d) load(d, d);
+    constexpr uint32_t PADDED = (NSTEPS + DE - 1) / DE * DE;
+    for (uint32_t b = 0; b < PADDED; b += DE) {
+#pragma unroll
+      for (int i = 0; i < DE; ++i) {
+        acc += (double)C[i].x * V[i][0] + (double)C[i].y * V[i][1] + (double)C[i].z * V[i][2] +
+               (double)C[i].w * V[i][3];
+        load(b + i + DE, i);
+      }
+    }
+  }
+  pad[t] = acc + xb[t & 1][t];
+  __syncthreads();
+  if (t == 0) out[u] = pad[5] + pad[999];
+}
+
 // ---- A: barrier-free vector cache skeleton
 // entries of unit u: [panel][compute wave][EPW], EPW <= 64 (one per lane)
 template <int R, int NS, int P, int WL, int L, int DE>
 __global__ __launch_bounds__(kT) void k_async(const uint32_t* __restrict__ code, const double* __restrict__ vals,
                                               const double* __restrict__ x, double* __restrict__ out,
                                               uint32_t part_cols, int S, uint32_t epw) {
+  static_assert(DE == 8, "ring (the final wait ties 8 slots)");
   constexpr int WC = kNW - WL;
   constexpr uint32_t RW = R / WC;  // rows owned by a compute wave
   __shared__ double ylds[R];
@@ -204,7 +294,7 @@ __global__ __launch_bounds__(kT) void k_async(const uint32_t* __restrict__ code,
 #pragma unroll
       for (int i = 0; i < DE; ++i) {
         const uint32_t p = b + i;
-        vm_wait<2 * (DE - 1)>();  // slot i landed, DE - 1 panels of entries still in flight
+        vm_wait_tie<2 * (DE - 1)>(C[i], V[i]);  // slot i landed, DE - 1 panels of entries still in flight
         if (p < npan) {
           const uint32_t need = WL * (p / NS + 1);
           while (lds_ld(&landed[p % NS]) < need) __builtin_amdgcn_s_sleep(1);
@@ -219,7 +309,7 @@ __global__ __launch_bounds__(kT) void k_async(const uint32_t* __restrict__ code,
         load(p + DE, i);
       }
     }
-    vm_wait<0>();
+    vm_wait_tie<0>(C[0], C[1], C[2], C[3], C[4], C[5], C[6], C[7], V[0], V[1], V[2], V[3], V[4], V[5], V[6], V[7]);
   }
   __syncthreads();
   if (t == 0) out[u] = ylds[5] + ylds[R - 1];
@@ -251,7 +341,7 @@ __global__ __launch_bounds__(kT) void k_gather(const uint32_t* __restrict__ code
   // per step p: gather x for p + 1 (its code landed), entries of p + DE, wait
   // for the gather of p, apply p.  The loop starts at p = -DE with dummy
   // gathers so every wait count is the steady-state one.
-  static_assert(DE % 2 == 0 && DE >= 4, "ring");
+  static_assert(DE == 8, "ring (the final wait ties 8 slots)");
   uint32_t C[DE];
   double V[DE], X[2];
   auto load = [&](int p, int i) {
@@ -263,23 +353,28 @@ __global__ __launch_bounds__(kT) void k_gather(const uint32_t* __restrict__ code
     const size_t col = p >= 0 ? min((size_t)p * P + (c & 0xFFFF) % P, (size_t)part_cols - 1) : 0;
     X[slot] = ald_f64(xp + col);
   };
-  const int padded = (int)((npan + DE - 1) / DE * DE);
-  for (int b = -DE; b < padded; b += DE) {
+  // fully unrolled (S = 4 parts: npan = 2^18 / P panels, a constant): no loop
+  // back-edge, so no phi copy of a ring register whose load is in flight
+  constexpr int NPAN = (int)((kCols / 4) / P), PADDED = (NPAN + DE - 1) / DE * DE;
+#pragma unroll
+  for (int b = -DE; b < PADDED; b += DE) {
 #pragma unroll
     for (int i = 0; i < DE; ++i) {
       const int p = b + i;
-      vm_wait<3 * (DE - 2)>();  // the code of p + 1 landed
+      vm_wait_tie<3 * (DE - 2)>(C[(i + 1) % DE]);  // the code of p + 1 landed
       gather(p + 1, C[(i + 1) % DE], (i + 1) & 1);
+      vm_wait_tie<2>(C[i], V[i]);  // entries of p landed (older than the gather of p + 1)
+      const uint32_t c = C[i];  // slot i is reloaded next
+      const double v = V[i];
       load(p + DE, i);
-      vm_wait<5>();  // the gather of p landed
-      if (p >= 0 && p < (int)npan) {
+      vm_wait_tie<5>(X[i & 1]);  // the gather of p landed
+      if (p >= 0 && p < NPAN) {
         if (D > 0 && p >= D) {
           while (lds_ld(&done[(p - D) & 63]) < (uint32_t)WC) __builtin_amdgcn_s_sleep(1);
         }
         if (lane < epw) {
-          const uint32_t c = C[i];
           const uint32_t row = ((c >> 16) * RW) >> 16;
-          yw[row] = yw[row] + V[i] * X[i & 1];
+          yw[row] = yw[row] + v * X[i & 1];
         }
         if (D > 0) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -291,7 +386,8 @@ __global__ __launch_bounds__(kT) void k_gather(const uint32_t* __restrict__ code
       }
     }
   }
-  vm_wait<0>();
+  vm_wait_tie<0>(C[0], C[1], C[2], C[3], C[4], C[5], C[6], C[7], V[0], V[1], V[2], V[3], V[4], V[5], V[6], V[7],
+                 X[0], X[1]);
   __syncthreads();
   if (t == 0) out[u] = ylds[5] + ylds[R - 1];
 }
@@ -356,6 +452,22 @@ int main(int argc, char** argv) {
         timeit(nm, [&] { hipLaunchKernelGGL((k_free<false, true, 3, 4000>), U, kT, 0, 0, code, vals, x, out, pc, S); }, 0, xb);
         std::snprintf(nm, sizeof nm, "EX free S=%d WL=3 P=4000", S);
         timeit(nm, [&] { hipLaunchKernelGGL((k_free<true, true, 3, 4000>), U, kT, 0, 0, code, vals, x, out, pc, S); }, eb, xb);
+      }
+      if (want("M") && S == 4) {
+        timeit("X S=4 WL=3 P=4000 XCD map", [&] { hipLaunchKernelGGL((k_free<false, true, 3, 4000, 1>), U, kT, 0, 0, code, vals, x, out, pc, S); }, 0, xb);
+        timeit("EX free S=4 WL=3 P=4000 XCD map", [&] { hipLaunchKernelGGL((k_free<true, true, 3, 4000, 1>), U, kT, 0, 0, code, vals, x, out, pc, S); }, eb, xb);
+        timeit("E 13 waves, 11-byte entries", [&] { hipLaunchKernelGGL((k_free<true, false, 3, 4000, 0, true>), U, kT, 0, 0, code, vals, x, out, pc, S); }, eb, 0);
+        timeit("EX free S=4 XCD map, 11-byte entries", [&] { hipLaunchKernelGGL((k_free<true, true, 3, 4000, 1, true>), U, kT, 0, 0, code, vals, x, out, pc, S); }, eb, xb);
+      }
+      if (want("W")) {
+        std::snprintf(nm, sizeof nm, "E 13 waves, 16-B loads (DE=3)");
+        timeit(nm, [&] { hipLaunchKernelGGL((k_wide<false, 3, 4000, 1, 3>), U, kT, 0, 0, code, vals, x, out, pc, S); }, eb, 0);
+        std::snprintf(nm, sizeof nm, "EX free S=%d XCD map, 16-B entry loads (DE=3)", S);
+        timeit(nm, [&] { hipLaunchKernelGGL((k_wide<true, 3, 4000, 1, 3>), U, kT, 0, 0, code, vals, x, out, pc, S); }, eb, xb);
+        std::snprintf(nm, sizeof nm, "EX free S=%d XCD map, 16-B entry loads (DE=2)", S);
+        timeit(nm, [&] { hipLaunchKernelGGL((k_wide<true, 3, 4000, 1, 2>), U, kT, 0, 0, code, vals, x, out, pc, S); }, eb, xb);
+        std::snprintf(nm, sizeof nm, "EX free S=%d, 16-B entry loads (DE=3)", S);
+        timeit(nm, [&] { hipLaunchKernelGGL((k_wide<true, 3, 4000, 0, 3>), U, kT, 0, 0, code, vals, x, out, pc, S); }, eb, xb);
       }
       if (want("A")) {
         if (S == 3) {  // R 12352: ring of 4 x 1920 columns (60 KiB)

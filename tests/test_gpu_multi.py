@@ -38,7 +38,8 @@ def test_multi_ordered_matches_oracle(gpu, name, ndev, beta):
 
 
 @pytest.mark.parametrize("kernel,mode", [("vcache_split", hs.MODE_FAST), ("csr_vector", hs.MODE_FAST),
-                                         ("vcache", hs.MODE_ORDERED), ("sell", hs.MODE_ORDERED)])
+                                         ("vcache", hs.MODE_ORDERED), ("sell", hs.MODE_ORDERED),
+                                         ("vcache_split4", hs.MODE_FAST)])
 def test_multi_equals_single_device(gpu, kernel, mode):
     n = 1 << 17
     rowptr, colind, vals = hs.gen_stripe_csr(0, n, 1 << 20, 32)
@@ -133,3 +134,39 @@ def test_rccl_collectives_single_rank(gpu, tmp_path):
     out = subprocess.run([sys.executable, str(script), hs.PKG_DIR], env=env, capture_output=True, text=True,
                          timeout=240)
     assert out.returncode == 0 and "rccl ok" in out.stdout, out.stdout[-2000:] + out.stderr[-2000:]
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.uint64])
+def test_multi_wcsr_wide_skewed(gpu, dtype):
+    # wcsr on row shards of a wide, skewed matrix (include/hipspmv.h, Row
+    # partitions: the one documented exception) -- u64 bit-identical to the
+    # single device, f64 within the FAST bound of the oracle on every shard
+    rng = np.random.default_rng(8)
+    rows, cols = 4096, (1 << 21) + 5
+    want = rng.zipf(1.5, rows).clip(0, 20000)
+    per_row = [np.unique(rng.integers(0, cols, int(k))) for k in want]
+    lens = np.array([c.size for c in per_row], np.int64)
+    rowptr = np.zeros(rows + 1, np.uint32)
+    rowptr[1:] = np.cumsum(lens)
+    colind = np.concatenate(per_row).astype(np.uint32)
+    if dtype == np.float64:
+        vals, x = rng.uniform(-1, 1, colind.size), rng.uniform(-1, 1, cols)
+    else:
+        vals = rng.integers(0, 2**64, colind.size, dtype=np.uint64)
+        x = rng.integers(0, 2**64, cols, dtype=np.uint64)
+    colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+    one = hs.Handle.from_csc(colptr, rowind, cvals, rows, cols)
+    one.set_kernel("wcsr")
+    y1 = one.exec(x, beta=0, mode=hs.MODE_FAST)
+    one.close()
+    m = hs.MultiHandle(colptr, rowind, cvals, rows, cols, _devices(3))
+    m.set_kernel("wcsr")
+    y3 = m.exec(x, beta=0, mode=hs.MODE_FAST)
+    m.close()
+    y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=rows)
+    if dtype == np.uint64:
+        assert y3.tobytes() == y1.tobytes() == y_ref.tobytes()
+    else:
+        absprod = np.bincount(np.repeat(np.arange(rows), lens), weights=np.abs(vals * x[colind]), minlength=rows)
+        bound = 2.0 * np.maximum(lens, 1) * 2.0 ** -53 * absprod + 1e-300
+        assert np.all(np.abs(y3 - y_ref) <= bound) and np.all(np.abs(y1 - y_ref) <= bound)

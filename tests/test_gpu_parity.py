@@ -35,7 +35,8 @@ def _csr_stats(rows, cols, colptr, rowind, vals, x):
 def _check(name, rows, cols, colptr, rowind, vals, x, kernel, beta, mode=hs.MODE_ORDERED, y0=None):
     h = hs.Handle.from_csc(colptr, rowind, vals, rows, cols)
     if (kernel == "vcache" and not h.stat("vcache_eligible")) or \
-            (kernel == "vcache_split" and not h.stat("vcache_split_eligible")):
+            (kernel == "vcache_split" and not h.stat("vcache_split_eligible")) or \
+            (kernel == "vcache_split4" and not h.stat("vcache_split4_eligible")):
         pytest.skip("vcache not eligible")
     h.set_kernel(kernel)
     npdt = vals.dtype
@@ -58,7 +59,8 @@ def _check(name, rows, cols, colptr, rowind, vals, x, kernel, beta, mode=hs.MODE
 
 
 @pytest.mark.parametrize("name", fx.ALL_FIXTURES)
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr",
+                                    "vcache_split4"])
 @pytest.mark.parametrize("beta", [0, 1])
 def test_fixtures(gpu, name, kernel, beta):
     rows, cols, colptr, rowind, vals = fx.load(name)
@@ -100,7 +102,8 @@ def _random_csc(rows, cols, density, rng, dtype=np.float64, empty_rows=True, lon
 # panel patched); (900, 14001): 4 panels, column parts of 1, 1 and 2 (vc_part_first)
 @pytest.mark.parametrize("shape", [(1, 1), (1, 300), (300, 1), (257, 1000), (5000, 333), (3000, 20000),
                                    (700, 20001), (900, 14001)])
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr",
+                                    "vcache_split4"])
 def test_random_ragged(gpu, shape, kernel):
     rng = np.random.default_rng(shape[0] * 31 + shape[1])
     rows, cols = shape
@@ -112,7 +115,8 @@ def test_random_ragged(gpu, shape, kernel):
         _check(f"rand{shape}", rows, cols, colptr, rowind, vals, x, kernel, beta, mode)
 
 
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr",
+                                    "vcache_split4"])
 def test_random_u64_wraparound(gpu, kernel):
     rng = np.random.default_rng(5)
     rows, cols = 4000, 9000
@@ -122,7 +126,8 @@ def test_random_u64_wraparound(gpu, kernel):
         _check("u64", rows, cols, colptr, rowind, vals, x, kernel, beta, hs.MODE_FAST)
 
 
-@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr"])
+@pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr",
+                                    "vcache_split4"])
 def test_random_duplicates(gpu, kernel):
     # repeated (row, col) entries (5 % of a ragged matrix with a full-width row):
     # ORDERED kernels add each copy in CSC order, bit for bit; FAST within the bound
@@ -464,6 +469,79 @@ def test_split_combine_concurrent_streams(gpu):
             assert outs[i][k].cpu().numpy().tobytes() == want[i], (i, k)
 
 
+# ---- k_vquad (vcache_split4, csrc/vquad.hip): four column parts, x panels in
+# flight in registers; every configuration on the full C3 matrix and on
+# ragged / wide shapes: deterministic, within the FAST bound, u64 exact, and
+# no combine hand-off timed out
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_vquad_variants(gpu, variant):
+    cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20), (20000, 1 << 22),
+             (16385, 7937)]
+    ran = 0
+    for rows, cols in cases:
+        rng = np.random.default_rng(rows + variant)
+        if cols >= 1 << 20:
+            rowptr, colind, vals = hs.gen_stripe_csr(0, rows, cols, 32)
+        else:
+            lens = rng.integers(0, 12, rows)
+            rowptr = np.zeros(rows + 1, np.uint32)
+            rowptr[1:] = np.cumsum(lens)
+            colind = np.concatenate([np.sort(rng.choice(cols, n, replace=False)) for n in lens]).astype(np.uint32)
+            vals = rng.uniform(-1, 1, colind.size)
+        x = rng.uniform(-1, 1, cols)
+        h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+        if not h.stat("vcache_split4_eligible"):
+            h.close()
+            continue
+        h.set_kernel("vcache_split4")
+        h.set_option("vquad_variant", variant)
+        colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+        lens = np.diff(rowptr.astype(np.int64))
+        absprod = np.bincount(np.repeat(np.arange(rows), lens), weights=np.abs(vals * x[colind]), minlength=rows)
+        for beta in (0, 1):
+            y0 = rng.uniform(-1, 1, rows)
+            y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else None), rows=rows)
+            ys = [h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST) for _ in range(2)]
+            assert ys[0].tobytes() == ys[1].tobytes(), (rows, cols, beta)  # deterministic
+            bound = 2.0 * (lens + 1) * 2.0 ** -53 * (absprod + (np.abs(y0) if beta else 0)) + 1e-300
+            assert np.all(np.abs(ys[0] - y_ref) <= bound), (rows, cols, beta)
+        if rows <= 70001:  # the u64 semiring: exact mod 2^64
+            uv = rng.integers(0, 2**64, colind.size, dtype=np.uint64)
+            ux = rng.integers(0, 2**64, cols, dtype=np.uint64)
+            hu = hs.Handle.from_csr(rowptr, colind, uv, rows, cols)
+            hu.set_kernel("vcache_split4")
+            hu.set_option("vquad_variant", variant)
+            _, _, cuv = oracle.csr2csc(rows, cols, rowptr, colind, uv)
+            assert hu.exec(ux, beta=0, mode=hs.MODE_FAST).tobytes() == \
+                oracle.spmv_csc(colptr, rowind, cuv, ux, rows=rows).tobytes(), (rows, cols)
+            assert hu.stat("handoff_timeouts") == 0
+            hu.close()
+        assert h.stat("handoff_timeouts") == 0
+        h.close()
+        ran += 1
+    assert ran >= 5
+
+
+def test_vquad_c3_full_size(gpu):
+    # the four-part kernel on full C3: x streamed into LDS per launch is 64 row
+    # blocks x 8 MB (three parts: 85 x 8 MB); deterministic and within the bound
+    n = 1 << 20
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+    x = hs.gen_vector(n, 3)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    assert h.stat("vcache_split4_eligible") == 1
+    assert h.stat("vcache_split4_x_bytes") == 64 * 8 * n
+    h.set_kernel("vcache_split4")
+    ys = [h.exec(x, beta=0, mode=hs.MODE_FAST) for _ in range(3)]
+    assert ys[0].tobytes() == ys[1].tobytes() == ys[2].tobytes()
+    colptr, rowind, cvals = oracle.csr2csc(n, n, rowptr, colind, vals)
+    y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=n)
+    absprod = np.zeros(n)
+    np.add.at(absprod, np.repeat(np.arange(n), 32), np.abs(vals * x[colind]))
+    assert np.all(np.abs(ys[0] - y_ref) <= _fast_bound(np.full(n, 32), absprod, 0))
+    assert h.stat("handoff_timeouts") == 0
+
+
 # ---- experimental vcache variants (never chosen by AUTO): four column parts
 # and the LDS-DMA x loader.  Addressing is replayed on the CPU by
 # tests/test_vcache_sim.py; on the GPU they run only with HIPSPMV_EXPERIMENTAL=1
@@ -473,11 +551,10 @@ EXPERIMENTAL = os.environ.get("HIPSPMV_EXPERIMENTAL") == "1"
 
 @pytest.mark.skipif(not EXPERIMENTAL, reason="experimental kernels: set HIPSPMV_EXPERIMENTAL=1")
 @pytest.mark.parametrize("kernel,dma,xlane,xmap", [
-    ("vcache_split4", 0, 0, 0), ("vcache_split4", 1, 0, 0), ("vcache_split", 1, 0, 0), ("vcache", 1, 0, 0),
+    ("vcache_split", 1, 0, 0), ("vcache", 1, 0, 0),
     ("wgather", 0, 0, 0), ("vcache", 0, 1, 0), ("vcache", 0, 2, 0), ("vcache_split", 0, 1, 0),
-    ("vcache_split", 0, 2, 0), ("vcache_split", 1, 2, 0), ("vcache_split4", 0, 2, 0), ("wgather", 0, 2, 0),
-    ("vcache", 0, 3, 0), ("vcache_split", 0, 3, 0), ("vcache_split4", 0, 0, 1), ("vcache_split4", 0, 3, 1),
-    ("vcache_split4", 0, 2, 1)])
+    ("vcache_split", 0, 2, 0), ("vcache_split", 1, 2, 0), ("wgather", 0, 2, 0),
+    ("vcache", 0, 3, 0), ("vcache_split", 0, 3, 0)])
 def test_experimental_vcache_variants(gpu, kernel, dma, xlane, xmap):
     cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20), (20000, 1 << 22)]
     for rows, cols in cases:
