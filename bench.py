@@ -95,6 +95,13 @@ def parse():
     p.add_argument("--no-strong", action="store_true",
                    help="c3: skip the strong-scaling C4 block (the 2^s x 2^s stripe matrix split over the N ranks)")
     p.add_argument("--strong-scale", type=int, default=24, help="log2 of the strong block's matrix dimension (C4: 24)")
+    p.add_argument("--no-c5-shards", action="store_true",
+                   help="c3 at N=1: skip the C5 per-shard block (every shard of the 8-way partition timed on this GPU)")
+    p.add_argument("--c5-scale", type=int, default=24, help="log2 of the C5 block's R-MAT dimension (C5: 24)")
+    p.add_argument("--c5-parts", type=int, default=8)
+    p.add_argument("--c5-partition", default="cost", choices=["cost", "nnz"],
+                   help="C5 row partition: wcsr cost model (entries + segments + rows) or nonzeros only")
+    p.add_argument("--c5-steps", type=int, default=50)
     p.add_argument("--parity-rows", type=int, default=2000,
                    help="rows of each rank's shard recomputed by the oracle after timing (per-rank parity)")
     return p.parse_args()
@@ -520,6 +527,65 @@ def run_strong(a, dist, dev, local: int, rank: int, world: int, stream) -> dict:
             "setup_ns_lib": setup_ns}
 
 
+def run_c5_shards(a, dev, stream) -> dict:
+    """SURVEY §8(d)'s C5 row on one GPU: R-MAT scale s (24: C5), edge factor 16, cut into --c5-parts row
+    shards by the wcsr cost model (hipspmv.c5_partition), and every shard run on this GPU in turn: AUTO's
+    FAST kernel, its per-launch time (HIP events over --c5-steps back-to-back launches after a warmup),
+    alg bytes and roofline fraction, and sampled rows against the oracle.  max/min of the shard times is
+    the load balance an 8-GPU C5 step would see (the slowest rank sets it); value = all shards' flops /
+    the slowest shard's time (the N-GPU strong-scaling estimate from one GPU, x replicated)."""
+    parts, scale = a.c5_parts, a.c5_scale
+    t0 = time.perf_counter()
+    bounds, counts = hs.c5_partition(scale, parts, model=a.c5_partition)
+    part_s = time.perf_counter() - t0
+    n = 1 << scale
+    x = torch.from_numpy(hs.gen_vector(n, 3)).to(dev)
+    shards = []
+    total_nnz = 0
+    for r in range(parts):
+        row0, row1 = int(bounds[r]), int(bounds[r + 1])
+        if row1 == row0:  # a tiny matrix snapped to SHARD_ALIGN rows can leave a shard empty
+            shards.append({"shard": r, "rows": [row0, row1], "nnz": 0, "kernel": None})
+            continue
+        tg = time.perf_counter()
+        rowptr, colind, vals = hs.gen_rmat_rows(scale, row0, row1, 16, 4)
+        gen_s = time.perf_counter() - tg
+        ts = time.perf_counter()
+        h = hs.Handle.from_csr(rowptr, colind, vals, row1 - row0, n, device=dev.index or 0)
+        setup_s = time.perf_counter() - ts
+        y = torch.empty(row1 - row0, dtype=torch.float64, device=dev)
+        kname = h.kernel_name(hs.MODE_FAST)
+        for _ in range(3):
+            h.exec_device(x, y, beta=0, mode=hs.MODE_FAST, stream=stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(a.c5_steps):
+            h.exec_device(x, y, beta=0, mode=hs.MODE_FAST, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / a.c5_steps
+        alg = h.stat("alg_bytes")
+        parity = shard_parity(rowptr, colind, vals, x.cpu().numpy(), y.cpu().numpy(), hs.MODE_FAST,
+                              sample_rows(rowptr, 200, seed=r))
+        shards.append({"shard": r, "rows": [row0, row1], "nnz": int(colind.size), "kernel": kname,
+                       "kernel_us": round(us, 3), "roofline_frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                       "segments": h.stat("wcsr_segments") if kname == "wcsr" else None,
+                       "parity": parity, "gen_s": round(gen_s, 2), "setup_s": round(setup_s, 2)})
+        total_nnz += int(colind.size)
+        h.close()
+        del y
+        torch.cuda.empty_cache()
+    times = [s["kernel_us"] for s in shards if s["kernel"]]
+    return {"workload": f"C5 R-MAT scale {scale} (a,b,c=0.57,0.19,0.19), edge factor 16, {parts} row shards "
+                        f"({a.c5_partition} partition), each run alone on this GPU", "mode": "fast",
+            "nnz_total": total_nnz, "max_over_min": round(max(times) / min(times), 4),
+            "slowest_us": max(times), "min_roofline_frac": min(s["roofline_frac"] for s in shards if s["kernel"]),
+            "value": round(2.0 * total_nnz / (max(times) * 1e-6) / 1e9, 2), "unit": "GFLOP/s",
+            "value_note": "all shards' flops / the slowest shard's time: the 8-GPU strong-scaling step, x replicated",
+            "partition_s": round(part_s, 2), "shards": shards}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -722,6 +788,14 @@ def main():
         except Exception as e:  # reported, never fatal for the headline line
             strong = {"error": f"{type(e).__name__}: {e}"}
 
+    # C5 per-shard block beside the C3 headline, N=1 only
+    c5 = None
+    if a.workload == "c3" and world == 1 and not a.no_c5_shards and not a.rocprof_child:
+        try:
+            c5 = run_c5_shards(a, dev, stream)
+        except Exception as e:  # reported, never fatal for the headline line
+            c5 = {"error": f"{type(e).__name__}: {e}"}
+
     # parity on rank 0 at N=1: the timed kernels' outputs vs the oracle (checker only)
     cpu = None
     cpu_mt = None
@@ -815,6 +889,7 @@ def main():
             "rank_kernel_us": [round(v * 1e3, 3) for v in rank_kern_ms],
             "rank_parity": rank_parity,
             "strong": strong,
+            "c5_shards": c5,
             # host time to generate the synthetic shard / to build the handle (transpose-free CSR
             # create: validation, upload, every layout AUTO runs); setup_ns_lib: the library's own
             # setup_ns statistic after the timed runs (create + layouts built later, if any)

@@ -169,6 +169,21 @@ int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void 
  * "profile_units" "profile_span_cycles". */
 int hipspmv_stat(hipspmv_t *h, const char *key, uint64_t *out);
 
+/* Hardware counters behind the cache statistics (the reference reads its
+ * counters from the accelerator after a run, HardwareSpMVNewCache.cpp:161-173).
+ * hipspmv_pmc_counter: mean per dispatch of `counter` over the dispatches whose
+ * kernel name contains `kernel` (NULL: any hipspmv kernel; the instantiation
+ * with the most dispatches) in a rocprofv3 --pmc counter_collection.csv, or
+ * the per_dispatch value of a tools/pmc_summary.py summary; no device needed.
+ * hipspmv_attach_pmc: such a CSV (collected for this handle's kernel; NULL or
+ * "" detaches) backs the stat keys "read_misses" (TCC_MISS), "hazard_stalls"
+ * (SQ_LDS_BANK_CONFLICT) and "capacity_stalls" (TCP_PENDING_STALL_CYCLES) of
+ * the last kernel when it holds them; "read_misses_model" and
+ * "hazard_stalls_model" keep the layout values; "pmc_attached". */
+int hipspmv_pmc_counter(const char *csv_path, const char *kernel, const char *counter, double *mean,
+                        uint64_t *dispatches);
+int hipspmv_attach_pmc(hipspmv_t *h, const char *csv_path);
+
 /* Name of the kernel that HIPSPMV_MODE `mode` would run (static string). */
 const char *hipspmv_kernel_name(hipspmv_t *h, int mode);
 

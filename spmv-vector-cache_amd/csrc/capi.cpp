@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <fstream>
 #include <new>
 #include <string>
 
@@ -113,6 +114,9 @@ struct hipspmv_handle {
   // bit 0: a k_vquad combine hand-off wait timed out (never observed; the
   // launch's y is then wrong and the scratch counters need a reset)
   uint32_t* d_status = nullptr;
+  // hipspmv_attach_pmc: a rocprofv3 --pmc counter CSV whose counters back the
+  // cache statistics read_misses / hazard_stalls / capacity_stalls
+  std::string pmc_csv;
   // option "wgather_chunk": row blocks per k_wgather launch:
   // one launch's blocks are all resident at once (2 per CU), so they walk
   // the x windows together and the gathered window stays in L2
@@ -783,6 +787,35 @@ static int read_status(hipspmv_t* h, uint32_t* out) {
   return HIPSPMV_OK;
 }
 
+// The last kernel's symbol prefix in a rocprofv3 CSV (dtype-qualified where
+// one kernel template has several geometries)
+static std::string kernel_symbol(const hipspmv_t* h) {
+  const std::string T = h->dtype == HIPSPMV_U64 ? "unsigned long" : "double";
+  switch (h->last_kernel) {
+    case HIPSPMV_KERNEL_VCACHE: return "k_vcache<" + T + ", 1,";
+    case HIPSPMV_KERNEL_VCACHE_SPLIT: return "k_vcache<" + T + ", 3,";
+    case HIPSPMV_KERNEL_VCACHE_SPLIT4: return "k_vquad<" + T + ",";
+    case HIPSPMV_KERNEL_WGATHER: return "k_wgather<" + T + ",";
+    case HIPSPMV_KERNEL_CSR_LANE: return "k_csr_lane<" + T + ">";
+    case HIPSPMV_KERNEL_CSR_VECTOR: return "k_csr_vector<" + T + ", false>";
+    case HIPSPMV_KERNEL_WCSR: return "k_csr_vector<" + T + ", true>";
+    case HIPSPMV_KERNEL_SELL: return "k_sell";
+    default: return "hipspmv::";
+  }
+}
+
+// A counter of the attached PMC CSV for the last kernel: true and *v set when
+// the CSV holds it
+static bool pmc_value(const hipspmv_t* h, const char* counter, uint64_t* v) {
+  if (h->pmc_csv.empty()) return false;
+  double m = 0;
+  uint64_t n = 0;
+  if (hipspmv_pmc_counter(h->pmc_csv.c_str(), kernel_symbol(h).c_str(), counter, &m, &n) != HIPSPMV_OK || !n)
+    return false;
+  *v = (uint64_t)std::llround(m);
+  return true;
+}
+
 static int resolve_pending(hipspmv_t* h) {
   if (!h->pending) return HIPSPMV_OK;
   DeviceGuard g(h->device);
@@ -1060,14 +1093,21 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "clock_khz") *out = (uint64_t)h->clock_khz;
   // The reference accelerator's cache statistics (HardwareSpMVNewCache.cpp:
   // 189-204), restated for the last kernel's layout:
-  else if (k == "read_misses" || k == "hazard_stalls" || k == "ocm_depth") {
+  else if (k == "pmc_attached") *out = h->pmc_csv.empty() ? 0 : 1;
+  else if ((k == "read_misses" && pmc_value(h, "TCC_MISS", out)) ||
+           (k == "hazard_stalls" && pmc_value(h, "SQ_LDS_BANK_CONFLICT", out)) ||
+           (k == "capacity_stalls" && pmc_value(h, "TCP_PENDING_STALL_CYCLES", out))) {
+    // measured: the attached counter CSV's mean per dispatch of the last kernel (L2 misses, LDS
+    // bank-conflict cycles, L1 cycles stalled on requests pending at L2), DESIGN.md §6.9
+  } else if (k == "read_misses" || k == "hazard_stalls" || k == "ocm_depth" || k == "read_misses_model" ||
+             k == "hazard_stalls_model") {
     const int kn = h->last_kernel;
     const int li = kn == HIPSPMV_KERNEL_VCACHE ? 0 : kn == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1
                  : kn == HIPSPMV_KERNEL_VCACHE_SPLIT4 ? 2 : kn == HIPSPMV_KERNEL_WGATHER ? 3 : -1;
     const bool lds_x = li >= 0 && li < 3;  // x panels staged in LDS (wgather gathers x from L2)
-    if (k == "read_misses")  // x words not held on chip when a product needs them
+    if (k == "read_misses" || k == "read_misses_model")  // x words not held on chip when a product needs them
       *out = lds_x ? (uint64_t)h->vc[li].nblocks * h->cols : (uint64_t)h->nnz;
-    else if (k == "hazard_stalls")  // adds that must wait for the previous add to the same y row
+    else if (k == "hazard_stalls" || k == "hazard_stalls_model")  // adds waiting on the previous add to their y row
       *out = li >= 0 ? h->vc[li].n_cont
            : kn == HIPSPMV_KERNEL_CSR_VECTOR ? 0 : (uint64_t)h->nnz - (h->rows - h->empty_rows);
     else  // on-chip vector words per workgroup: the y block + the two x panels
@@ -1130,6 +1170,21 @@ const char* hipspmv_kernel_name(hipspmv_t* h, int mode) {
     case HIPSPMV_KERNEL_WCSR: return "wcsr";
     default: return "unsupported";
   }
+}
+
+int hipspmv_attach_pmc(hipspmv_t* h, const char* csv_path) {
+  if (!h) return HIPSPMV_ERR_INVALID_ARG;
+  if (!csv_path || !*csv_path) {
+    h->pmc_csv.clear();
+    return HIPSPMV_OK;
+  }
+  std::ifstream probe(csv_path);
+  if (!probe) {
+    set_last_error(std::string("pmc: cannot open ") + csv_path);
+    return HIPSPMV_ERR_INVALID_ARG;
+  }
+  h->pmc_csv = csv_path;
+  return HIPSPMV_OK;
 }
 
 int hipspmv_destroy(hipspmv_t* h) {

@@ -98,6 +98,9 @@ def load_hipspmv() -> C.CDLL:
     lib.hipspmv_kernel_name.argtypes = [vp, C.c_int]
     lib.hipspmv_kernel_name.restype = C.c_char_p
     lib.hipspmv_destroy.argtypes = [vp]
+    lib.hipspmv_pmc_counter.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_double),
+                                        C.POINTER(C.c_uint64)]
+    lib.hipspmv_attach_pmc.argtypes = [vp, C.c_char_p]
     lib.hipspmv_strerror.argtypes = [C.c_int]
     lib.hipspmv_strerror.restype = C.c_char_p
     lib.hipspmv_last_error.argtypes = []
@@ -260,6 +263,11 @@ class Handle:
         _check(self._lib.hipspmv_stat(self._h, key.encode(), C.byref(v)), f"stat({key})")
         return int(v.value)
 
+    def attach_pmc(self, csv_path: str | None) -> None:
+        """A rocprofv3 --pmc counter CSV of this handle's kernel backs read_misses /
+        hazard_stalls / capacity_stalls (include/hipspmv.h); None detaches."""
+        _check(self._lib.hipspmv_attach_pmc(self._h, (csv_path or "").encode()), "attach_pmc")
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._lib.hipspmv_destroy(self._h)
@@ -377,6 +385,15 @@ def gen_rmat_csr(scale: int, edge_factor: int = 16, seed: int = 4):
     return rowptr, colind[:nnz].copy(), vals[:nnz].copy()
 
 
+def pmc_counter(csv_path: str, counter: str, kernel: str | None = None):
+    """(mean per dispatch, dispatches) of `counter` in a rocprofv3 --pmc CSV over the
+    dispatches whose kernel name contains `kernel` (hipspmv_pmc_counter; no GPU needed)."""
+    m, n = C.c_double(), C.c_uint64()
+    _check(load_hipspmv().hipspmv_pmc_counter(csv_path.encode(), kernel.encode() if kernel else None,
+                                              counter.encode(), C.byref(m), C.byref(n)), f"pmc_counter({counter})")
+    return float(m.value), int(n.value)
+
+
 def gen_rmat_row_counts(scale: int, edge_factor: int = 16, seed: int = 4) -> np.ndarray:
     counts = np.empty(1 << scale, dtype=np.uint32)
     load_host().spmvhost_gen_rmat_row_counts(scale, edge_factor, seed, counts)
@@ -387,6 +404,75 @@ def partition_row_counts(counts: np.ndarray, parts: int) -> np.ndarray:
     bounds = np.empty(parts + 1, dtype=np.uint32)
     load_host().spmvhost_partition_row_counts(np.ascontiguousarray(counts, dtype=np.uint32), counts.size, parts, bounds)
     return bounds
+
+
+def rmat_expected_segments(counts: np.ndarray, scale: int, log2w: int = 17, a: float = 0.57, b: float = 0.19,
+                           c: float = 0.19, cap: int = 256) -> np.ndarray:
+    """Expected wcsr segments per row of the R-MAT matrix gen_rmat_rows makes
+    (DESIGN.md §6.11): a row of len edges, whose columns are independent given
+    the row (every level of host/Synthetic.cpp rmatEdge picks the column bit
+    with P(1 | row bit 0) = b / (a + b), P(1 | row bit 1) = d / (c + d)),
+    touches window w (the top scale - log2w column bits) with probability
+    p_w(row) = prod_k P(col bit k | row bit k), so E[windows] =
+    sum_w 1 - (1 - p_w)^len; pieces past `cap` entries in a window add
+    max(0, len * p_w - cap) / cap.  Depends on the row only through its top
+    scale - log2w bits and its length."""
+    d = 1.0 - a - b - c
+    k = max(0, scale - log2w)
+    nw = 1 << k
+    p1 = (b / (a + b), d / (c + d))  # P(col bit = 1 | row bit 0 / 1)
+    counts = np.asarray(counts, dtype=np.int64)
+    rows = counts.size
+    prefix = (np.arange(rows, dtype=np.int64) >> (scale - k)) if k else np.zeros(rows, np.int64)
+    wbits = (np.arange(nw)[:, None] >> (k - 1 - np.arange(k))[None, :]) & 1 if k else np.zeros((1, 0), np.int64)
+    out = np.zeros(rows, dtype=np.float64)
+    for pf in range(1 << k):
+        rbits = (pf >> (k - 1 - np.arange(k))) & 1 if k else np.zeros(0, np.int64)
+        q = np.array([p1[r] for r in rbits]) if k else np.zeros(0)
+        pw = np.prod(np.where(wbits == 1, q[None, :], 1.0 - q[None, :]), axis=1) if k else np.ones(1)
+        sel = np.nonzero(prefix == pf)[0]
+        lens, inv = np.unique(counts[sel], return_inverse=True)
+        L = lens.astype(np.float64)[:, None]
+        e = np.sum(1.0 - np.power(1.0 - pw[None, :], L), axis=1) + \
+            np.sum(np.maximum(0.0, L * pw[None, :] - cap), axis=1) / cap
+        out[sel] = e[inv]
+    return out
+
+
+def partition_row_weights(weights: np.ndarray, parts: int) -> np.ndarray:
+    """Contiguous row partition balancing the sum of per-row weights (a cost
+    model), interior bounds snapped to the nearer multiple of SHARD_ALIGN like
+    host/Synthetic.cpp partitionRowCounts: bounds[0] = 0, bounds[parts] = rows."""
+    w = np.asarray(weights, dtype=np.float64)
+    rows = w.size
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    bounds = np.zeros(parts + 1, dtype=np.int64)
+    for p in range(1, parts):
+        r = int(np.searchsorted(cum, cum[-1] * p / parts, side="left"))
+        r = min(r, rows)
+        lo = r // SHARD_ALIGN * SHARD_ALIGN
+        snapped = min(rows, lo if r - lo <= SHARD_ALIGN // 2 else lo + SHARD_ALIGN)
+        bounds[p] = max(snapped, bounds[p - 1])
+    bounds[parts] = rows
+    return bounds.astype(np.uint32)
+
+
+# wcsr shard cost per row in entry units (DESIGN.md §6.11): each segment and
+# each row costs this many entries' time (fit to the per-shard kernel times of
+# C5's 8-way partition, profiles/r04)
+WCSR_COST_SEGMENT, WCSR_COST_ROW = 0.52, 1.67
+
+
+def c5_partition(scale: int, parts: int, edge_factor: int = 16, seed: int = 4, model: str = "cost"):
+    """C5's row partition: "nnz" balances entries (partition_row_counts);
+    "cost" balances entries + WCSR_COST_SEGMENT * expected segments +
+    WCSR_COST_ROW per row.  Returns (bounds, per-row counts)."""
+    counts = gen_rmat_row_counts(scale, edge_factor, seed)
+    if model == "nnz":
+        return partition_row_counts(counts, parts), counts
+    segs = rmat_expected_segments(counts, scale)
+    w = counts.astype(np.float64) + WCSR_COST_SEGMENT * segs + WCSR_COST_ROW
+    return partition_row_weights(w, parts), counts
 
 
 def gen_rmat_rows(scale: int, row0: int, row1: int, edge_factor: int = 16, seed: int = 4, cap: int | None = None):

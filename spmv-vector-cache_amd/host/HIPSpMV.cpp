@@ -60,6 +60,7 @@ void HIPSpMV::setupRegs() {
     return;
   }
   m_builtVersion = m_A->version();
+  if (m_h && !m_pmc.empty()) hipspmv_attach_pmc(m_h, m_pmc.c_str());
   if (regs()->kernel != HIPSPMV_KERNEL_AUTO)
     m_status = multi() ? hipspmv_multi_set_option(m_multi, "kernel", regs()->kernel)
                        : hipspmv_set_option(m_h, "kernel", regs()->kernel);
@@ -97,6 +98,11 @@ bool HIPSpMV::exec() {
   return m_status == 0;
 }
 
+void HIPSpMV::setPmcCsv(const std::string& path) {
+  m_pmc = path;
+  if (m_h) hipspmv_attach_pmc(m_h, path.c_str());
+}
+
 uint64_t HIPSpMV::statU64(const std::string& key) {
   uint64_t v = 0;
   if (m_multi) {
@@ -122,6 +128,8 @@ std::vector<std::string> HIPSpMV::statKeys() {
                         "sColdMiss", "totalCycles", "activeCycles", "readMisses", "ocmDepth", "issueWindow",
                         "hazardStalls", "capacityStalls", "cms", "noValidButReady", "noReadyButValid"})
     keys.push_back(k);
+  // the layout-derived values readMisses / hazardStalls report without a counter CSV
+  for (const char* k : {"readMissesModel", "hazardStallsModel"}) keys.push_back(k);
   return keys;
 }
 
@@ -165,8 +173,20 @@ unsigned int HIPSpMV::statInt(std::string name) {
   // ocmDepth = on-chip vector-cache words per workgroup (y block + x panels)
   if (name == "totalCycles") return (unsigned int)statU64("total_cycles");
   if (name == "activeCycles") return (unsigned int)statU64("active_cycles");
+  // with a counter CSV and no device handle (the run failed, or the CSV comes from another host),
+  // the counters still reach the row: the CSV's dominant hipspmv kernel
+  if (!m_pmc.empty() && !m_h && !m_multi &&
+      (name == "readMisses" || name == "hazardStalls" || name == "capacityStalls")) {
+    const char* c = name == "readMisses" ? "TCC_MISS" : name == "hazardStalls" ? "SQ_LDS_BANK_CONFLICT"
+                                                                             : "TCP_PENDING_STALL_CYCLES";
+    double v = 0;
+    uint64_t n = 0;
+    if (hipspmv_pmc_counter(m_pmc.c_str(), nullptr, c, &v, &n) == HIPSPMV_OK && n) return (unsigned int)(v + 0.5);
+  }
   if (name == "readMisses") return (unsigned int)statU64("read_misses");
   if (name == "hazardStalls") return (unsigned int)statU64("hazard_stalls");
+  if (name == "readMissesModel") return (unsigned int)statU64("read_misses_model");
+  if (name == "hazardStallsModel") return (unsigned int)statU64("hazard_stalls_model");
   if (name == "ocmDepth") return (unsigned int)statU64("ocm_depth");
   // the cache-FSM state counts (stateNames, HardwareSpMVNewCache.cpp:6-7) and the
   // stream-monitor stalls, measured by a profiled launch (register `profile`):

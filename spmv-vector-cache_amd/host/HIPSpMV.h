@@ -9,6 +9,7 @@
 #define SPMV_AMD_HIPSPMV_H_
 
 #include <cstdint>
+#include <string>
 
 #include "HardwareSpMV.h"
 #include "hipspmv.h"
@@ -55,6 +56,13 @@ class HIPSpMV : public HardwareSpMV {
   virtual std::vector<std::string> statKeys();
   uint64_t statU64(const std::string& key);  // full-width libhipspmv statistic
   int status() const { return m_status; }
+  // A rocprofv3 --pmc counter CSV of this backend's kernel: readMisses,
+  // hazardStalls and capacityStalls then report the measured counters
+  // (TCC_MISS, SQ_LDS_BANK_CONFLICT, TCP_PENDING_STALL_CYCLES per launch), as
+  // the reference reads its counters from the accelerator
+  // (HardwareSpMVNewCache.cpp:161-173); readMissesModel / hazardStallsModel
+  // keep the layout values.  "" detaches.
+  void setPmcCsv(const std::string& path);
 
  protected:
   const HIPSpMVRegisterFile* regs() const { return reinterpret_cast<const HIPSpMVRegisterFile*>(
@@ -75,6 +83,7 @@ class HIPSpMV : public HardwareSpMV {
   uint64_t m_prepVersion = ~0ull;
   uint64_t m_builtVersion = ~0ull;
   int m_status = 0;
+  std::string m_pmc;
 };
 
 #endif

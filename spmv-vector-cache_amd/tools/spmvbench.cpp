@@ -15,6 +15,8 @@
 //             [--cms 0|1] [--confs hip,sw] [--profile 0|1] matrix...
 // --profile 1: vcache-family launches record the NewCache state statistics
 // (sActive ... noReadyButValid), measured in-kernel.
+// --pmc FILE: a rocprofv3 --pmc counter CSV of the backend's kernel; readMisses,
+// hazardStalls and capacityStalls report its counters (HIPSpMV::setPmcCsv).
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
@@ -92,6 +94,7 @@ std::vector<std::string> readList() {
 int main(int argc, char** argv) {
   std::string dir = "tests/golden/matrices";
   int device = 0, mode = HIPSPMV_MODE_ORDERED, kernel = HIPSPMV_KERNEL_AUTO, reps = 1, profile = 0;
+  std::string pmc;
   bool cms = false, haveCms = false;
   std::vector<std::string> confs, ms;
   for (int i = 1; i < argc; ++i) {
@@ -106,9 +109,12 @@ int main(int argc, char** argv) {
                : k == "vcache_split" ? HIPSPMV_KERNEL_VCACHE_SPLIT
                : k == "csr_lane" ? HIPSPMV_KERNEL_CSR_LANE
                : k == "csr_vector" ? HIPSPMV_KERNEL_CSR_VECTOR
-               : k == "sell" ? HIPSPMV_KERNEL_SELL : HIPSPMV_KERNEL_AUTO;
+               : k == "sell" ? HIPSPMV_KERNEL_SELL
+               : k == "vcache_split4" ? HIPSPMV_KERNEL_VCACHE_SPLIT4
+               : k == "wcsr" ? HIPSPMV_KERNEL_WCSR : HIPSPMV_KERNEL_AUTO;
     } else if (a == "--reps") reps = std::atoi(next().c_str());
     else if (a == "--profile") profile = std::atoi(next().c_str());
+    else if (a == "--pmc") pmc = next();
     else if (a == "--cms") { cms = std::atoi(next().c_str()) != 0; haveCms = true; }
     else if (a == "--confs") {
       std::stringstream ss(next());
@@ -169,6 +175,8 @@ int main(int argc, char** argv) {
       if (cms) A->markRowStarts();
       HardwareSpMV* spmv = HWSpMVFactory::make(accBase, resBase, A, x.data(), y.data());
       if (!spmv) return 2;
+      if (!pmc.empty())
+        if (auto* hip = dynamic_cast<HIPSpMV*>(spmv)) hip->setPmcCsv(pmc);
       if (!keysBuilt) {
         keys = spmv->statKeys();
         keys.push_back("accType");

@@ -49,6 +49,8 @@ class FakeHandle:
     def stat(self, key):
         if key == "setup_ns":
             return 1000
+        if key == "wcsr_segments":
+            return 0
         assert key == "alg_bytes"
         return 12 * self.nnz + 4 * (self.rows + 1) + 8 * self.cols + 8 * self.rows
 
@@ -112,7 +114,7 @@ def test_bench_json_contract_single(monkeypatch):
     sys.path.insert(0, REPO)
     bench = _patch(monkeypatch)
     out = _run(bench, ["--steps", "2", "--warmup", "1", "--log2-rows", "12", "--log2-cols", "12",
-                       "--cpu-seconds", "0.05", "--strong-scale", "12"])
+                       "--cpu-seconds", "0.05", "--strong-scale", "12", "--c5-scale", "14", "--c5-steps", "2"])
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
                 "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert key in out, key
@@ -142,6 +144,12 @@ def test_bench_json_contract_single(monkeypatch):
     assert st["scaling"] == "strong" and st["nnz_total"] == 32 << 12 and st["rows_per_rank"] == 1 << 12
     assert st["rank_parity"][0].startswith("within FAST bound") and len(st["rank_kernel_us"]) == 1
     assert out["gen_s"] >= 0 and out["setup_s"] >= 0 and out["setup_ns_lib"] == 1000
+    # the C5 block: 8 cost-balanced shards of R-MAT scale 12, each timed and checked against the oracle
+    c5 = out["c5_shards"]
+    assert len(c5["shards"]) == 8 and c5["nnz_total"] == sum(s["nnz"] for s in c5["shards"])
+    assert c5["shards"][0]["rows"][0] == 0 and c5["shards"][-1]["rows"][1] == 1 << 14
+    assert all(s["parity"].startswith("within FAST bound") for s in c5["shards"] if s["kernel"]), c5
+    assert c5["max_over_min"] >= 1.0 and c5["value"] > 0
 
 
 FAKE_ROCPROF = """#!/usr/bin/env python3

@@ -48,3 +48,55 @@ def test_kernel_stats_from_pmc_matches_committed(tmp_path):
     rows = {r["Name"]: r for r in csv.DictReader(open(out))}
     k = next(r for n, r in rows.items() if "k_vcache<double, 2," in n)
     assert abs(float(k["AverageNs"]) / 1e3 - 143.5) / 143.5 < 0.02
+
+
+R04 = os.path.join(os.path.dirname(hs.PKG_DIR), "profiles", "r04", "s1")
+
+
+def _pmc_mean(path, kernel_sub, counter):
+    import csv
+    vals = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel_sub in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                vals[row["Dispatch_Id"]] = float(row["Counter_Value"])
+    return sum(vals.values()) / len(vals), len(vals)
+
+
+def test_pmc_counter_reads_round4_csv():
+    # hipspmv_pmc_counter (libhipspmv, no device) on the committed round-4 pass of the
+    # product kernel: the mean per dispatch of each counter equals a plain CSV read
+    path = os.path.join(R04, "pmc_c3_split_pass3.csv")
+    for counter in ("TCC_MISS", "TCC_HIT", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_LDS"):
+        want, n = _pmc_mean(path, "k_vcache<double, 3,", counter)
+        got, gn = hs.pmc_counter(path, counter, "k_vcache<double, 3,")
+        assert gn == n == 10 and got == pytest.approx(want, rel=1e-12), counter
+    # no kernel filter: the hipspmv kernel with the most dispatches; the summary CSV form
+    assert hs.pmc_counter(path, "TCC_MISS")[0] == pytest.approx(_pmc_mean(path, "k_vcache", "TCC_MISS")[0])
+    summ = os.path.join(R04, "pmc_c3_split_summary.csv")
+    assert hs.pmc_counter(summ, "TCC_MISS")[0] == pytest.approx(_pmc_mean(path, "k_vcache", "TCC_MISS")[0],
+                                                                rel=1e-5)
+    with pytest.raises(hs.HipSpMVError):
+        hs.pmc_counter(path, "NO_SUCH_COUNTER")
+
+
+def test_spmvbench_csv_row_carries_pmc_counters():
+    # spmvbench --pmc: the counters reach the plugin's CSV row (readMisses <- TCC_MISS,
+    # hazardStalls <- SQ_LDS_BANK_CONFLICT; the layout values under *Model), as the
+    # reference reads its counters from the accelerator (HardwareSpMVNewCache.cpp:161-173).
+    # Without a GPU the backend's run fails, and the row still carries the CSV's counters.
+    import subprocess
+    if hs.device_count() > 0:
+        pytest.skip("with a device the row reports the counters of the kernel that ran (a -m gpu concern)")
+    path = os.path.join(R04, "pmc_c3_split_pass3.csv")
+    repo = os.path.dirname(hs.PKG_DIR)
+    out = subprocess.run([os.path.join(hs.LIB_DIR, "spmvbench"), "--dir", os.path.join(repo, "tests", "golden",
+                          "matrices"), "--confs", "hip", "--cms", "0", "--pmc", path, "circuit204"],
+                         capture_output=True, text=True, timeout=120).stdout.splitlines()
+    head = next(l for l in out if l.startswith("nnz,") or "readMisses" in l)
+    keys = head.rstrip(",").split(",")
+    row = [l for l in out if l.rstrip(",").endswith("circuit204")][-1].rstrip(",").split(",")
+    rec = dict(zip(keys, row))
+    assert "readMissesModel" in rec and "hazardStallsModel" in rec
+    assert int(rec["readMisses"]) == round(_pmc_mean(path, "k_vcache", "TCC_MISS")[0])
+    assert int(rec["hazardStalls"]) == round(_pmc_mean(path, "k_vcache", "SQ_LDS_BANK_CONFLICT")[0])
