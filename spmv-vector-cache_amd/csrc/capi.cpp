@@ -204,11 +204,15 @@ static void free_vc(hipspmv_t* h, int k) {
 
 // Build vcache-family layout k (geometry g) from `a` and upload it; on
 // failure nothing of it stays allocated.
-static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g) {
+static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uint32_t lanes = 0) {
   auto& v = h->vc[k];
   const uint64_t bytes0 = h->device_bytes;
   VcacheLayout L;
-  build_vcache(a, g, L);
+  if (lanes) {  // k_vquad's placement (build_vcache_lanes); false: not placeable, not eligible
+    if (!build_vcache_lanes(a, g, lanes, L)) return HIPSPMV_ERR_UNSUPPORTED;
+  } else {
+    build_vcache(a, g, L);
+  }
   v.split = g.split;
   v.rows_per_block = L.rows_per_block;
   v.nblocks = L.nblocks;
@@ -229,7 +233,8 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g) {
   if ((st = dev_upload(&v.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return fail(st);
   if (v.split > 1) {
     // [0, nblocks): arrival tickets, [nblocks, 2 nblocks): published partials
-    // (the ticket-first combine of k_vcache); both self-reset after each launch;
+    // (the ticket-first combine of k_vcache; k_vquad: 4 of each per block, per
+    // quarter of its rows, within the same words); both self-reset after each launch;
     // then kVcProfWords per unit for the profile stamps (option "profile")
     std::vector<uint32_t> zeros(2ull * v.nblocks + (uint64_t)kVcProfWords * v.nblocks * v.split, 0u);
     if ((st = dev_upload(&v.d_tickets, zeros.data(), zeros.size(), h->device_bytes))) return fail(st);
@@ -524,9 +529,9 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   if (vcache_eligible(a, kVcSplit) && (st = upload_vc(h, 1, a, kVcSplit))) return st;
   // the four-part layout (k_vquad) wherever eligible and every segment fits
   // the kernel's register window (k_vquad has no slow path for longer ones)
-  if (vcache_eligible(a, kVcSplit4)) {
-    if ((st = upload_vc(h, 2, a, kVcSplit4))) return st;
-    if (h->vc[2].max_seg > vquad_max_window(0)) free_vc(h, 2);
+  if (vcache_eligible(a, kVcQuad)) {
+    st = upload_vc(h, 2, a, kVcQuad, kVqLanes);
+    if (st && st != HIPSPMV_ERR_UNSUPPORTED) return st;
   }
   h->wg_eligible = vcache_eligible(a, kWgWindow);
   if (h->wg_eligible) h->wg_max_run = vcache_max_run(a, (uint32_t)kWgWindow.panel);
@@ -703,7 +708,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
       kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
     const int k = kernel == HIPSPMV_KERNEL_VCACHE ? 0 : kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1 : 2;
     const auto& v = h->vc[k];
-    const VcGeom geoms[3] = {kVcOrdered, kVcSplit, kVcSplit4};
+    const VcGeom geoms[3] = {kVcOrdered, kVcSplit, kVcQuad};
     VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    v.d_partial,
                  v.d_tickets, h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
                  v.npad,      h->nnz - 1, v.split,   beta, h->vcache_dma, (uint32_t)geoms[k].panel,
@@ -781,7 +786,7 @@ static int read_status(hipspmv_t* h, uint32_t* out) {
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(out, h->d_status, 4, hipMemcpyDeviceToHost));
   if (*out) {
-    if (h->vc[2].d_tickets) HIP_TRY(hipMemset(h->vc[2].d_tickets, 0, 8ull * h->vc[2].nblocks));
+    if (h->vc[2].d_tickets) HIP_TRY(hipMemset(h->vc[2].d_tickets, 0, 4ull * 2 * 4 * h->vc[2].nblocks));  // k_vquad: per (block, quarter)
     HIP_TRY(hipMemset(h->d_status, 0, 4));
   }
   return HIPSPMV_OK;
@@ -912,7 +917,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "vcache_map") {
     h->vcache_map = value ? 1 : 0;
   } else if (k == "vquad_variant") {  // k_vquad configuration (csrc/vquad.hip)
-    if (value < 0 || value > 16) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < 0 || value > 20) return HIPSPMV_ERR_INVALID_ARG;
     if (h->vc[2].ok && h->vc[2].max_seg > vquad_max_window((int)value)) return HIPSPMV_ERR_UNSUPPORTED;
     h->vquad_variant = (int)value;
   } else if (k == "wgather_chunk") {  // row blocks per k_wgather launch (0: all in one launch)

@@ -56,6 +56,13 @@ constexpr uint32_t kVcMore = 1u << 31;  // next entry continues this entry's row
 // per entry (R-MAT s20 with hub rows: 23.6 ms in k_vcache split against
 // 0.25 ms in csr_vector, round-2 sweep).
 constexpr uint32_t kVcRunMax = 16;
+// build_vcache_lanes / k_vquad: the entry's run continues in the same lane's
+// next slot (position + CT), not in the next lane
+constexpr uint32_t kVqLMore = 1u << 28;
+// the k_vquad geometry: 16384 rows, 1984-column panels, 4 parts, 12 column
+// bits (the code holds row_local << 12 and the flags in bits 28-31)
+constexpr VcGeom kVcQuad{16384, 1984, 4, 12};
+constexpr uint32_t kVqLanes = 13 * 64;  // k_vquad's compute lanes (13 of 16 waves): the layout's CT
 
 // ---- wcsr: csr_vector over the column-windowed segment matrix
 // Every row is cut at column windows of 2^kWcLog2Window columns (1 MiB of
@@ -199,6 +206,8 @@ bool vcache_eligible(const HostCSR& a, const VcGeom& g);
 void vcache_geometry(uint32_t rows, uint32_t cols, const VcGeom& g, VcacheLayout& out);
 uint32_t vcache_max_run(const HostCSR& a, uint32_t panel);
 void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out);
+// k_vquad's placement of the same entries for CT compute lanes (plan.cpp)
+bool build_vcache_lanes(const HostCSR& a, const VcGeom& g, uint32_t CT, VcacheLayout& out);
 void build_sell(const HostCSR& a, SellLayout& out);
 // The column-windowed segment matrix of `a` (columns sorted within each row:
 // vcache_eligible's condition).  Throws std::bad_alloc on host OOM.

@@ -187,6 +187,101 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
   out.max_run = vcache_max_run(a, P);
 }
 
+// The k_vquad form of the vcache layout: the same blocks,
+// panels and segment offsets, entries of a segment placed for a kernel whose
+// step gives lane ct of the CT compute lanes the positions ct and CT + ct
+// (two entries per lane, EPT = 2), code = col_local | row_local << 12 | flags:
+//  * a row with two entries in the segment takes both slots of one lane
+//    (first: kVqLMore, second: kVcCont) while lanes with two slots last, so the
+//    lane adds its pair without any cross-lane step;
+//  * longer runs (and pairs past that) take consecutive positions inside one
+//    slot row and one 64-lane wave (kVcMore / kVcCont as in build_vcache): the
+//    kernel finishes them with wave shuffles, never across a wave;
+//  * single entries fill the rest.
+// Rows are independent inside a segment, so the order of rows is free (FAST,
+// u64); every row's entries stay in column order.  Returns false when a
+// segment exceeds 2 * CT entries or a run cannot be placed that way.
+bool build_vcache_lanes(const HostCSR& a, const VcGeom& g, uint32_t CT, VcacheLayout& out) {
+  if (g.colbits != 12 || CT % 64 || CT == 0) return false;
+  build_vcache(a, g, out);  // geometry, segment offsets and (row, col) order
+  const uint32_t P = (uint32_t)g.panel, S = (uint32_t)g.split, npad = out.npad;
+  std::vector<uint32_t> code(out.code.size());
+  std::vector<uint64_t> vals(out.vals.size());
+  std::vector<int64_t> pos;  // position of each entry of the segment (-1 unplaced)
+  std::vector<uint8_t> used;
+  for (uint32_t b = 0; b < out.nblocks; ++b)
+    for (uint32_t h = 0; h < S; ++h) {
+      const uint32_t* sg = &out.seg[((size_t)b * S + h) * (npad + 1)];
+      for (uint32_t i = 0; i < npad; ++i) {
+        const uint32_t s0 = sg[i], s1 = sg[i + 1], n = s1 - s0;
+        if (!n) continue;
+        if (n > 2 * CT) return false;
+        // runs of the segment: [start, len) in storage (row, col) order
+        std::vector<std::pair<uint32_t, uint32_t>> runs;
+        for (uint32_t e = s0; e < s1;) {
+          uint32_t f = e + 1;
+          while (f < s1 && (out.code[f] & kVcCont)) ++f;
+          runs.emplace_back(e, f - e);
+          e = f;
+        }
+        const uint32_t m = n > CT ? n - CT : 0;  // lanes with a second slot
+        pos.assign(n, -1);
+        used.assign(n, 0);
+        auto put = [&](uint32_t e, uint32_t p, uint32_t flags) {
+          pos[e - s0] = p;
+          used[p] = 1;
+          code[s0 + p] = (out.code[e] & ~(kVcCont | kVcMore)) | flags;
+          vals[s0 + p] = out.vals[e];
+        };
+        // 1. pairs lane-local on lanes [0, m)
+        uint32_t lane = 0;
+        for (auto& r : runs)
+          if (r.second == 2 && lane < m) {
+            put(r.first, lane, kVqLMore);
+            put(r.first + 1, CT + lane, kVcCont);
+            ++lane;
+            r.second = 0;  // placed
+          }
+        // 2. other multi-entry runs: consecutive positions inside one slot row
+        // and one wave, from the first free position on
+        auto fits = [&](uint32_t p, uint32_t len) {
+          if (p + len > n) return false;
+          const uint32_t j = p / CT, c = p % CT;
+          if ((p + len - 1) / CT != j || c / 64 != (c + len - 1) / 64) return false;
+          for (uint32_t k = 0; k < len; ++k)
+            if (used[p + k]) return false;
+          return true;
+        };
+        // first fit, longest runs first (a run keeps its own entries in order)
+        std::vector<size_t> multi;
+        for (size_t i = 0; i < runs.size(); ++i)
+          if (runs[i].second >= 2) multi.push_back(i);
+        std::stable_sort(multi.begin(), multi.end(),
+                         [&](size_t u, size_t w) { return runs[u].second > runs[w].second; });
+        for (size_t i : multi) {
+          auto& r = runs[i];
+          uint32_t p = 0;
+          while (p < n && !fits(p, r.second)) ++p;
+          if (p >= n) return false;
+          for (uint32_t k = 0; k < r.second; ++k)
+            put(r.first + k, p + k, (k ? kVcCont : 0u) | (k + 1 < r.second ? kVcMore : 0u));
+          r.second = 0;
+        }
+        // 3. single entries in order into the free positions
+        uint32_t p = 0;
+        for (auto& r : runs) {
+          if (r.second != 1) continue;
+          while (used[p]) ++p;
+          put(r.first, p, 0u);
+        }
+      }
+    }
+  out.code.swap(code);
+  out.vals.swap(vals);
+  (void)P;
+  return true;
+}
+
 // SELL-C-sigma layout for k_sell (hipspmv_internal.h): within each window of
 // kSellSigma rows the rows of at most kSellHub entries are ordered by length,
 // longest first (ties by row id), and cut into slices of kSellRows; each

@@ -16,30 +16,33 @@
 // an x panel has DX steps to arrive.
 //
 // Work unit (b, h): rows [b*R, b*R + R), panels [vc_part_first(h), ...) of the
-// kVcSplit4 layout (csrc/plan.cpp build_vcache: per (block, panel) segment,
-// entries in (row, column) order, code = col_local | row_local << 16 | CONT |
-// MORE).  The parts of a block run in dispatch slots i, i+8, i+16, i+24 (one
-// XCD under round-robin placement: the combine's hand-off stays in one L2;
-// speed only).
+// kVcQuad layout (csrc/plan.cpp build_vcache per (block, panel) segment,
+// re-placed by build_vcache_lanes: compute lane ct holds segment positions ct
+// and CT + ct; code = col_local | row_local << 12 | LMORE | CONT | MORE).  The
+// parts of a block run in dispatch slots i, i+8, i+16, i+24 (one XCD under
+// round-robin placement: the combine's hand-off stays in one L2; speed only).
 //
 // Roles: waves [0, WL) stage x panels (LDS slot s & 1 holds panel s); waves
 // [WL, 16) stream the unit's entries DE steps ahead (asm loads, exact waits)
-// and apply them: every valid lane forms its rounded product from the LDS
-// panel, a run head (first entry of its row in the segment) adds the
-// products of its run's other entries from the next lanes (DPP-free
-// __shfl_down; a run that crosses into the next wave finishes with scalar
-// loads) and updates its y row in LDS.  No two lanes own one row in a step,
-// and the step barrier orders the steps.  One s_barrier per panel.
+// and apply them: every valid lane forms its rounded products from the LDS
+// panel, a lane whose pair is one row (LMORE) adds it in registers, a rare
+// longer run head (MORE) adds its run's next lanes by __shfl_down (the layout
+// keeps such runs inside a wave), and owners update their y rows in LDS.  No
+// two lanes own one row in a step, and the step barrier orders the steps.
+// One s_barrier per panel.
 //
-// Combine (fixed order y = p0 + p1 + p2 + p3, deterministic): ticket first --
-// the workgroups that are not last publish their partial with write-through
-// (sc1) 16-byte stores, drain, and count it; the last arriver polls that count
-// (sc1), reads the three partials (sc1) and writes y (MI355X_MICROARCH.md,
-// Valid forms, table row 1).  The publishers took their tickets before the
-// last arriver did, so they run and publish: the wait is bounded by their
-// work.  A wait that still exceeds ~0.3 s of polls sets bit 0 of *status and
-// leaves the counters alone (the host reports the launch failed and resets
-// the scratch) instead of reading partials that may be unpublished.
+// Combine (fixed order y = p0 + p1 + p2 + p3, deterministic): unit h owns
+// quarter h of the block's rows.  It publishes its partials of the other three
+// quarters with write-through (sc1) 16-byte stores, drains, counts each one
+// (agent-scope add on the quarter's word), then waits for the three
+// publishers of its own quarter, reads their partials (sc1) and writes those
+// y rows (MI355X_MICROARCH.md, Valid forms, table row 1).  The four parts run
+// at once (one wave of 256 units), so each CU moves 96 KiB out and 96 KiB in;
+// the single-combiner form (the last arriver reads 384 KiB) cost 11.5 us of
+// 118 at C3.  Deadlock freedom does not rest on co-residency: the owner's
+// wait is bounded, and an owner that gives up publishes its own part and
+// counts it too -- the add that finds the count at 3 (all four in) belongs to
+// the unit that combines the quarter, which then needs to wait for nothing.
 #include <hip/hip_runtime.h>
 
 #include "device_common.h"
@@ -50,7 +53,7 @@ namespace hipspmv {
 
 namespace {
 
-constexpr int VR = kVcSplit4.rows, VP = kVcSplit4.panel, SPLIT = 4;
+constexpr int VR = kVcQuad.rows, VP = kVcQuad.panel, SPLIT = 4;
 
 // an asm-load ring value may be read (or its register reused) only after the
 // wait that retired its load: the wait is followed by an empty asm that takes
@@ -75,6 +78,30 @@ __device__ __forceinline__ T ald_64_nt(const T* p) {
   return __builtin_bit_cast(T, r);
 }
 
+// entry loads through a buffer descriptor of the unit's entries: a lane past
+// its step's segment gets an out-of-range offset and the load returns 0
+// without a memory request, while every lane still issues the instruction
+// (the ring's vmcnt counts stay exact).  Clamped loads instead re-read the
+// next segment's entries: 1.68x the entry requests at four parts
+// (the round-4 skeletons: entries alone 80 us barrier-stepped vs 59 us
+// for a plain stream).
+typedef unsigned int u32x4d __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4d buf_desc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  return u32x4d{(uint32_t)a, (uint32_t)(a >> 32), bytes, 0x00020000u};
+}
+__device__ __forceinline__ uint32_t bld_u32_nt(u32x4d d, uint32_t off) {
+  uint32_t r;
+  asm volatile("buffer_load_dword %0, %1, %2, 0 offen nt" : "=v"(r) : "v"(off), "s"(d) : "memory");
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ T bld_64_nt(u32x4d d, uint32_t off) {
+  uint64_t r;
+  asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt" : "=v"(r) : "v"(off), "s"(d) : "memory");
+  return __builtin_bit_cast(T, r);
+}
+
 constexpr uint32_t gcd_u(uint32_t a, uint32_t b) { return b ? gcd_u(b, a % b) : a; }
 constexpr uint32_t lcm_u(uint32_t a, uint32_t b) { return a / gcd_u(a, b) * b; }
 
@@ -83,8 +110,9 @@ constexpr uint32_t lcm_u(uint32_t a, uint32_t b) { return a / gcd_u(a, b) * b; }
 // AB: ablation mask (timing probes only; results wrong unless 0): 1 no apply,
 // 2 no x stores into LDS, 4 no combine (each part writes its own rows), 8 no
 // step barrier, 16 x loads by LDS-DMA into the slots (timing only: DX > 1
-// panels in flight overwrite each other), 32 no x loads, 64 no entry loads
-template <typename T, int WL, int DX, int DE, int EPT, bool NOFB = false, int AB = 0>
+// panels in flight overwrite each other), 32 no x loads, 64 no entry loads;
+// 128 (results exact: the test of the combine's fallback) owners never wait
+template <typename T, int WL, int DX, int DE, int EPT, int AB = 0>
 __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict__ seg,
                                                        const uint32_t* __restrict__ ecode,
                                                        const T* __restrict__ evals, const T* __restrict__ x,
@@ -201,82 +229,64 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
   } else {
     // ---- entries: EPT per lane per step at clamped indices, DE steps in flight
     const int ct = t - LT;
-    const uint32_t lw = t & 63;
     uint32_t EC[DE][EPT];
     T EV[DE][EPT];
-    auto issue = [&](uint32_t s, uint32_t* c, T* v) {
+    // the unit's entries [segl[0], segl[npu]) through two descriptors
+    const uint32_t e0 = __builtin_amdgcn_readfirstlane(segl[0]),
+                   ne = __builtin_amdgcn_readfirstlane(segl[npu]) - e0;  // wave-uniform: SGPR descriptors
+    const u32x4d dcode = buf_desc(ecode + e0, 4 * ne), dvals = buf_desc(evals + e0, 8 * ne);
+    uint32_t SB[DE], SE[DE];  // each ring slot's segment bounds (unit-relative), read once from LDS
+    auto issue = [&](uint32_t s, uint32_t* c, T* v, uint32_t& sb, uint32_t& se) {
+      const uint32_t beg = segl[min(s, npad)] - e0, end = segl[min(s + 1, npad)] - e0;
+      sb = beg;
+      se = end;
       if (AB & 64) return;
-      const uint32_t beg = segl[min(s, npad)];
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        const uint32_t q = min(beg + ct + j * CT, last);
-        c[j] = ald_u32_nt(ecode + q);
-        v[j] = ald_64_nt(evals + q);
-      }
-    };
-    auto sload32 = [](const uint32_t* p) {
-      uint32_t r;
-      asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
-      return r;
-    };
-    auto sload64 = [](const T* p) {
-      uint64_t r;
-      asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
-      return __builtin_bit_cast(T, r);
-    };
-    // step s: products from LDS panel s & 1; a run head sums its run across
-    // the following lanes (the layout keeps a row's entries of one segment
-    // adjacent) and updates its y row; requires max_seg <= EPT * CT
-    auto apply = [&](uint32_t s, const uint32_t* c, const T* v) {
-      const T* xs = xb[s & 1];
-      const uint32_t beg = segl[s], end = segl[s + 1];
 #pragma unroll
       for (int j = 0; j < EPT; ++j) {
         const uint32_t q = beg + ct + j * CT;
-        const uint32_t code = c[j];
+        const bool in = q < end;
+        c[j] = bld_u32_nt(dcode, in ? 4 * q : 0x80000000u);
+        v[j] = bld_64_nt<T>(dvals, in ? 8 * q : 0x80000000u);
+      }
+    };
+    // step s over the build_vcache_lanes placement (lane ct holds positions ct
+    // and CT + ct of the segment [beg, end)): both products from LDS panel
+    // s & 1; a lane whose first entry carries kVqLMore adds its second entry
+    // (the same row); a run head with kVcMore (runs longer than two, rare)
+    // sums the next lanes of its wave by shuffles; every owner updates its y
+    // row once.  No two owners share a row in a step.
+    static_assert(EPT == 2, "build_vcache_lanes places two entries per lane");
+    auto apply = [&](uint32_t s, uint32_t beg, uint32_t end, const uint32_t* c, const T* v) {
+      const T* xs = xb[s & 1];
+      T p[2], acc[2];
+      bool own[2];
+      uint32_t row[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t q = beg + ct + j * CT;
         const bool valid = q < end;
-        const T p = valid ? v[j] * xs[code & 0xFFFF] : T(0);  // rounded product (contract off)
-        const bool own = valid && !(code & kVcCont);
-        const uint32_t row = (code >> 16) & 0x3FFF;
-        T acc = own ? ylds[row] + p : T(0);
-        bool more = own && (code & kVcMore);
-        bool fb = false;
-        uint32_t fbi = 0;
+        p[j] = valid ? v[j] * xs[c[j] & 0xFFF] : T(0);  // rounded product (contract off)
+        own[j] = valid && !(c[j] & kVcCont);
+        row[j] = (c[j] >> 12) & 0x3FFF;
+        acc[j] = own[j] ? ylds[row[j]] + p[j] : T(0);
+      }
+      if (own[0] && (c[0] & kVqLMore)) acc[0] = acc[0] + p[1];  // the lane's pair
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bool more = own[j] && (c[j] & kVcMore);
         for (uint32_t k = 1; __builtin_amdgcn_ballot_w64(more) != 0; ++k) {  // wave-uniform trip count
-          const T pk = __shfl_down(p, k);
-          const uint32_t ck = __shfl_down(code, k);
-          if (more) {
-            if (lw + k < 64) {
-              acc = acc + pk;
-              more = (ck & kVcMore) != 0;
-            } else {  // the run continues in the next wave's lanes
-              fb = true;
-              fbi = q + k;
-              more = false;
-            }
+          const T pk = __shfl_down(p[j], k);
+          const uint32_t ck = __shfl_down(c[j], k);
+          if (more) {  // the layout keeps such a run inside its wave
+            acc[j] = acc[j] + pk;
+            more = (ck & kVcMore) != 0;
           }
         }
-        for (uint64_t m = NOFB ? 0 : __builtin_amdgcn_ballot_w64(fb); m; m &= m - 1) {  // rare
-          const uint32_t l = (uint32_t)__builtin_ctzll(m);
-          uint32_t i = __builtin_amdgcn_readlane(fbi, l);
-          const uint64_t ab = __builtin_bit_cast(uint64_t, acc);
-          T a = __builtin_bit_cast(T, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)ab, l) |
-                                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(ab >> 32), l)
-                                           << 32));
-          uint32_t cd;
-          do {
-            cd = sload32(ecode + i);
-            const T pv = sload64(evals + i) * xs[cd & 0xFFFF];
-            a = a + pv;
-            ++i;
-          } while (cd & kVcMore);
-          if (lw == l) acc = a;
-        }
-        if (own) ylds[row] = acc;
+        if (own[j]) ylds[row[j]] = acc[j];
       }
     };
 #pragma unroll
-    for (int d = 0; d < DE; ++d) issue(d, EC[d], EV[d]);
+    for (int d = 0; d < DE; ++d) issue(d, EC[d], EV[d], SB[d], SE[d]);
     barrier();
     for (uint32_t base = 0; base < nsteps; base += DE) {
 #pragma unroll
@@ -291,8 +301,8 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
         // apply before the slot's reload: the old values die first, so the
         // reload reuses their registers and the loop carries no copy of a
         // register whose load is in flight (vmcnt_check: a copy there reads it)
-        if (!(AB & 1) && s < npu) apply(s, EC[i], EV[i]);
-        issue(s + DE, EC[i], EV[i]);
+        if (!(AB & 1) && s < npu) apply(s, SB[i], SE[i], EC[i], EV[i]);
+        issue(s + DE, EC[i], EV[i], SB[i], SE[i]);
         barrier();
       }
     }
@@ -310,110 +320,136 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
     for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
     return;
   }
-  // ---- combine: ticket first (header comment)
+  // ---- combine: unit h owns quarter h of the block's rows (header comment)
   constexpr uint32_t VRP = (VR + 1) & ~1u;
-  constexpr int NP = (VRP / 2 + VT - 1) / VT;  // row pairs per lane
-  static_assert(NP % 4 == 0, "whole chunks");
-  uint32_t* const published = tickets + nblocks;
-  if (t == 0) segl[0] = __hip_atomic_fetch_add(tickets + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
+  constexpr uint32_t QP = VRP / 2 / SPLIT;  // row pairs per quarter
+  constexpr int NQ = QP / VT;               // row pairs per lane per quarter
+  static_assert(QP % VT == 0 && NQ >= 1, "whole quarters");
+  uint32_t* const published = tickets + (size_t)SPLIT * b;  // [q]: partials of quarter q published
   const u64x2* const yl2 = reinterpret_cast<const u64x2*>(ylds);
   const uint32_t npairs = (nr + 1) / 2;
-  if (segl[0] != (uint32_t)SPLIT - 1) {
-    const __amdgpu_buffer_rsrc_t mine = buf_rsrc(partial + ((size_t)h * nblocks + b) * VRP, 8 * VRP);
+  const __amdgpu_buffer_rsrc_t mine = buf_rsrc(partial + ((size_t)h * nblocks + b) * VRP, 8 * VRP);
+  auto publish = [&](uint32_t q) {
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const uint32_t p = t + j * VT;
+    for (int j = 0; j < NQ; ++j) {
+      const uint32_t p = q * QP + t + j * VT;
       if (p < npairs) st_128_sc1(mine, 16 * p, yl2[p]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) __hip_atomic_fetch_add(published + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  if (t == 0) {
-    bool ok = false;
-    for (uint32_t spin = 0; spin < (1u << 18); ++spin) {
-      if (__hip_atomic_load(published + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)SPLIT - 1) {
-        ok = true;
-        break;
+  };
+  // y rows of quarter q = p0 + p1 + p2 + p3 in part order (own part from LDS)
+  auto combine = [&](uint32_t q) {
+    u64x2 v[SPLIT][NQ];
+#pragma unroll
+    for (int o = 0; o < SPLIT; ++o) {
+      const __amdgpu_buffer_rsrc_t src = buf_rsrc(partial + ((size_t)o * nblocks + b) * VRP, 8 * VRP);
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const uint32_t p = q * QP + t + j * VT;
+        v[o][j] = (uint32_t)o == h ? yl2[p] : ld_128_sc1(src, 16 * p);
       }
-      __builtin_amdgcn_s_sleep(2);
     }
-    if (ok) {  // both counters back to zero for the next launch (every add of this one is in)
-      __hip_atomic_store(published + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {  // never observed: report it, and leave the counters for the host to reset
-      __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      T a0 = __builtin_bit_cast(T, (uint64_t)v[0][j].x), a1 = __builtin_bit_cast(T, (uint64_t)v[0][j].y);
+#pragma unroll
+      for (int o = 1; o < SPLIT; ++o) {
+        a0 = a0 + __builtin_bit_cast(T, (uint64_t)v[o][j].x);
+        a1 = a1 + __builtin_bit_cast(T, (uint64_t)v[o][j].y);
+      }
+      const uint32_t p = q * QP + t + j * VT;
+      if (2 * p < nr) y_out[r0 + 2 * p] = a0;
+      if (2 * p + 1 < nr) y_out[r0 + 2 * p + 1] = a1;
     }
+  };
+  __syncthreads();  // the entry waves' last (clamped) issue read segl after the final step barrier
+#pragma unroll
+  for (int k = 1; k < SPLIT; ++k) publish((h + k) % SPLIT);  // the other owners' quarters
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // lanes q != h count quarter q; an add that finds 3 is the fourth: the
+  // owner gave up waiting and published too, so this unit combines it
+  if ((uint32_t)t < (uint32_t)SPLIT && (uint32_t)t != h)
+    segl[t] = __hip_atomic_fetch_add(published + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) {  // the owner's wait for the three publishers of quarter h, bounded (~0.5 ms)
+    uint32_t ok = 0;
+    for (uint32_t spin = 0; spin < ((AB & 128) ? 0u : 1u << 10) && !ok; ++spin) {
+      ok = __hip_atomic_load(published + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)SPLIT - 1;
+      if (!ok) __builtin_amdgcn_s_sleep(2);
+    }
+    segl[SPLIT] = ok;
   }
   __syncthreads();
-  // y = p0 + p1 + p2 + p3 in part order, row pairs in chunks of 4 per lane
+  uint32_t todo = 0;  // bit q: this unit writes y rows of quarter q (workgroup-uniform: LDS words)
 #pragma unroll
-  for (int j0 = 0; j0 < NP; j0 += 4) {
-    T acc[4][2];
-#pragma unroll
-    for (int q = 0; q < SPLIT; ++q) {
-      u64x2 v[4];
-      if ((uint32_t)q == h) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = yl2[min((uint32_t)(t + (j0 + j) * VT), VRP / 2 - 1)];
-      } else {
-        const __amdgpu_buffer_rsrc_t src = buf_rsrc(partial + ((size_t)q * nblocks + b) * VRP, 8 * VRP);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = ld_128_sc1(src, 16 * min((uint32_t)(t + (j0 + j) * VT), VRP / 2 - 1));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const T w0 = __builtin_bit_cast(T, (uint64_t)v[j].x), w1 = __builtin_bit_cast(T, (uint64_t)v[j].y);
-        acc[j][0] = q == 0 ? w0 : acc[j][0] + w0;
-        acc[j][1] = q == 0 ? w1 : acc[j][1] + w1;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t p = t + (j0 + j) * VT;
-      if (2 * p < nr) y_out[r0 + 2 * p] = acc[j][0];
-      if (2 * p + 1 < nr) y_out[r0 + 2 * p + 1] = acc[j][1];
+  for (uint32_t q = 0; q < (uint32_t)SPLIT; ++q)
+    if (q != h && segl[q] == (uint32_t)SPLIT - 1) todo |= 1u << q;
+  if (segl[SPLIT]) {
+    todo |= 1u << h;
+    if (t == 0) __hip_atomic_store(published + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all 3 adds in
+  } else {
+    // a publisher of quarter h is not running yet (the grid is not all
+    // resident): publish our part of it as well and count it; whoever adds
+    // last (finds 3) combines the quarter -- nobody waits, so no deadlock
+    publish(h);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) segl[SPLIT + 1] = __hip_atomic_fetch_add(published + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (segl[SPLIT + 1] == (uint32_t)SPLIT - 1) {
+      todo |= 1u << h;
+      if (t == 0) __hip_atomic_store(published + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all 4 in
     }
   }
+#pragma unroll
+  for (uint32_t q = 0; q < (uint32_t)SPLIT; ++q) {
+    if (!(todo & (1u << q))) continue;
+    if (q != h && t == 0) __hip_atomic_store(published + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all 4 in
+    combine(q);
+  }
+  (void)status;  // no hand-off can time out into unpublished reads: the word stays 0
 }
 
-template <typename T, int WL, int DX, int DE, bool NOFB = false, int AB = 0>
+template <typename T, int WL, int DX, int DE, int AB = 0>
 static void launch_cfg(const VcacheArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_vquad<T, WL, DX, DE, 2, NOFB, AB>), dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s, a.seg, a.code,
+  hipLaunchKernelGGL((k_vquad<T, WL, DX, DE, 2, AB>), dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s, a.seg, a.code,
                      (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets,
                      a.status, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.npad, a.last, a.beta);
 }
 
 // the register window (entries one step holds) of configuration v
-static uint32_t vquad_window(int v) { return (uint32_t)((16 - (v == 2 || v == 3 ? 4 : 3)) * 64 * 2); }
+static uint32_t vquad_window(int) { return kVqLanes * 2; }  // two slots per compute lane
 
 template <typename T>
 static hipError_t launch_vquad_t(const VcacheArgs& a, hipStream_t s) {
   if (!vcache_grid_ok(a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.panel,
-                      a.split, kVcSplit4) ||
+                      a.split, kVcQuad) ||
       !a.status || a.max_seg > vquad_window(a.variant))
     return hipErrorInvalidValue;
-  switch (a.variant) {  // (loader waves, x panels in flight, entry steps in flight)
+  switch (a.variant) {  // (x panels in flight, entry steps in flight); 3 loader waves (the layout's CT)
     case 1: launch_cfg<T, 3, 4, 6>(a, s); break;
-    case 2: launch_cfg<T, 4, 4, 6>(a, s); break;
-    case 3: launch_cfg<T, 4, 6, 6>(a, s); break;
+    case 2: launch_cfg<T, 3, 2, 6>(a, s); break;
+    case 3: launch_cfg<T, 3, 3, 4>(a, s); break;
     case 4: launch_cfg<T, 3, 3, 8>(a, s); break;
-    case 5: launch_cfg<T, 3, 3, 6, true>(a, s); break;  // timing probe: runs past a wave left unfinished (wrong y)
+    case 5: launch_cfg<T, 3, 4, 4>(a, s); break;
+    case 17: launch_cfg<T, 3, 4, 3>(a, s); break;
+    case 18: launch_cfg<T, 3, 2, 4>(a, s); break;
+    case 19: launch_cfg<T, 3, 4, 5>(a, s); break;
+    case 20: launch_cfg<T, 3, 3, 6, 128>(a, s); break;  // exact: every owner gives up waiting
     // ablations (timing probes, wrong y): 6 no apply, 7 no x stores, 8 no combine,
-    // 9 no apply and no x stores, 10 no step barriers (races), 11 skeleton (1|2|4)
-    case 6: launch_cfg<T, 3, 3, 6, false, 1>(a, s); break;
-    case 7: launch_cfg<T, 3, 3, 6, false, 2>(a, s); break;
-    case 8: launch_cfg<T, 3, 3, 6, false, 4>(a, s); break;
-    case 9: launch_cfg<T, 3, 3, 6, false, 3>(a, s); break;
-    case 10: launch_cfg<T, 3, 3, 6, false, 8>(a, s); break;
-    case 11: launch_cfg<T, 3, 3, 6, false, 7>(a, s); break;
-    case 12: launch_cfg<T, 3, 3, 6, false, 7 | 32>(a, s); break;   // skeleton, entries only
-    case 13: launch_cfg<T, 3, 3, 6, false, 7 | 64>(a, s); break;   // skeleton, x only
-    case 14: launch_cfg<T, 3, 3, 6, false, 7 | 16>(a, s); break;   // skeleton, x by LDS-DMA
-    case 15: launch_cfg<T, 3, 3, 6, false, 7 | 8>(a, s); break;    // skeleton without step barriers
-    case 16: launch_cfg<T, 3, 3, 6, false, 7 | 8 | 16>(a, s); break;  // ... and x by LDS-DMA
+    // 9 no apply and no x stores, 10 no step barriers (races), 11 skeleton (1|2|4),
+    // 12 skeleton entries only, 13 skeleton x only, 14 skeleton x by LDS-DMA,
+    // 15 skeleton without barriers, 16 ... and x by LDS-DMA
+    case 6: launch_cfg<T, 3, 3, 6, 1>(a, s); break;
+    case 7: launch_cfg<T, 3, 3, 6, 2>(a, s); break;
+    case 8: launch_cfg<T, 3, 3, 6, 4>(a, s); break;
+    case 9: launch_cfg<T, 3, 3, 6, 3>(a, s); break;
+    case 10: launch_cfg<T, 3, 3, 6, 8>(a, s); break;
+    case 11: launch_cfg<T, 3, 3, 6, 7>(a, s); break;
+    case 12: launch_cfg<T, 3, 3, 6, 7 | 32>(a, s); break;
+    case 13: launch_cfg<T, 3, 3, 6, 7 | 64>(a, s); break;
+    case 14: launch_cfg<T, 3, 3, 6, 7 | 16>(a, s); break;
+    case 15: launch_cfg<T, 3, 3, 6, 7 | 8>(a, s); break;
+    case 16: launch_cfg<T, 3, 3, 6, 7 | 8 | 16>(a, s); break;
     default: launch_cfg<T, 3, 3, 6>(a, s); break;
   }
   return hipGetLastError();

@@ -31,3 +31,16 @@ def test_layout_builder_and_replay_under_sanitizers():
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     assert sum(": ok" in l for l in out.stdout.splitlines()) >= 60
     assert "runtime error" not in out.stderr and "AddressSanitizer" not in out.stderr
+
+
+def test_vquad_lanes_layout_replay():
+    # k_vquad (csrc/vquad.hip) over build_vcache_lanes: every x index inside its panel, every y
+    # row inside its block, one owner per row per step, lane pairs and wave-local runs intact,
+    # every entry consumed once; u64 exact, f64 within the FAST bound -- plain and under ASan/UBSan
+    for tool in ("vq_sim", "vq_sim_san"):
+        subprocess.run(["make", "-C", hs.PKG_DIR, f"lib/{tool}"], check=True, stdout=subprocess.DEVNULL)
+        out = subprocess.run([os.path.join(hs.LIB_DIR, tool)], capture_output=True, text=True, timeout=900)
+        assert out.returncode == 0, out.stdout + out.stderr[-4000:]
+        oks = [l for l in out.stdout.splitlines() if l.endswith(": ok")]
+        assert any(l.startswith("stripe") for l in oks) and len(oks) >= 8, out.stdout
+        assert "VIOLATION" not in out.stderr and "runtime error" not in out.stderr
