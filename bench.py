@@ -78,7 +78,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-secondary", action="store_true", help="skip timing the other mode")
     p.add_argument("--no-graph", action="store_true", help="time K plain launches instead of a captured HIP graph")
-    p.add_argument("--vcache-xlane", type=int, default=-1, choices=[-1, 0, 1, 2, 3],
+    p.add_argument("--vcache-xlane", type=int, default=-1, choices=[-1, 0, 1, 2, 3, 4],
                    help="experimental vcache option (include/hipspmv.h); not the default path")
     p.add_argument("--vcache-dma", type=int, default=-1, choices=[-1, 0, 1],
                    help="LDS-DMA x loader (-1: the library default, on for the split geometry)")

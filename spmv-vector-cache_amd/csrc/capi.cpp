@@ -111,8 +111,8 @@ struct hipspmv_handle {
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
   int vcache_map = 0;    // option "vcache_map": XCD-aware part placement (unused since k_vquad; kept as an option)
   int vquad_variant = 0;  // option "vquad_variant": k_vquad configuration (csrc/vquad.hip launch_vquad_t)
-  // bit 0: a k_vquad combine hand-off wait timed out (never observed; the
-  // launch's y is then wrong and the scratch counters need a reset)
+  // bit 0: reserved for a combine hand-off that timed out into unpublished
+  // partials (csrc/combine.h has no such path since round 4; the word stays 0)
   uint32_t* d_status = nullptr;
   // hipspmv_attach_pmc: a rocprofv3 --pmc counter CSV whose counters back the
   // cache statistics read_misses / hazard_stalls / capacity_stalls
@@ -232,11 +232,10 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
   if ((st = dev_upload(&v.d_code, L.code.data(), L.code.size(), h->device_bytes))) return fail(st);
   if ((st = dev_upload(&v.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return fail(st);
   if (v.split > 1) {
-    // [0, nblocks): arrival tickets, [nblocks, 2 nblocks): published partials
-    // (the ticket-first combine of k_vcache; k_vquad: 4 of each per block, per
-    // quarter of its rows, within the same words); both self-reset after each launch;
-    // then kVcProfWords per unit for the profile stamps (option "profile")
-    std::vector<uint32_t> zeros(2ull * v.nblocks + (uint64_t)kVcProfWords * v.nblocks * v.split, 0u);
+    // [4 b, 4 b + split): the published-share counters of block b (the owner
+    // combine, csrc/combine.h; they return to 0 within each launch), then
+    // kVcProfWords per unit for the profile stamps (option "profile")
+    std::vector<uint32_t> zeros(4ull * v.nblocks + (uint64_t)kVcProfWords * v.nblocks * v.split, 0u);
     if ((st = dev_upload(&v.d_tickets, zeros.data(), zeros.size(), h->device_bytes))) return fail(st);
     // partials: part q of block b at (q * nblocks + b) * VRP doubles, VRP = the
     // geometry's y block rounded up to even (k_vcache's 16-byte combine)
@@ -786,7 +785,7 @@ static int read_status(hipspmv_t* h, uint32_t* out) {
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(out, h->d_status, 4, hipMemcpyDeviceToHost));
   if (*out) {
-    if (h->vc[2].d_tickets) HIP_TRY(hipMemset(h->vc[2].d_tickets, 0, 4ull * 2 * 4 * h->vc[2].nblocks));  // k_vquad: per (block, quarter)
+    if (h->vc[2].d_tickets) HIP_TRY(hipMemset(h->vc[2].d_tickets, 0, 16ull * h->vc[2].nblocks));
     HIP_TRY(hipMemset(h->d_status, 0, 4));
   }
   return HIPSPMV_OK;
@@ -842,7 +841,7 @@ static int resolve_profile(hipspmv_t* h) {
   const auto& v = h->vc[h->prof_layout];
   const uint32_t units = v.nblocks * v.split;
   std::vector<uint32_t> st((size_t)kVcProfWords * units);
-  const uint32_t* src = h->prof_layout == 0 ? h->d_prof : v.d_tickets + 2ull * v.nblocks;
+  const uint32_t* src = h->prof_layout == 0 ? h->d_prof : v.d_tickets + 4ull * v.nblocks;
   HIP_TRY(hipMemcpy(st.data(), src, 4ull * st.size(), hipMemcpyDeviceToHost));
   const double cyc_per_tick = h->clock_khz / 1e5;
   auto at = [&](uint32_t u, int k) { return st[(size_t)kVcProfWords * u + k]; };
@@ -940,7 +939,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
     if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_nt = value;
   } else if (k == "vcache_xlane") {
-    if (value < -1 || value > 3) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < -1 || value > 4) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_xlane = (int)value;
   } else if (k == "mode") {
     if (value != HIPSPMV_MODE_ORDERED && value != HIPSPMV_MODE_FAST) return HIPSPMV_ERR_INVALID_ARG;

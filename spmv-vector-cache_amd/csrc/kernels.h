@@ -92,7 +92,7 @@ hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);
 // The same kernel in its default configuration (ordered: register-staged
 // loaders; split 3: LDS-DMA loaders, cross-lane runs when the layout fits)
 // with the profile stamps on (k_vcache AB bit 128): 8 u32 per workgroup at
-// a.tickets + 2 * nblocks (split 3) or at a.partial (split 1).  Results are
+// a.tickets + 4 * nblocks (split 3) or at a.partial (split 1).  Results are
 // the default kernel's bits.  Split 4: hipErrorInvalidValue.
 hipError_t launch_vcache_profiled(int dtype, const VcacheArgs& a, hipStream_t s);
 constexpr int kVcProfWords = 8;

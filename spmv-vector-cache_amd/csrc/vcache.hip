@@ -27,6 +27,7 @@
 
 #include <type_traits>
 
+#include "combine.h"
 #include "device_common.h"
 #include "vc_map.h"
 #include "hipspmv_internal.h"
@@ -61,7 +62,7 @@ struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane
 // 2 no x LDS stores, 4 no entry loads, 8 no compute, 16 x always from panel 0,
 // 32 no per-panel barrier, 64 no column-part combine (wrong results, timing only),
 // 128 profile stamps, results unchanged (option "profile"): 8 u32
-// per workgroup at tickets + 2 * nblocks + 8 * blockIdx.x (SPLIT 1: at partial):
+// per workgroup at tickets + 4 * nblocks + 8 * blockIdx.x (SPLIT 1: at partial):
 // s_memrealtime (100 MHz) at start, main-loop start, main-loop end, exit; the
 // combine ticket; s_memtime cycles summed over the steps: loader wave 0 working,
 // loader wave 0 waiting at the step barrier, first compute wave waiting there.
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   const uint32_t r0 = b * rows_per_block;
   if (r0 >= rows) return;  // never with a vcache_grid_ok geometry (workgroup-uniform, before any barrier)
   const uint32_t nr = min(rows_per_block, rows - r0);
-  uint32_t* const sbuf = (SPLIT == 1 ? reinterpret_cast<uint32_t*>(partial) : tickets + 2 * nblocks) + 8 * blockIdx.x;
+  uint32_t* const sbuf = (SPLIT == 1 ? reinterpret_cast<uint32_t*>(partial) : tickets + 4 * nblocks) + 8 * blockIdx.x;
   auto stamp = [&](int k, uint32_t v) {
     if ((AB & 128) && t == 0) sbuf[k] = v;
   };
@@ -182,6 +183,25 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       return;
     }
     const uint32_t beg = segl[min(s, npad)];
+    if constexpr (CX == 4) {
+      // masked: a lane past the step's segment gets an out-of-range offset in
+      // a descriptor of the unit's entries -- zero, and no memory request
+      // (clamped lanes re-read the next segment: 1.1x the entry requests here,
+      // 1.68x at four parts)
+      const uint32_t e0 = __builtin_amdgcn_readfirstlane(segl[0]);
+      const uint32_t ne = __builtin_amdgcn_readfirstlane(segl[npu]) - e0;
+      const uint32_t end = segl[min(s + 1, npad)] - e0;
+      const __amdgpu_buffer_rsrc_t dc = buf_rsrc(ecode + e0, 4 * ne), dv = buf_rsrc(evals + e0, 8 * ne);
+      constexpr int aux = decltype(ntc)::value || NT ? 2 : 0;  // nt
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        const uint32_t q = beg - e0 + ct + j * CT;
+        const bool in = q < end;
+        c[j] = __builtin_amdgcn_raw_buffer_load_b32(dc, in ? (int)(4 * q) : (int)0x80000000, 0, aux);
+        v[j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(dv, in ? (int)(8 * q) : (int)0x80000000, 0, aux));
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const uint32_t i = min(beg + ct + j * CT, last);
@@ -441,124 +461,13 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     if (AB & 128) stamp(3, now());
     return;
   }
-  // ---- combine the column parts, fixed order p0 + p1 + p2 (+ p3), ticket
-  // first: one lane adds to the block's arrival counter tickets[b]; the
-  // workgroups that arrive before the last publish their partial and count it
-  // in tickets[nblocks + b]; the last one does not publish (its partial stays
-  // in LDS), waits for the others' count, reads their partials and writes y.
-  // Hand-off per MI355X_MICROARCH.md (Valid forms, table row 1): every
-  // partial byte stored write-through (sc1: agent-scope relaxed atomic
-  // store), every storing wave drains vmcnt, then after the barrier one lane
-  // makes the agent-scope add; the consumer polls the count with sc1 loads
-  // from one lane and its waves load (sc1) after the barrier that lane joins.
-  // No wait can deadlock: the publishers took their tickets before the last
-  // arriver did, so they are running and publish unconditionally.
-  // Partials: part q of block b at partial + (q * nblocks + b) * VRP, VRP even,
-  // so each lane moves row pairs with 16-byte write-through (sc1) buffer
-  // accesses, NP of them in flight per lane.
-  constexpr uint32_t VRP = (VR + 1) & ~1u;
-  constexpr int NP = (VRP / 2 + VT - 1) / VT;  // row pairs per lane
-  uint32_t* const published = tickets + nblocks;
-  if (t == 0) segl[0] = __hip_atomic_fetch_add(tickets + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const u64x2* const yl2 = reinterpret_cast<const u64x2*>(ylds);  // ylds: VR (even) doubles, 16-B aligned
-  const uint32_t npairs = (nr + 1) / 2;
-  if (segl[0] != (uint32_t)SPLIT - 1) {
-    const __amdgpu_buffer_rsrc_t mine = buf_rsrc(partial + ((size_t)h * nblocks + b) * VRP, 8 * VRP);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const uint32_t p = t + j * VT;
-      if (p < npairs) st_128_sc1(mine, 16 * p, yl2[p]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) __hip_atomic_fetch_add(published + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (AB & 128) {
-      stamp(3, now());
-      stamp(4, segl[0]);
-    }
-    return;
-  }
-  if (t == 0) {
-    // bounded spin (~0.3 s of sc1 polls): the protocol cannot deadlock, and a bound keeps a
-    // broken invariant from hanging the GPU (the parity tests would see it)
-    for (uint32_t spin = 0; spin < (1u << 18); ++spin) {
-      if (__hip_atomic_load(published + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)SPLIT - 1) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-    // both counters back to zero for the next launch (every add of this one is in)
-    __hip_atomic_store(published + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if constexpr (SPLIT == 4) {
-    // four parts: row pairs in chunks of 4 per lane (all 8 at once spilled
-    // past 128 VGPRs), y = p0 + p1 + p2 + p3 in part order
-    static_assert(NP % 4 == 0, "whole chunks");
-#pragma unroll
-    for (int j0 = 0; j0 < NP; j0 += 4) {
-      T acc[4][2];
-#pragma unroll
-      for (int q = 0; q < SPLIT; ++q) {
-        u64x2 v[4];
-        if ((uint32_t)q == h) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = yl2[min((uint32_t)(t + (j0 + j) * VT), VRP / 2 - 1)];
-        } else {
-          const __amdgpu_buffer_rsrc_t src = buf_rsrc(partial + ((size_t)q * nblocks + b) * VRP, 8 * VRP);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = ld_128_sc1(src, 16 * min((uint32_t)(t + (j0 + j) * VT), VRP / 2 - 1));
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const T w0 = __builtin_bit_cast(T, (uint64_t)v[j].x), w1 = __builtin_bit_cast(T, (uint64_t)v[j].y);
-          acc[j][0] = q == 0 ? w0 : acc[j][0] + w0;
-          acc[j][1] = q == 0 ? w1 : acc[j][1] + w1;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t p = t + (j0 + j) * VT;
-        if (2 * p < nr) y_out[r0 + 2 * p] = acc[j][0];
-        if (2 * p + 1 < nr) y_out[r0 + 2 * p + 1] = acc[j][1];
-      }
-    }
-    if (AB & 128) {
-      stamp(3, now());
-      stamp(4, segl[0]);
-    }
-    return;
-  }
-  // y = p0 + p1 + p2 (+ p3) in part order; part h from LDS, the others loaded
-  T acc[NP][2];
-#pragma unroll
-  for (int q = 0; q < SPLIT; ++q) {
-    u64x2 v[NP];
-    if ((uint32_t)q == h) {
-#pragma unroll
-      for (int j = 0; j < NP; ++j) v[j] = yl2[min((uint32_t)(t + j * VT), VRP / 2 - 1)];
-    } else {
-      const __amdgpu_buffer_rsrc_t src = buf_rsrc(partial + ((size_t)q * nblocks + b) * VRP, 8 * VRP);
-#pragma unroll
-      for (int j = 0; j < NP; ++j) v[j] = ld_128_sc1(src, 16 * min((uint32_t)(t + j * VT), VRP / 2 - 1));
-    }
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {  // components by name (.x/.y): an indexed subscript lost .y
-      const T w0 = __builtin_bit_cast(T, (uint64_t)v[j].x), w1 = __builtin_bit_cast(T, (uint64_t)v[j].y);
-      acc[j][0] = q == 0 ? w0 : acc[j][0] + w0;
-      acc[j][1] = q == 0 ? w1 : acc[j][1] + w1;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    const uint32_t p = t + j * VT;
-    if (2 * p < nr) y_out[r0 + 2 * p] = acc[j][0];
-    if (2 * p + 1 < nr) y_out[r0 + 2 * p + 1] = acc[j][1];
-  }
-  if (AB & 128) {
-    stamp(3, now());
-    stamp(4, segl[0]);
-  }
+  // ---- combine the column parts, fixed order p0 + p1 + p2 (+ p3): unit h
+  // owns share h of the block's row pairs (csrc/combine.h); counters at
+  // tickets + 4 b, partials of part q of block b at partial + (q * nblocks + b) * VRP
+  __syncthreads();  // segl is the combine's scratch from here
+  owner_combine<T, SPLIT, VT, (VR + 1) & ~1u>(ylds, segl, partial, tickets + 4 * (size_t)b, b, h, nblocks, nr,
+                                              y_out + r0, t);
+  if (AB & 128) stamp(3, now());
 }
 
 template <typename T, int SPLIT, int LD, int CX = 0, int MAP = 0>
@@ -578,8 +487,12 @@ static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
       launch_one<T, SPLIT, 1, 1, MAP>(a, s);
     else if (cx == 2)
       launch_one<T, SPLIT, 1, 2, MAP>(a, s);
-    else
+    else if (cx == 3)
       launch_one<T, SPLIT, 1, 3, MAP>(a, s);
+    else
+      launch_one<T, SPLIT, 1, 4, MAP>(a, s);
+  } else if (cx == 4) {  // (split 3 only)
+    launch_one<T, SPLIT, 0, 3, MAP>(a, s);
   } else if (cx == 0) {
     ld == 1 ? launch_one<T, SPLIT, 1, 0, MAP>(a, s) : launch_one<T, SPLIT, 0, 0, MAP>(a, s);
   } else if (cx == 1) {
@@ -606,7 +519,8 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   };
   // xlane 1: cross-lane continuation; 2: also padded loops and asm rings
   // (entries, and x unless LDS-DMA stages it) with explicit vmcnt waits;
-  // 3: cross-lane continuation and padded loops, the compiler's own waits.
+  // 3: cross-lane continuation and padded loops, the compiler's own waits;
+  // 4 (split 3): 3 with the entry loads masked past each step's segment.
   // -1 (default): 3 for the split geometry (C3: 131.7 us against 135.7 with
   // the run continuation re-read from memory), 0 for the others.
   const int xl = a.xlane < 0 ? (a.split == 3 ? 3 : 0) : a.xlane;

@@ -32,19 +32,12 @@
 // One s_barrier per panel.
 //
 // Combine (fixed order y = p0 + p1 + p2 + p3, deterministic): unit h owns
-// quarter h of the block's rows.  It publishes its partials of the other three
-// quarters with write-through (sc1) 16-byte stores, drains, counts each one
-// (agent-scope add on the quarter's word), then waits for the three
-// publishers of its own quarter, reads their partials (sc1) and writes those
-// y rows (MI355X_MICROARCH.md, Valid forms, table row 1).  The four parts run
-// at once (one wave of 256 units), so each CU moves 96 KiB out and 96 KiB in;
-// the single-combiner form (the last arriver reads 384 KiB) cost 11.5 us of
-// 118 at C3.  Deadlock freedom does not rest on co-residency: the owner's
-// wait is bounded, and an owner that gives up publishes its own part and
-// counts it too -- the add that finds the count at 3 (all four in) belongs to
-// the unit that combines the quarter, which then needs to wait for nothing.
+// quarter h of the block's rows and combines it; the other quarters it
+// publishes (csrc/combine.h: bounded owner wait, publish-and-count fallback,
+// so no deadlock rests on co-residency).
 #include <hip/hip_runtime.h>
 
+#include "combine.h"
 #include "device_common.h"
 #include "hipspmv_internal.h"
 #include "kernels.h"
@@ -320,92 +313,10 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
     for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
     return;
   }
-  // ---- combine: unit h owns quarter h of the block's rows (header comment)
-  constexpr uint32_t VRP = (VR + 1) & ~1u;
-  constexpr uint32_t QP = VRP / 2 / SPLIT;  // row pairs per quarter
-  constexpr int NQ = QP / VT;               // row pairs per lane per quarter
-  static_assert(QP % VT == 0 && NQ >= 1, "whole quarters");
-  uint32_t* const published = tickets + (size_t)SPLIT * b;  // [q]: partials of quarter q published
-  const u64x2* const yl2 = reinterpret_cast<const u64x2*>(ylds);
-  const uint32_t npairs = (nr + 1) / 2;
-  const __amdgpu_buffer_rsrc_t mine = buf_rsrc(partial + ((size_t)h * nblocks + b) * VRP, 8 * VRP);
-  auto publish = [&](uint32_t q) {
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) {
-      const uint32_t p = q * QP + t + j * VT;
-      if (p < npairs) st_128_sc1(mine, 16 * p, yl2[p]);
-    }
-  };
-  // y rows of quarter q = p0 + p1 + p2 + p3 in part order (own part from LDS)
-  auto combine = [&](uint32_t q) {
-    u64x2 v[SPLIT][NQ];
-#pragma unroll
-    for (int o = 0; o < SPLIT; ++o) {
-      const __amdgpu_buffer_rsrc_t src = buf_rsrc(partial + ((size_t)o * nblocks + b) * VRP, 8 * VRP);
-#pragma unroll
-      for (int j = 0; j < NQ; ++j) {
-        const uint32_t p = q * QP + t + j * VT;
-        v[o][j] = (uint32_t)o == h ? yl2[p] : ld_128_sc1(src, 16 * p);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) {
-      T a0 = __builtin_bit_cast(T, (uint64_t)v[0][j].x), a1 = __builtin_bit_cast(T, (uint64_t)v[0][j].y);
-#pragma unroll
-      for (int o = 1; o < SPLIT; ++o) {
-        a0 = a0 + __builtin_bit_cast(T, (uint64_t)v[o][j].x);
-        a1 = a1 + __builtin_bit_cast(T, (uint64_t)v[o][j].y);
-      }
-      const uint32_t p = q * QP + t + j * VT;
-      if (2 * p < nr) y_out[r0 + 2 * p] = a0;
-      if (2 * p + 1 < nr) y_out[r0 + 2 * p + 1] = a1;
-    }
-  };
+  // ---- combine: unit h owns quarter h of the block's rows (csrc/combine.h)
   __syncthreads();  // the entry waves' last (clamped) issue read segl after the final step barrier
-#pragma unroll
-  for (int k = 1; k < SPLIT; ++k) publish((h + k) % SPLIT);  // the other owners' quarters
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // lanes q != h count quarter q; an add that finds 3 is the fourth: the
-  // owner gave up waiting and published too, so this unit combines it
-  if ((uint32_t)t < (uint32_t)SPLIT && (uint32_t)t != h)
-    segl[t] = __hip_atomic_fetch_add(published + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t == 0) {  // the owner's wait for the three publishers of quarter h, bounded (~0.5 ms)
-    uint32_t ok = 0;
-    for (uint32_t spin = 0; spin < ((AB & 128) ? 0u : 1u << 10) && !ok; ++spin) {
-      ok = __hip_atomic_load(published + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)SPLIT - 1;
-      if (!ok) __builtin_amdgcn_s_sleep(2);
-    }
-    segl[SPLIT] = ok;
-  }
-  __syncthreads();
-  uint32_t todo = 0;  // bit q: this unit writes y rows of quarter q (workgroup-uniform: LDS words)
-#pragma unroll
-  for (uint32_t q = 0; q < (uint32_t)SPLIT; ++q)
-    if (q != h && segl[q] == (uint32_t)SPLIT - 1) todo |= 1u << q;
-  if (segl[SPLIT]) {
-    todo |= 1u << h;
-    if (t == 0) __hip_atomic_store(published + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all 3 adds in
-  } else {
-    // a publisher of quarter h is not running yet (the grid is not all
-    // resident): publish our part of it as well and count it; whoever adds
-    // last (finds 3) combines the quarter -- nobody waits, so no deadlock
-    publish(h);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) segl[SPLIT + 1] = __hip_atomic_fetch_add(published + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (segl[SPLIT + 1] == (uint32_t)SPLIT - 1) {
-      todo |= 1u << h;
-      if (t == 0) __hip_atomic_store(published + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all 4 in
-    }
-  }
-#pragma unroll
-  for (uint32_t q = 0; q < (uint32_t)SPLIT; ++q) {
-    if (!(todo & (1u << q))) continue;
-    if (q != h && t == 0) __hip_atomic_store(published + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // all 4 in
-    combine(q);
-  }
+  owner_combine<T, SPLIT, VT, (VR + 1) & ~1u, (AB & 128) != 0>(ylds, segl, partial, tickets + (size_t)SPLIT * b, b, h,
+                                                               nblocks, nr, y_out + r0, t);
   (void)status;  // no hand-off can time out into unpublished reads: the word stays 0
 }
 

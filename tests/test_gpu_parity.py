@@ -522,6 +522,52 @@ def test_vquad_variants(gpu, variant):  # configurations: x / entry ring depths 
     assert ran >= 3  # shapes whose runs the lane placement cannot keep inside waves are not eligible
 
 
+@pytest.mark.parametrize("xlane", [3, 4])
+def test_vcache_split_entry_loads(gpu, xlane):  # 3: clamped entry loads; 4: masked past the segment
+    cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20), (16385, 12001)]
+    ran = 0
+    for rows, cols in cases:
+        rng = np.random.default_rng(rows + 7 * xlane)
+        if cols >= 1 << 20:
+            rowptr, colind, vals = hs.gen_stripe_csr(0, rows, cols, 32)
+        else:
+            lens = rng.integers(0, 14, rows)
+            rowptr = np.zeros(rows + 1, np.uint32)
+            rowptr[1:] = np.cumsum(lens)
+            colind = np.concatenate([np.sort(rng.choice(cols, n, replace=False)) for n in lens]).astype(np.uint32)
+            vals = rng.uniform(-1, 1, colind.size)
+        x = rng.uniform(-1, 1, cols)
+        h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+        if not h.stat("vcache_split_eligible"):
+            h.close()
+            continue
+        h.set_kernel("vcache_split")
+        h.set_option("vcache_xlane", xlane)
+        colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+        lens = np.diff(rowptr.astype(np.int64))
+        absprod = np.bincount(np.repeat(np.arange(rows), lens), weights=np.abs(vals * x[colind]), minlength=rows)
+        for beta in (0, 1):
+            y0 = rng.uniform(-1, 1, rows)
+            y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else None), rows=rows)
+            ys = [h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST) for _ in range(2)]
+            assert ys[0].tobytes() == ys[1].tobytes(), (rows, cols, beta)  # deterministic
+            bound = 2.0 * (lens + 1) * 2.0 ** -53 * (absprod + (np.abs(y0) if beta else 0)) + 1e-300
+            assert np.all(np.abs(ys[0] - y_ref) <= bound), (rows, cols, beta)
+        if rows <= 70001:  # the u64 semiring: exact mod 2^64
+            uv = rng.integers(0, 2**64, colind.size, dtype=np.uint64)
+            ux = rng.integers(0, 2**64, cols, dtype=np.uint64)
+            hu = hs.Handle.from_csr(rowptr, colind, uv, rows, cols)
+            hu.set_kernel("vcache_split")
+            hu.set_option("vcache_xlane", xlane)
+            _, _, cuv = oracle.csr2csc(rows, cols, rowptr, colind, uv)
+            assert hu.exec(ux, beta=0, mode=hs.MODE_FAST).tobytes() == \
+                oracle.spmv_csc(colptr, rowind, cuv, ux, rows=rows).tobytes(), (rows, cols)
+            hu.close()
+        h.close()
+        ran += 1
+    assert ran >= 3
+
+
 def test_vquad_c3_full_size(gpu):
     # the four-part kernel on full C3: x streamed into LDS per launch is 64 row
     # blocks x 8 MB (three parts: 85 x 8 MB); deterministic and within the bound
