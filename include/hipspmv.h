@@ -73,7 +73,7 @@ extern "C" {
 #define HIPSPMV_KERNEL_WGATHER 6 /* y block in LDS, x gathered from global in
                                     2^17-column windows (wide x: C4/C5);
                                     ordered; experimental like VCACHE_SPLIT4 */
-#define HIPSPMV_KERNEL_WCSR 8 /* csr_vector over the rows cut at 2^17-column
+#define HIPSPMV_KERNEL_WCSR 8 /* csr_vector over the rows cut at 2^20-column
                                  windows (window-major), then each row's window
                                  partials summed in a fixed order; fast,
                                  deterministic; wide, skewed x (C5 shards) */

@@ -3,7 +3,9 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "hipspmv.h"
@@ -65,16 +67,17 @@ constexpr VcGeom kVcQuad{16384, 1984, 4, 12};
 constexpr uint32_t kVqLanes = 13 * 64;  // k_vquad's compute lanes (13 of 16 waves): the layout's CT
 
 // ---- wcsr: csr_vector over the column-windowed segment matrix
-// Every row is cut at column windows of 2^kWcLog2Window columns (1 MiB of
+// Every row is cut at column windows of 2^kWcLog2Window columns (8 MiB of
 // x); the pieces ("segments", one per (window, row) pair that has
 // entries) form the rows of A', in window-major order.  csr_vector over A'
 // walks x one window at a time; y[r] is the sum of r's segment partials in
-// window order (k_wreduce).  One width for every matrix (round 4): the
-// round-3 rule (2^16 unless that left more than one segment per five
-// entries) chose by the shard's own row lengths, so two shards of one matrix
-// could cut a row differently; 2^17 measured 275 / 313 / 410 us on C5 shards
-// 0 / 3 / 7 against 269 / 343 / 436 at 2^16.
-constexpr uint32_t kWcLog2Window = 17;
+// window order (k_wreduce).  One width for every matrix (a width that depends
+// on the shard could cut a row differently in two partitions).  Round 4, C5
+// 8-way cost partition, slowest shard / fastest (profiles/r04/logs
+// bench_c5_cost.log, bench_c5_w*.log): 2^17 309.5 / 288.3 us, 2^18 297.2,
+// 2^19 286.0, 2^20 283.2 / 271.3, 2^21 293.9, 2^22 319.2 -- fewer segments
+// (shard 7: 11.8 M at 2^17, 6.6 M at 2^20) against gathers over more of x.
+constexpr uint32_t kWcLog2Window = 20;
 // AUTO considers wcsr from this many columns (x of 16 MiB: four XCD L2s)
 // wcsr LDS form (k_wseg, opt-in HIPSPMV_WCSR_LDS=1): x windows of 2^14 f64
 // (128 KiB of LDS), chunks of at most kWsChunkNnz entries of one window per
@@ -152,10 +155,38 @@ inline bool vcache_grid_ok(uint32_t rows, uint32_t cols, uint32_t rows_per_block
   return npad + 1 <= (uint32_t)kVcSegMax && npad >= part_panels;
 }
 
+// Host arrays the size of the matrix: resize() leaves new elements
+// uninitialised (no single-threaded zero fill -- the builders write every
+// element, from several threads, so the pages are first touched in parallel).
+template <class T>
+struct UninitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = UninitAlloc<U>;
+  };
+  UninitAlloc() = default;
+  template <class U>
+  UninitAlloc(const UninitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... args) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(args)...);
+  }
+};
+template <class T>
+using hvec = std::vector<T, UninitAlloc<T>>;
+
+// Worker threads of the host-side builders: $HIPSPMV_THREADS, else
+// $OMP_NUM_THREADS, else min(16, hardware threads) (plan.cpp).
+unsigned plan_threads();
+
 struct HostCSR {
   uint32_t rows = 0, cols = 0, nnz = 0;
-  std::vector<uint32_t> rowptr, colind;
-  std::vector<uint64_t> vals;  // 8-byte words (f64 bits or u64)
+  hvec<uint32_t> rowptr, colind;
+  hvec<uint64_t> vals;  // 8-byte words (f64 bits or u64)
 };
 
 struct VcacheLayout {
@@ -164,8 +195,8 @@ struct VcacheLayout {
   uint32_t part_panels = 0;  // panels of the largest column part (vc_part_first cuts: parts differ by <= 1)
   uint32_t npad = 0;         // seg entries per unit - 1 (= part_panels)
   std::vector<uint32_t> seg;    // (nblocks * split) units * (npad + 1) global entry offsets
-  std::vector<uint32_t> code;   // per entry: col_local | row_local << 16 | CONT | MORE
-  std::vector<uint64_t> vals;   // per entry
+  hvec<uint32_t> code;          // per entry: col_local | row_local << 16 | CONT | MORE
+  hvec<uint64_t> vals;          // per entry
   uint32_t max_seg = 0;
   uint32_t max_run = 0;  // longest run of one row inside one segment
   uint64_t n_cont = 0;   // entries continuing a run (added after another entry of their row in one step)
@@ -175,18 +206,18 @@ struct WinLayout {
   uint32_t log2w = 0, nseg = 0, max_seg = 0;
   std::vector<uint32_t> winseg;  // windows + 1: window w's segments are [winseg[w], winseg[w+1])
   HostCSR seg;                  // A': rows = segments (window-major, then row), cols = the matrix's
-  std::vector<uint32_t> rowseg; // rows + 1: row r's segments are segidx[rowseg[r] .. rowseg[r+1])
-  std::vector<uint32_t> segidx; // nseg: segment ids of each row, in window order
+  hvec<uint32_t> rowseg;        // rows + 1: row r's segments are segidx[rowseg[r] .. rowseg[r+1])
+  hvec<uint32_t> segidx;        // nseg: segment ids of each row, in window order
 };
 
 struct SellLayout {
   uint32_t nslices = 0, nhubs = 0, niso = 0;
   std::vector<uint64_t> off;    // nslices + 1: first entry of each slice
   std::vector<uint32_t> width;  // nslices: longest row of the slice
-  std::vector<uint32_t> row;    // nslices * kSellRows: row id (kSellNoRow past the window's rows)
-  std::vector<uint32_t> len;    // nslices * kSellRows: row length (0 for kSellNoRow)
-  std::vector<uint32_t> col;    // off[nslices] entries; padding: column 0
-  std::vector<uint64_t> vals;   // padding: 0 (never added: k < len selects)
+  hvec<uint32_t> row;           // nslices * kSellRows: row id (kSellNoRow past the window's rows)
+  hvec<uint32_t> len;           // nslices * kSellRows: row length (0 for kSellNoRow)
+  hvec<uint32_t> col;           // off[nslices] entries; padding: column 0
+  hvec<uint64_t> vals;          // padding: 0 (never added: k < len selects)
   std::vector<uint32_t> hubs;   // hub rows, longest first (ORDERED: one wave each)
   std::vector<uint32_t> pieces; // FAST: kSellPieceWords per piece, pieces of a row contiguous
   uint32_t npieces = 0, ntickets = 0;

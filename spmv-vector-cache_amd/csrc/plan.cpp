@@ -1,6 +1,8 @@
 // Host-side planning for libhipspmv: CSC -> CSR transpose, validation, and the
 // device layouts each kernel reads.
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -11,12 +13,58 @@ namespace hipspmv {
 
 namespace {
 constexpr uint32_t kRowMask = 0x3FFFFFFFu;  // SparseMatrix.cpp:64,77 cold-miss-skip bits
+
+// fn(t, lo, hi) over nt contiguous chunks of [0, n), chunk 0 on the calling
+// thread.  The builders allocate before they fork: a worker never throws.
+template <class F>
+void par_chunks(uint64_t n, unsigned nt, F&& fn) {
+  nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nt, n));
+  std::vector<std::thread> ts;
+  for (unsigned t = 1; t < nt; ++t) ts.emplace_back([&fn, t, n, nt] { fn(t, n * t / nt, n * (t + 1) / nt); });
+  fn(0u, (uint64_t)0, n / nt);
+  for (auto& th : ts) th.join();
+}
+
+// row ranges of about nnz / nt entries each: rows [b[t], b[t+1])
+std::vector<uint32_t> row_chunks(const uint32_t* rowptr, uint32_t rows, unsigned nt) {
+  std::vector<uint32_t> b(nt + 1, rows);
+  b[0] = 0;
+  const uint64_t nnz = rowptr[rows];
+  for (unsigned t = 1; t < nt; ++t) {
+    const uint32_t target = (uint32_t)(nnz * t / nt);
+    b[t] = (uint32_t)(std::lower_bound(rowptr, rowptr + rows + 1, target) - rowptr);
+    b[t] = std::max(std::min(b[t], rows), b[t - 1]);
+  }
+  return b;
+}
+
+// fn(t, r0, r1) over entry-balanced row ranges, in parallel
+template <class F>
+void par_rows(const uint32_t* rowptr, uint32_t rows, F&& fn) {
+  const unsigned nt = std::max(1u, std::min(plan_threads(), std::max(1u, rows / 64)));
+  const std::vector<uint32_t> b = row_chunks(rowptr, rows, nt);
+  par_chunks(nt, nt, [&](unsigned, uint64_t lo, uint64_t hi) {
+    for (uint64_t t = lo; t < hi; ++t) fn((unsigned)t, b[t], b[t + 1]);
+  });
+}
+}  // namespace
+
+unsigned plan_threads() {
+  for (const char* k : {"HIPSPMV_THREADS", "OMP_NUM_THREADS"})
+    if (const char* e = std::getenv(k)) {
+      const int v = std::atoi(e);
+      if (v > 0) return (unsigned)std::min(v, 256);
+    }
+  return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
 }
 
 // Stable counting-sort transpose, the algorithm of software/csr2csc.c:11-39
 // applied to the CSC arrays (so it yields CSR with column ids ascending within
 // each row, and duplicate entries in their CSC order -- exactly the order in
 // which SoftwareSpMV::exec (SoftwareSpMV.cpp:59-64) adds them into y[row]).
+// In parallel: thread t owns a range of rows, counts and places only their
+// entries while walking every column in order -- the same bytes as a serial
+// transpose.
 int csc_to_csr(const uint32_t* colptr, const uint32_t* rowind, const void* vals, uint32_t rows, uint32_t cols,
                uint32_t nnz, HostCSR& out, std::string& why) {
   if (colptr[0] != 0 || colptr[cols] != nnz) {
@@ -28,30 +76,57 @@ int csc_to_csr(const uint32_t* colptr, const uint32_t* rowind, const void* vals,
       why = "colptr not monotone at column " + std::to_string(c);
       return HIPSPMV_ERR_INVALID_MATRIX;
     }
+  const unsigned nt = std::max(1u, std::min(plan_threads(), std::max(1u, rows / 1024)));
+  {  // the first out-of-range row id
+    std::vector<uint64_t> bad(nt, UINT64_MAX);
+    par_chunks(nnz, nt, [&](unsigned t, uint64_t lo, uint64_t hi) {
+      for (uint64_t e = lo; e < hi; ++e)
+        if ((rowind[e] & kRowMask) >= rows) {
+          bad[t] = e;
+          return;
+        }
+    });
+    const uint64_t e = *std::min_element(bad.begin(), bad.end());
+    if (e != UINT64_MAX) {
+      why = "row id " + std::to_string(rowind[e] & kRowMask) + " out of range at element " + std::to_string(e);
+      return HIPSPMV_ERR_INVALID_MATRIX;
+    }
+  }
   out.rows = rows;
   out.cols = cols;
   out.nnz = nnz;
-  out.rowptr.assign((size_t)rows + 1, 0);
-  for (uint32_t e = 0; e < nnz; ++e) {
-    const uint32_t r = rowind[e] & kRowMask;
-    if (r >= rows) {
-      why = "row id " + std::to_string(r) + " out of range at element " + std::to_string(e);
-      return HIPSPMV_ERR_INVALID_MATRIX;
-    }
-    out.rowptr[r + 1]++;
-  }
-  for (uint32_t r = 0; r < rows; ++r) out.rowptr[r + 1] += out.rowptr[r];
+  out.rowptr.resize((size_t)rows + 1);
   out.colind.resize(nnz);
   out.vals.resize(nnz);
-  std::vector<uint32_t> cursor(out.rowptr.begin(), out.rowptr.end() - 1);
   const uint64_t* v = static_cast<const uint64_t*>(vals);
-  for (uint32_t c = 0; c < cols; ++c) {
-    for (uint32_t e = colptr[c]; e < colptr[c + 1]; ++e) {
-      const uint32_t d = cursor[rowind[e] & kRowMask]++;
-      out.colind[d] = c;
-      out.vals[d] = v[e];
+  auto rlo = [&](uint64_t t) { return (uint32_t)((uint64_t)rows * t / nt); };
+  par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {  // counts of the thread's rows
+    for (uint64_t t = t0; t < t1; ++t) {
+      const uint32_t r0 = rlo(t), span = rlo(t + 1) - r0;
+      for (uint32_t r = r0; r < r0 + span; ++r) out.rowptr[r + 1] = 0;
+      for (uint32_t e = 0; e < nnz; ++e) {
+        const uint32_t r = (rowind[e] & kRowMask) - r0;
+        if (r < span) out.rowptr[r0 + r + 1]++;
+      }
     }
-  }
+  });
+  out.rowptr[0] = 0;
+  for (uint32_t r = 0; r < rows; ++r) out.rowptr[r + 1] += out.rowptr[r];
+  hvec<uint32_t> cursor(out.rowptr.begin(), out.rowptr.end() - 1);
+  par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
+    for (uint64_t t = t0; t < t1; ++t) {
+      const uint32_t r0 = rlo(t), span = rlo(t + 1) - r0;
+      for (uint32_t c = 0; c < cols; ++c)
+        for (uint32_t e = colptr[c]; e < colptr[c + 1]; ++e) {
+          const uint32_t r = (rowind[e] & kRowMask) - r0;
+          if (r < span) {
+            const uint32_t d = cursor[r0 + r]++;
+            out.colind[d] = c;
+            out.vals[d] = v[e];
+          }
+        }
+    }
+  });
   return HIPSPMV_OK;
 }
 
@@ -66,18 +141,31 @@ int copy_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, u
       why = "rowptr not monotone at row " + std::to_string(r);
       return HIPSPMV_ERR_INVALID_MATRIX;
     }
-  for (uint32_t e = 0; e < nnz; ++e)
-    if (colind[e] >= cols) {
-      why = "column id " + std::to_string(colind[e]) + " out of range at element " + std::to_string(e);
-      return HIPSPMV_ERR_INVALID_MATRIX;
-    }
   out.rows = rows;
   out.cols = cols;
   out.nnz = nnz;
   out.rowptr.assign(rowptr, rowptr + (size_t)rows + 1);
-  out.colind.assign(colind, colind + nnz);
+  out.colind.resize(nnz);
   out.vals.resize(nnz);
-  if (nnz) std::memcpy(out.vals.data(), vals, sizeof(uint64_t) * nnz);
+  // copy (first touch of the pages in parallel) and check the column ids
+  const unsigned nt = plan_threads();
+  std::vector<uint64_t> bad(nt, UINT64_MAX);
+  const uint64_t* v = static_cast<const uint64_t*>(vals);
+  par_chunks(nnz, nt, [&](unsigned t, uint64_t lo, uint64_t hi) {
+    if (hi <= lo) return;
+    std::memcpy(out.colind.data() + lo, colind + lo, 4 * (hi - lo));
+    std::memcpy(out.vals.data() + lo, v + lo, 8 * (hi - lo));
+    for (uint64_t e = lo; e < hi; ++e)
+      if (colind[e] >= cols) {
+        bad[t] = e;
+        return;
+      }
+  });
+  const uint64_t e = *std::min_element(bad.begin(), bad.end());
+  if (e != UINT64_MAX) {
+    why = "column id " + std::to_string(colind[e]) + " out of range at element " + std::to_string(e);
+    return HIPSPMV_ERR_INVALID_MATRIX;
+  }
   return HIPSPMV_OK;
 }
 
@@ -110,10 +198,16 @@ bool vcache_eligible(const HostCSR& a, const VcGeom& g) {
   const uint32_t npad = part;  // the kernel clamps prefetches past its last panel
   if (npad + 1 > (uint32_t)kVcSegMax) return false;
   // panel order must equal each row's summation order: columns non-decreasing
-  for (uint32_t r = 0; r < a.rows; ++r)
-    for (uint32_t e = a.rowptr[r] + 1; e < a.rowptr[r + 1]; ++e)
-      if (a.colind[e] < a.colind[e - 1]) return false;
-  return true;
+  std::atomic<bool> sorted{true};
+  par_rows(a.rowptr.data(), a.rows, [&](unsigned, uint32_t r0, uint32_t r1) {
+    for (uint32_t r = r0; r < r1 && sorted.load(std::memory_order_relaxed); ++r)
+      for (uint32_t e = a.rowptr[r] + 1; e < a.rowptr[r + 1]; ++e)
+        if (a.colind[e] < a.colind[e - 1]) {
+          sorted = false;
+          return;
+        }
+  });
+  return sorted;
 }
 
 // Longest run of one row inside one panel of `panel` columns (columns sorted
@@ -121,17 +215,21 @@ bool vcache_eligible(const HostCSR& a, const VcGeom& g) {
 // sequentially in one lane, so AUTO keeps matrices with long runs (R-MAT hub
 // rows) off the vcache-family kernels.
 uint32_t vcache_max_run(const HostCSR& a, uint32_t panel) {
-  uint32_t best = 0;
-  for (uint32_t r = 0; r < a.rows; ++r) {
-    uint32_t run = 0, prev = UINT32_MAX;
-    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
-      const uint32_t p = a.colind[e] / panel;
-      run = p == prev ? run + 1 : 1;
-      prev = p;
-      best = std::max(best, run);
+  std::vector<uint32_t> best(plan_threads() + 1, 0);
+  par_rows(a.rowptr.data(), a.rows, [&](unsigned t, uint32_t r0, uint32_t r1) {
+    uint32_t b = 0;
+    for (uint32_t r = r0; r < r1; ++r) {
+      uint32_t run = 0, prev = UINT32_MAX;
+      for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+        const uint32_t p = a.colind[e] / panel;
+        run = p == prev ? run + 1 : 1;
+        prev = p;
+        b = std::max(b, run);
+      }
     }
-  }
-  return best;
+    best[t] = b;
+  });
+  return *std::max_element(best.begin(), best.end());
 }
 
 // Entries of row block b that fall into column panel p form segment (b, p),
@@ -147,43 +245,60 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
   out.seg.assign((size_t)nb * S * (npad + 1), 0);
   out.code.resize(a.nnz);
   out.vals.resize(a.nnz);
-  out.max_seg = 0;
-  out.n_cont = 0;
-  std::vector<uint32_t> cnt(np + 1);
-  uint32_t base = 0;
-  for (uint32_t b = 0; b < nb; ++b) {
-    const uint32_t r0 = b * R, r1 = std::min(a.rows, r0 + R);
-    std::fill(cnt.begin(), cnt.end(), 0);
-    for (uint32_t e = a.rowptr[r0]; e < a.rowptr[r1]; ++e) cnt[a.colind[e] / P + 1]++;
-    for (uint32_t p = 0; p < np; ++p) {
-      out.max_seg = std::max(out.max_seg, cnt[p + 1]);
-      cnt[p + 1] += cnt[p];
-    }
-    for (uint32_t h = 0; h < S; ++h) {
-      uint32_t* seg = &out.seg[((size_t)b * S + h) * (npad + 1)];
-      const uint32_t pfirst = vc_part_first(h, np, S), plast = vc_part_first(h + 1, np, S);
-      for (uint32_t i = 0; i <= npad; ++i) seg[i] = base + cnt[std::min(pfirst + i, plast)];
-    }
-    std::vector<uint32_t> cur(cnt.begin(), cnt.end() - 1);
-    for (uint32_t r = r0; r < r1; ++r) {
-      uint32_t prev_d = UINT32_MAX, prev_p = UINT32_MAX;
-      for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
-        const uint32_t c = a.colind[e], p = c / P;
-        const uint32_t d = base + cur[p]++;
-        uint32_t code = (c - p * P) | ((r - r0) << g.colbits);
-        if (p == prev_p && d == prev_d + 1) {  // same row, same segment, adjacent: extend the run
-          code |= kVcCont;
-          ++out.n_cont;
-          out.code[prev_d] |= kVcMore;
+  // row blocks are independent (block b's entries start at rowptr[b R]):
+  // contiguous block ranges per thread, entry-balanced
+  const unsigned nt = std::max(1u, std::min(plan_threads(), nb));
+  std::vector<uint32_t> bb(nt + 1, nb);
+  bb[0] = 0;
+  for (unsigned t = 1; t < nt; ++t) {
+    const uint32_t target = (uint32_t)((uint64_t)a.nnz * t / nt);
+    uint32_t b = (uint32_t)(std::lower_bound(a.rowptr.begin(), a.rowptr.end(), target) - a.rowptr.begin()) / R;
+    bb[t] = std::max(std::min(b, nb), bb[t - 1]);
+  }
+  std::vector<uint32_t> tmax(nt, 0);
+  std::vector<uint64_t> tcont(nt, 0);
+  std::vector<std::vector<uint32_t>> tcnt(nt, std::vector<uint32_t>(np + 1)), tcur(nt, std::vector<uint32_t>(np));
+  par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
+    for (uint64_t t = t0; t < t1; ++t) {
+      std::vector<uint32_t>& cnt = tcnt[t];
+      std::vector<uint32_t>& cur = tcur[t];
+      for (uint32_t b = bb[t]; b < bb[t + 1]; ++b) {
+        const uint32_t r0 = b * R, r1 = std::min(a.rows, r0 + R), base = a.rowptr[r0];
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (uint32_t e = a.rowptr[r0]; e < a.rowptr[r1]; ++e) cnt[a.colind[e] / P + 1]++;
+        for (uint32_t p = 0; p < np; ++p) {
+          tmax[t] = std::max(tmax[t], cnt[p + 1]);
+          cnt[p + 1] += cnt[p];
         }
-        out.code[d] = code;
-        out.vals[d] = a.vals[e];
-        prev_d = d;
-        prev_p = p;
+        for (uint32_t h = 0; h < S; ++h) {
+          uint32_t* seg = &out.seg[((size_t)b * S + h) * (npad + 1)];
+          const uint32_t pfirst = vc_part_first(h, np, S), plast = vc_part_first(h + 1, np, S);
+          for (uint32_t i = 0; i <= npad; ++i) seg[i] = base + cnt[std::min(pfirst + i, plast)];
+        }
+        std::copy(cnt.begin(), cnt.end() - 1, cur.begin());
+        for (uint32_t r = r0; r < r1; ++r) {
+          uint32_t prev_d = UINT32_MAX, prev_p = UINT32_MAX;
+          for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+            const uint32_t c = a.colind[e], p = c / P;
+            const uint32_t d = base + cur[p]++;
+            uint32_t code = (c - p * P) | ((r - r0) << g.colbits);
+            if (p == prev_p && d == prev_d + 1) {  // same row, same segment, adjacent: extend the run
+              code |= kVcCont;
+              ++tcont[t];
+              out.code[prev_d] |= kVcMore;
+            }
+            out.code[d] = code;
+            out.vals[d] = a.vals[e];
+            prev_d = d;
+            prev_p = p;
+          }
+        }
       }
     }
-    base += cnt[np];
-  }
+  });
+  out.max_seg = *std::max_element(tmax.begin(), tmax.end());
+  out.n_cont = 0;
+  for (uint64_t c : tcont) out.n_cont += c;
   out.max_run = vcache_max_run(a, P);
 }
 
@@ -204,81 +319,95 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
 bool build_vcache_lanes(const HostCSR& a, const VcGeom& g, uint32_t CT, VcacheLayout& out) {
   if (g.colbits != 12 || CT % 64 || CT == 0) return false;
   build_vcache(a, g, out);  // geometry, segment offsets and (row, col) order
-  const uint32_t P = (uint32_t)g.panel, S = (uint32_t)g.split, npad = out.npad;
-  std::vector<uint32_t> code(out.code.size());
-  std::vector<uint64_t> vals(out.vals.size());
-  std::vector<int64_t> pos;  // position of each entry of the segment (-1 unplaced)
-  std::vector<uint8_t> used;
-  for (uint32_t b = 0; b < out.nblocks; ++b)
-    for (uint32_t h = 0; h < S; ++h) {
-      const uint32_t* sg = &out.seg[((size_t)b * S + h) * (npad + 1)];
-      for (uint32_t i = 0; i < npad; ++i) {
-        const uint32_t s0 = sg[i], s1 = sg[i + 1], n = s1 - s0;
-        if (!n) continue;
-        if (n > 2 * CT) return false;
-        // runs of the segment: [start, len) in storage (row, col) order
-        std::vector<std::pair<uint32_t, uint32_t>> runs;
-        for (uint32_t e = s0; e < s1;) {
-          uint32_t f = e + 1;
-          while (f < s1 && (out.code[f] & kVcCont)) ++f;
-          runs.emplace_back(e, f - e);
-          e = f;
-        }
-        const uint32_t m = n > CT ? n - CT : 0;  // lanes with a second slot
-        pos.assign(n, -1);
-        used.assign(n, 0);
-        auto put = [&](uint32_t e, uint32_t p, uint32_t flags) {
-          pos[e - s0] = p;
-          used[p] = 1;
-          code[s0 + p] = (out.code[e] & ~(kVcCont | kVcMore)) | flags;
-          vals[s0 + p] = out.vals[e];
-        };
-        // 1. pairs lane-local on lanes [0, m)
-        uint32_t lane = 0;
-        for (auto& r : runs)
-          if (r.second == 2 && lane < m) {
-            put(r.first, lane, kVqLMore);
-            put(r.first + 1, CT + lane, kVcCont);
-            ++lane;
-            r.second = 0;  // placed
+  const uint32_t S = (uint32_t)g.split, npad = out.npad;
+  hvec<uint32_t> code(out.code.size());
+  hvec<uint64_t> vals(out.vals.size());
+  std::atomic<bool> ok{true};
+  const uint32_t units = out.nblocks * S;
+  // units are independent (disjoint segments): strided over the threads
+  const unsigned nt = std::max(1u, std::min(plan_threads(), units));
+  par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
+    std::vector<int64_t> pos;  // position of each entry of the segment (-1 unplaced)
+    std::vector<uint8_t> used;
+    std::vector<std::pair<uint32_t, uint32_t>> runs;
+    std::vector<size_t> multi;
+    for (uint64_t t = t0; t < t1; ++t)
+      for (uint32_t u = (uint32_t)t; u < units && ok.load(std::memory_order_relaxed); u += nt) {
+        const uint32_t* sg = &out.seg[(size_t)u * (npad + 1)];
+        for (uint32_t i = 0; i < npad; ++i) {
+          const uint32_t s0 = sg[i], s1 = sg[i + 1], n = s1 - s0;
+          if (!n) continue;
+          if (n > 2 * CT) {
+            ok = false;
+            return;
           }
-        // 2. other multi-entry runs: consecutive positions inside one slot row
-        // and one wave, from the first free position on
-        auto fits = [&](uint32_t p, uint32_t len) {
-          if (p + len > n) return false;
-          const uint32_t j = p / CT, c = p % CT;
-          if ((p + len - 1) / CT != j || c / 64 != (c + len - 1) / 64) return false;
-          for (uint32_t k = 0; k < len; ++k)
-            if (used[p + k]) return false;
-          return true;
-        };
-        // first fit, longest runs first (a run keeps its own entries in order)
-        std::vector<size_t> multi;
-        for (size_t i = 0; i < runs.size(); ++i)
-          if (runs[i].second >= 2) multi.push_back(i);
-        std::stable_sort(multi.begin(), multi.end(),
-                         [&](size_t u, size_t w) { return runs[u].second > runs[w].second; });
-        for (size_t i : multi) {
-          auto& r = runs[i];
+          // runs of the segment: [start, len) in storage (row, col) order
+          runs.clear();
+          for (uint32_t e = s0; e < s1;) {
+            uint32_t f = e + 1;
+            while (f < s1 && (out.code[f] & kVcCont)) ++f;
+            runs.emplace_back(e, f - e);
+            e = f;
+          }
+          const uint32_t m = n > CT ? n - CT : 0;  // lanes with a second slot
+          pos.assign(n, -1);
+          used.assign(n, 0);
+          auto put = [&](uint32_t e, uint32_t p, uint32_t flags) {
+            pos[e - s0] = p;
+            used[p] = 1;
+            code[s0 + p] = (out.code[e] & ~(kVcCont | kVcMore)) | flags;
+            vals[s0 + p] = out.vals[e];
+          };
+          // 1. pairs lane-local on lanes [0, m)
+          uint32_t lane = 0;
+          for (auto& r : runs)
+            if (r.second == 2 && lane < m) {
+              put(r.first, lane, kVqLMore);
+              put(r.first + 1, CT + lane, kVcCont);
+              ++lane;
+              r.second = 0;  // placed
+            }
+          // 2. other multi-entry runs: consecutive positions inside one slot row
+          // and one wave, from the first free position on
+          auto fits = [&](uint32_t p, uint32_t len) {
+            if (p + len > n) return false;
+            const uint32_t j = p / CT, c = p % CT;
+            if ((p + len - 1) / CT != j || c / 64 != (c + len - 1) / 64) return false;
+            for (uint32_t k = 0; k < len; ++k)
+              if (used[p + k]) return false;
+            return true;
+          };
+          // first fit, longest runs first (a run keeps its own entries in order)
+          multi.clear();
+          for (size_t k = 0; k < runs.size(); ++k)
+            if (runs[k].second >= 2) multi.push_back(k);
+          std::stable_sort(multi.begin(), multi.end(),
+                           [&](size_t v, size_t w) { return runs[v].second > runs[w].second; });
+          for (size_t k : multi) {
+            auto& r = runs[k];
+            uint32_t p = 0;
+            while (p < n && !fits(p, r.second)) ++p;
+            if (p >= n) {
+              ok = false;
+              return;
+            }
+            for (uint32_t q = 0; q < r.second; ++q)
+              put(r.first + q, p + q, (q ? kVcCont : 0u) | (q + 1 < r.second ? kVcMore : 0u));
+            r.second = 0;
+          }
+          // 3. single entries in order into the free positions
           uint32_t p = 0;
-          while (p < n && !fits(p, r.second)) ++p;
-          if (p >= n) return false;
-          for (uint32_t k = 0; k < r.second; ++k)
-            put(r.first + k, p + k, (k ? kVcCont : 0u) | (k + 1 < r.second ? kVcMore : 0u));
-          r.second = 0;
-        }
-        // 3. single entries in order into the free positions
-        uint32_t p = 0;
-        for (auto& r : runs) {
-          if (r.second != 1) continue;
-          while (used[p]) ++p;
-          put(r.first, p, 0u);
+          for (auto& r : runs) {
+            if (r.second != 1) continue;
+            while (used[p]) ++p;
+            put(r.first, p, 0u);
+          }
         }
       }
-    }
+  });
+  if (!ok) return false;
   out.code.swap(code);
   out.vals.swap(vals);
-  (void)P;
   return true;
 }
 
@@ -294,7 +423,7 @@ void build_sell(const HostCSR& a, SellLayout& out) {
   // the windows are independent: sorted in parallel, laid out at offsets
   // from a serial prefix sum, filled in parallel -- the same bytes as a
   // serial build
-  const unsigned nthr = std::max(1u, std::min({std::thread::hardware_concurrency(), 16u, nwin}));
+  const unsigned nthr = std::max(1u, std::min(plan_threads(), nwin));
   auto parallel = [&](auto&& fn) {
     std::vector<std::thread> ts;
     for (unsigned t = 0; t < nthr; ++t)
@@ -321,12 +450,19 @@ void build_sell(const HostCSR& a, SellLayout& out) {
       out.width[s] = len(order[w][(size_t)(s - first_slice[w]) * kSellRows]);  // longest first
       out.off[s + 1] = out.off[s] + (uint64_t)out.width[s] * kSellRows;
     }
-  out.col.assign(out.off[nslices], 0u);
-  out.vals.assign(out.off[nslices], 0u);
-  out.row.assign((size_t)nslices * kSellRows, kSellNoRow);
-  out.len.assign((size_t)nslices * kSellRows, 0u);
+  out.col.resize(out.off[nslices]);
+  out.vals.resize(out.off[nslices]);
+  out.row.resize((size_t)nslices * kSellRows);
+  out.len.resize((size_t)nslices * kSellRows);
   parallel([&](uint32_t w) {
     const auto& ord = order[w];
+    {  // the window's slices start as padding: column 0, value 0, no row
+      const uint32_t s0 = first_slice[w], s1 = first_slice[w + 1];
+      std::fill(out.col.begin() + out.off[s0], out.col.begin() + out.off[s1], 0u);
+      std::fill(out.vals.begin() + out.off[s0], out.vals.begin() + out.off[s1], 0u);
+      std::fill(out.row.begin() + (size_t)s0 * kSellRows, out.row.begin() + (size_t)s1 * kSellRows, kSellNoRow);
+      std::fill(out.len.begin() + (size_t)s0 * kSellRows, out.len.begin() + (size_t)s1 * kSellRows, 0u);
+    }
     for (size_t i = 0; i < ord.size(); ++i) {
       const uint32_t s = first_slice[w] + (uint32_t)(i / kSellRows), q = (uint32_t)(i % kSellRows);
       const uint32_t j = q / 64, l = q % 64;
@@ -372,83 +508,138 @@ void build_sell(const HostCSR& a, SellLayout& out) {
 // within a window, so a kernel walking them in order gathers from one window
 // of x at a time.  For each row, its segment ids in window order.
 uint64_t windowed_segments(const HostCSR& a, uint32_t log2w) {
-  uint64_t n = 0;
-  for (uint32_t r = 0; r < a.rows; ++r) {
-    uint32_t prev = UINT32_MAX;
-    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
-      const uint32_t w = a.colind[e] >> log2w;
-      n += w != prev;
-      prev = w;
+  std::vector<uint64_t> n(plan_threads() + 1, 0);
+  par_rows(a.rowptr.data(), a.rows, [&](unsigned t, uint32_t r0, uint32_t r1) {
+    uint64_t k = 0;
+    for (uint32_t r = r0; r < r1; ++r) {
+      uint32_t prev = UINT32_MAX;
+      for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e) {
+        const uint32_t w = a.colind[e] >> log2w;
+        k += w != prev;
+        prev = w;
+      }
     }
-  }
-  return n;
+    n[t] = k;
+  });
+  uint64_t s = 0;
+  for (uint64_t k : n) s += k;
+  return s;
 }
 
+// In parallel over entry-balanced row ranges (thread t: rows [rb[t], rb[t+1])):
+// a window's segments are numbered by rows ascending, so thread t's first
+// segment of window w follows every earlier thread's segments of w.
 void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t cap) {
   out = WinLayout{};
   out.log2w = log2w;
   const uint32_t nwin = (uint32_t)(((uint64_t)a.cols + (1ull << log2w) - 1) >> log2w);
-  // pass 1: segments per window (a row's windows change where its columns cross a boundary)
-  std::vector<uint64_t> wstart((size_t)nwin + 1, 0);
-  out.rowseg.assign((size_t)a.rows + 1, 0);
-  for (uint32_t r = 0; r < a.rows; ++r) {
-    uint32_t prev = UINT32_MAX, n = 0, run = 0;
-    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
-      const uint32_t w = a.colind[e] >> log2w;
-      if (w != prev || run == cap) {  // a new window, or the segment is full
-        wstart[w + 1]++;
-        ++n;
-        prev = w;
-        run = 0;
+  const unsigned nt = std::max(1u, std::min(plan_threads(), std::max(1u, a.rows / 64)));
+  const std::vector<uint32_t> rb = row_chunks(a.rowptr.data(), a.rows, nt);
+  auto each_thread = [&](auto&& fn) {
+    par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
+      for (uint64_t t = t0; t < t1; ++t) fn((unsigned)t, rb[t], rb[t + 1]);
+    });
+  };
+  // pass 1: segments per row and per (thread, window)
+  std::vector<std::vector<uint64_t>> wcnt(nt, std::vector<uint64_t>(nwin, 0));
+  out.rowseg.resize((size_t)a.rows + 1);
+  each_thread([&](unsigned t, uint32_t r0, uint32_t r1) {
+    for (uint32_t r = r0; r < r1; ++r) {
+      uint32_t prev = UINT32_MAX, n = 0, run = 0;
+      for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
+        const uint32_t w = a.colind[e] >> log2w;
+        if (w != prev || run == cap) {  // a new window, or the segment is full
+          wcnt[t][w]++;
+          ++n;
+          prev = w;
+          run = 0;
+        }
       }
+      out.rowseg[r + 1] = n;
     }
-    out.rowseg[r + 1] = out.rowseg[r] + n;
+  });
+  out.rowseg[0] = 0;
+  for (uint32_t r = 0; r < a.rows; ++r) out.rowseg[r + 1] += out.rowseg[r];
+  std::vector<uint64_t> wstart((size_t)nwin + 1, 0);
+  std::vector<std::vector<uint64_t>> cursor(nt, std::vector<uint64_t>(nwin));
+  for (uint32_t w = 0; w < nwin; ++w) {
+    uint64_t c = wstart[w];
+    for (unsigned t = 0; t < nt; ++t) {
+      cursor[t][w] = c;
+      c += wcnt[t][w];
+    }
+    wstart[w + 1] = c;
   }
-  for (uint32_t w = 0; w < nwin; ++w) wstart[w + 1] += wstart[w];
   out.nseg = (uint32_t)wstart[nwin];
   out.winseg.assign(wstart.begin(), wstart.end());
   // pass 2: each segment's id (rows ascend, so ids ascend within a window) and length
-  std::vector<uint64_t> cursor(wstart.begin(), wstart.end() - 1);
-  std::vector<uint32_t> len(out.nseg, 0);
+  hvec<uint32_t> len(out.nseg);
   out.segidx.resize(out.nseg);
-  for (uint32_t r = 0; r < a.rows; ++r) {
-    uint32_t prev = UINT32_MAX, k = out.rowseg[r], run = 0;
-    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
-      const uint32_t w = a.colind[e] >> log2w;
-      if (w != prev || run == cap) {
-        out.segidx[k++] = (uint32_t)cursor[w]++;
-        prev = w;
-        run = 0;
+  each_thread([&](unsigned t, uint32_t r0, uint32_t r1) {
+    for (uint32_t r = r0; r < r1; ++r) {
+      uint32_t prev = UINT32_MAX, k = out.rowseg[r], run = 0;
+      for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
+        const uint32_t w = a.colind[e] >> log2w;
+        if (w != prev || run == cap) {
+          out.segidx[k] = (uint32_t)cursor[t][w]++;
+          len[out.segidx[k]] = 0;
+          ++k;
+          prev = w;
+          run = 0;
+        }
+        len[out.segidx[k - 1]]++;
       }
-      len[out.segidx[k - 1]]++;
     }
-  }
+  });
   HostCSR& g = out.seg;
   g.rows = out.nseg;
   g.cols = a.cols;
   g.nnz = a.nnz;
-  g.rowptr.assign((size_t)out.nseg + 1, 0);
-  for (uint32_t i = 0; i < out.nseg; ++i) {
-    g.rowptr[i + 1] = g.rowptr[i] + len[i];
-    out.max_seg = std::max(out.max_seg, len[i]);
+  g.rowptr.resize((size_t)out.nseg + 1);
+  {  // rowptr = exclusive prefix of len, in two parallel passes over chunks
+    const unsigned nc = std::max(1u, std::min(plan_threads(), std::max(1u, out.nseg / 4096)));
+    std::vector<uint64_t> csum(nc + 1, 0);
+    std::vector<uint32_t> cmax(nc, 0);
+    par_chunks(out.nseg, nc, [&](unsigned c, uint64_t lo, uint64_t hi) {
+      uint64_t s = 0;
+      uint32_t m = 0;
+      for (uint64_t i = lo; i < hi; ++i) {
+        s += len[i];
+        m = std::max(m, len[i]);
+      }
+      csum[c + 1] = s;
+      cmax[c] = m;
+    });
+    for (unsigned c = 0; c < nc; ++c) csum[c + 1] += csum[c];
+    par_chunks(out.nseg, nc, [&](unsigned c, uint64_t lo, uint64_t hi) {
+      uint64_t s = csum[c];
+      for (uint64_t i = lo; i < hi; ++i) {
+        g.rowptr[i] = (uint32_t)s;
+        s += len[i];
+      }
+    });
+    g.rowptr[out.nseg] = a.nnz;
+    out.max_seg = *std::max_element(cmax.begin(), cmax.end());
   }
   // pass 3: copy each row's entries into its segments
   g.colind.resize(a.nnz);
   g.vals.resize(a.nnz);
-  for (uint32_t r = 0; r < a.rows; ++r) {
-    uint32_t prev = UINT32_MAX, k = out.rowseg[r], d = 0, run = 0;
-    for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
-      const uint32_t w = a.colind[e] >> log2w;
-      if (w != prev || run == cap) {
-        d = g.rowptr[out.segidx[k++]];
-        prev = w;
-        run = 0;
+  each_thread([&](unsigned, uint32_t r0, uint32_t r1) {
+    for (uint32_t r = r0; r < r1; ++r) {
+      uint32_t prev = UINT32_MAX, k = out.rowseg[r], d = 0, run = 0;
+      for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
+        const uint32_t w = a.colind[e] >> log2w;
+        if (w != prev || run == cap) {
+          d = g.rowptr[out.segidx[k++]];
+          prev = w;
+          run = 0;
+        }
+        g.colind[d] = a.colind[e];
+        g.vals[d] = a.vals[e];
+        ++d;
       }
-      g.colind[d] = a.colind[e];
-      g.vals[d] = a.vals[e];
-      ++d;
     }
-  }
+  });
 }
 
 // Greedy row groups: consecutive rows while the group stays within

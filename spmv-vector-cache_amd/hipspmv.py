@@ -406,7 +406,7 @@ def partition_row_counts(counts: np.ndarray, parts: int) -> np.ndarray:
     return bounds
 
 
-def rmat_expected_segments(counts: np.ndarray, scale: int, log2w: int = 17, a: float = 0.57, b: float = 0.19,
+def rmat_expected_segments(counts: np.ndarray, scale: int, log2w: int = 20, a: float = 0.57, b: float = 0.19,
                            c: float = 0.19, cap: int = 256) -> np.ndarray:
     """Expected wcsr segments per row of the R-MAT matrix gen_rmat_rows makes
     (DESIGN.md §6.11): a row of len edges, whose columns are independent given
@@ -458,9 +458,12 @@ def partition_row_weights(weights: np.ndarray, parts: int) -> np.ndarray:
 
 
 # wcsr shard cost per row in entry units: each segment and
-# each row costs this many entries' time (fit to the per-shard kernel times of
-# C5's 8-way partition, profiles/r04)
-WCSR_COST_SEGMENT, WCSR_COST_ROW = 0.52, 1.67
+# each row costs this many entries' time -- the least-squares fit (no
+# intercept) of the eight per-shard kernel times of C5 at the library's
+# window (kWcLog2Window = 20), round 4 (profiles/r04/logs/bench_c5_w20.log:
+# 7.08 us per M entries, 6.77 per M segments, 7.51 per M rows; residuals
+# within 3 us of 271-283)
+WCSR_COST_SEGMENT, WCSR_COST_ROW = 0.956, 1.061
 
 
 def c5_partition(scale: int, parts: int, edge_factor: int = 16, seed: int = 4, model: str = "cost"):

@@ -308,8 +308,8 @@ int main(int argc, char** argv) {
     HostCSR A;
     A.rows = A.cols = 1u << sc;
     A.nnz = (uint32_t)ci.size();
-    A.rowptr = rp;
-    A.colind = ci;
+    A.rowptr.assign(rp.begin(), rp.end());
+    A.colind.assign(ci.begin(), ci.end());
     A.vals.resize(A.nnz);
     std::memcpy(A.vals.data(), v.data(), 8ull * A.nnz);
     cases.push_back({"rmat s" + std::to_string(sc), std::move(A)});

@@ -1,0 +1,91 @@
+// setup_probe: host-side phases of hipspmv_create_csr on a BASELINE matrix,
+// timed on the CPU (no HIP: the device uploads are not in it) -- where the
+// create time of full C4 goes.
+//
+//   setup_probe c4|c3|c5 [threads]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../host/Synthetic.h"
+#include "hipspmv_internal.h"
+
+using namespace hipspmv;
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+  const std::string which = argc > 1 ? argv[1] : "c4";
+  std::vector<uint32_t> rowptr, colind;
+  std::vector<double> vals;
+  uint32_t n = 0;
+  double t = now_s();
+  if (which == "c5") {
+    n = 1u << 24;
+    genRmatCSR(24, 16, 4, 0.57, 0.19, 0.19, rowptr, colind, vals);
+  } else {
+    n = which == "c3" ? 1u << 20 : 1u << 24;
+    const uint64_t nnz = (uint64_t)n * 32;
+    rowptr.resize(n + 1);
+    colind.resize(nnz);
+    vals.resize(nnz);
+    genStripeCSR(0, n, n, 32, 1, 2, rowptr.data(), colind.data(), vals.data());
+  }
+  const uint32_t nnz = rowptr[n];
+  std::printf("%s: %u rows, %u nnz, generated in %.2f s\n", which.c_str(), n, nnz, now_s() - t);
+  auto phase = [](const char* name, double t0) { std::printf("  %-34s %7.3f s\n", name, now_s() - t0); };
+  HostCSR a;
+  std::string why;
+  t = now_s();
+  copy_csr(rowptr.data(), colind.data(), vals.data(), n, n, nnz, a, why);
+  phase("copy_csr", t);
+  t = now_s();
+  uint32_t maxlen = 0;
+  for (uint32_t r = 0; r < a.rows; ++r) maxlen = std::max(maxlen, a.rowptr[r + 1] - a.rowptr[r]);
+  phase("row lengths", t);
+  t = now_s();
+  std::vector<uint32_t> groups;
+  build_row_groups(a, groups);
+  phase("build_row_groups", t);
+  const VcGeom geoms[] = {kVcOrdered, kVcSplit, kVcQuad, kWgWindow};
+  const char* gname[] = {"vcache_eligible ordered", "vcache_eligible split", "vcache_eligible quad",
+                         "vcache_eligible wgather"};
+  bool wg = false;
+  for (int i = 0; i < 4; ++i) {
+    t = now_s();
+    const bool e = vcache_eligible(a, geoms[i]);
+    if (i == 3) wg = e;
+    phase(gname[i], t);
+  }
+  if (wg) {
+    t = now_s();
+    (void)vcache_max_run(a, (uint32_t)kWgWindow.panel);
+    phase("vcache_max_run wgather", t);
+  }
+  t = now_s();
+  const uint64_t segs = windowed_segments(a, kWcLog2Window);
+  phase("windowed_segments", t);
+  std::printf("  (segments %llu)\n", (unsigned long long)segs);
+  t = now_s();
+  SellLayout S;
+  build_sell(a, S);
+  phase("build_sell", t);
+  if (wg) {
+    t = now_s();
+    VcacheLayout W;
+    build_vcache(a, kWgWindow, W);
+    phase("build_vcache wgather", t);
+  }
+  if (which == "c5") {
+    t = now_s();
+    WinLayout L;
+    build_windowed(a, kWcLog2Window, L, (uint32_t)kCvGroupNnz);
+    phase("build_windowed", t);
+  }
+  return 0;
+}

@@ -45,6 +45,9 @@ template <typename T>
 struct Buf {  // bounds-checked global array
   const char* name;
   std::vector<T> v;
+  Buf(const char* n, std::vector<T> src) : name(n), v(std::move(src)) {}
+  template <class A>
+  Buf(const char* n, const std::vector<T, A>& src) : name(n), v(src.begin(), src.end()) {}
   T get(size_t i) const {
     CHECK(i < v.size(), "%s[%zu] read, size %zu", name, i, v.size());
     return i < v.size() ? v[i] : T();
@@ -425,8 +428,8 @@ int main(int argc, char** argv) {
     HostCSR A;
     A.rows = A.cols = 1u << 14;
     A.nnz = (uint32_t)ci.size();
-    A.rowptr = rp;
-    A.colind = ci;
+    A.rowptr.assign(rp.begin(), rp.end());
+    A.colind.assign(ci.begin(), ci.end());
     A.vals.resize(A.nnz);
     std::memcpy(A.vals.data(), v.data(), 8ull * A.nnz);
     cases.push_back({"rmat s14", std::move(A)});

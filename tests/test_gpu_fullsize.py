@@ -93,7 +93,8 @@ def c5(c5_csr):
 
 
 @pytest.mark.parametrize("kernel,mode", [("auto", hs.MODE_ORDERED), ("auto", hs.MODE_FAST),
-                                         ("sell", hs.MODE_ORDERED), ("sell", hs.MODE_FAST)])
+                                         ("sell", hs.MODE_ORDERED), ("sell", hs.MODE_FAST),
+                                         ("wcsr", hs.MODE_FAST)])
 @pytest.mark.parametrize("which", ["c4", "c5"])
 def test_full_size_sampled_rows(request, which, kernel, mode):
     h, x, rows, want, absprod, lens = request.getfixturevalue(which)
@@ -113,8 +114,10 @@ U64_KERNELS = {  # (kernel, mode); the C3 list includes the vector-cache kernels
                ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
     # wide x (16 M columns, no vector-cache layout): every generic kernel by name
     "c4_csr": [("csr_lane", hs.MODE_ORDERED), ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST),
-               ("wgather", hs.MODE_ORDERED)],
-    "c5_csr": [("csr_lane", hs.MODE_ORDERED), ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST)],
+               ("wgather", hs.MODE_ORDERED), ("wcsr", hs.MODE_FAST)],
+    # wcsr: AUTO's FAST kernel for C5 (and its shards), by name on both
+    "c5_csr": [("csr_lane", hs.MODE_ORDERED), ("csr_vector", hs.MODE_FAST), ("sell", hs.MODE_FAST),
+               ("wcsr", hs.MODE_FAST)],
 }
 
 

@@ -69,6 +69,31 @@ def test_fixtures(gpu, name, kernel, beta):
         _check(f"{name}[{xname}]", rows, cols, colptr, rowind, vals, x, kernel, beta, mode)
 
 
+def _tile_columns(cols, colptr, rowind, vals, k):
+    """[A A ... A] (k copies side by side): the reference fixture widened until
+    the column-part geometries apply, rows and their column order intact"""
+    nnz = rowind.size
+    cp = np.concatenate([colptr[:-1].astype(np.int64) + j * nnz for j in range(k)] + [[k * nnz]]).astype(np.uint32)
+    return k * cols, cp, np.tile(rowind, k), np.tile(vals, k)
+
+
+@pytest.mark.parametrize("name", ["circuit204", "circuit204-uint64"])
+@pytest.mark.parametrize("kernel", ["vcache_split", "vcache_split4"])
+@pytest.mark.parametrize("beta", [0, 1])
+def test_tiled_fixture_column_parts(gpu, name, kernel, beta):
+    # the headline FAST kernels on a reference-held matrix: circuit204 tiled to
+    # 12 x 1020 = 12,240 columns (three / four column parts) against the oracle
+    rows, cols, colptr, rowind, vals = fx.load(name)
+    k = -(-12001 // cols)
+    tcols, tcp, tri, tv = _tile_columns(cols, colptr, rowind, vals, k)
+    h = hs.Handle.from_csc(tcp, tri, tv, rows, tcols)
+    key = "vcache_split_eligible" if kernel == "vcache_split" else "vcache_split4_eligible"
+    assert h.stat(key), (name, kernel, tcols)
+    h.close()
+    for xname, x in fx.x_variants(name, tcols).items():
+        _, y = _check(f"{name}x{k}[{xname}]", rows, tcols, tcp, tri, tv, x, kernel, beta, hs.MODE_FAST)
+
+
 @pytest.mark.parametrize("name", fx.F64_FIXTURES)
 def test_reference_golden_bin_exact(gpu, name):
     # HIPSpMV ordered == reference golden.bin (A*1), the reference's own compareGolden
@@ -144,7 +169,7 @@ def test_random_duplicates(gpu, kernel):
 
 @pytest.mark.parametrize("dtype", [np.float64, np.uint64])
 def test_wcsr_wide_windows(gpu, dtype):
-    # wcsr cuts rows at 2^16-column windows: a wide, skewed matrix (rows spanning many windows, a
+    # wcsr cuts rows at 2^20-column windows: a wide, skewed matrix (rows spanning every window, a
     # full-width row, empty rows, an odd column count) -- FAST within the bound and identical bits
     # on every run; u64 exact; the segment count matches a CPU recount
     rng = np.random.default_rng(21)
