@@ -121,6 +121,9 @@ struct hipspmv_handle {
   // one launch's blocks are all resident at once (2 per CU), so they walk
   // the x windows together and the gathered window stays in L2
   uint32_t wgather_chunk = kWgChunk;
+  // env HIPSPMV_WGATHER_SORT=0 at create: the wgather layout keeps (row, column) order in
+  // each segment instead of sorting row runs by x line (probe)
+  bool wgather_sort = true;
   // option "vcache_nt": row blocks b >= vcache_nt load their entries
   // non-temporally; -1 default: every block for the split
   // geometry, the second half of the blocks for the ordered one
@@ -212,6 +215,7 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
     if (!build_vcache_lanes(a, g, lanes, L)) return HIPSPMV_ERR_UNSUPPORTED;
   } else {
     build_vcache(a, g, L);
+    if (k == 3 && h->wgather_sort) sort_segments_by_line(L);  // k_wgather: gathers of one line side by side
   }
   v.split = g.split;
   v.rows_per_block = L.rows_per_block;
@@ -586,6 +590,7 @@ static int create_common(uint32_t rows, uint32_t cols, uint32_t nnz, int dtype, 
   hipspmv_t* h = new hipspmv_t;
   h->device = device;
   h->dtype = dtype;
+  if (const char* e = std::getenv("HIPSPMV_WGATHER_SORT")) h->wgather_sort = std::strcmp(e, "0") != 0;
   h->rows = rows;
   h->cols = cols;
   h->nnz = nnz;

@@ -37,7 +37,7 @@ constexpr VcGeom kVcSplit4{16384, 1984, 4};
 // (1 MiB of x, L2-resident) with x gathered from global memory instead of
 // staged in LDS -- for matrices whose x is too wide for LDS streaming to pay
 // (C4/C5: 16M columns).  y block in LDS (<= 8192 rows, 13 bits), ORDERED.
-constexpr VcGeom kWgWindow{8192, 1 << 17, 1, 17};
+constexpr VcGeom kWgWindow{16384, 1 << 16, 1, 16};
 // Row blocks per k_wgather launch (option "wgather_chunk"): one per CU.  A
 // matrix with more blocks than that (full C4: 2048 blocks of 8192 rows) runs
 // in several launches, so every launch's workgroups are resident together
@@ -237,6 +237,8 @@ bool vcache_eligible(const HostCSR& a, const VcGeom& g);
 void vcache_geometry(uint32_t rows, uint32_t cols, const VcGeom& g, VcacheLayout& out);
 uint32_t vcache_max_run(const HostCSR& a, uint32_t panel);
 void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out);
+// k_wgather's segment order: row runs by the x line of their first column (plan.cpp)
+void sort_segments_by_line(VcacheLayout& L);
 // k_vquad's placement of the same entries for CT compute lanes (plan.cpp)
 bool build_vcache_lanes(const HostCSR& a, const VcGeom& g, uint32_t CT, VcacheLayout& out);
 void build_sell(const HostCSR& a, SellLayout& out);

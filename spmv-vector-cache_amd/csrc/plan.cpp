@@ -302,6 +302,56 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
   out.max_run = vcache_max_run(a, P);
 }
 
+// k_wgather's order inside each segment: row runs (a run is one row's entries
+// in this window, consecutive, in column order) stably sorted by the 128-byte
+// x line of their first column, so lanes of a wave that gather from one line
+// sit next to each other and the gather instruction merges them into one L2
+// request.  Rows stay one run per segment and keep their column order inside
+// it: ORDERED sums are unchanged.
+void sort_segments_by_line(VcacheLayout& L) {
+  const uint32_t colmask = (1u << L.geom.colbits) - 1, units = L.nblocks * (uint32_t)L.geom.split;
+  const uint32_t npad = L.npad;
+  const unsigned nt = std::max(1u, std::min(plan_threads(), units));
+  par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
+    std::vector<uint64_t> runs;  // line << 40 | start << 20 ... packed below
+    std::vector<uint32_t> code;
+    std::vector<uint64_t> vals;
+    for (uint64_t t = t0; t < t1; ++t)
+      for (uint32_t u = (uint32_t)t; u < units; u += nt) {
+        const uint32_t* sg = &L.seg[(size_t)u * (npad + 1)];
+        for (uint32_t i = 0; i < npad; ++i) {
+          const uint32_t s0 = sg[i], s1 = sg[i + 1], n = s1 - s0;
+          if (n < 2) continue;
+          // (line, position of the run's first entry); positions are < 2^32 - s0
+          std::vector<std::pair<uint32_t, uint32_t>> rk;
+          rk.reserve(n);
+          for (uint32_t e = s0; e < s1;) {
+            rk.emplace_back((L.code[e] & colmask) >> 4, e);
+            uint32_t f = e + 1;
+            while (f < s1 && (L.code[f] & kVcCont)) ++f;
+            e = f;
+          }
+          std::stable_sort(rk.begin(), rk.end(),
+                           [](const std::pair<uint32_t, uint32_t>& p, const std::pair<uint32_t, uint32_t>& q) {
+                             return p.first < q.first;
+                           });
+          code.assign(L.code.begin() + s0, L.code.begin() + s1);
+          vals.assign(L.vals.begin() + s0, L.vals.begin() + s1);
+          uint32_t d = s0;
+          for (const auto& r : rk) {
+            uint32_t e = r.second;
+            do {
+              L.code[d] = code[e - s0];
+              L.vals[d] = vals[e - s0];
+              ++d;
+              ++e;
+            } while (e < s1 && (code[e - s0] & kVcCont));
+          }
+        }
+      }
+  });
+}
+
 // The k_vquad form of the vcache layout: the same blocks,
 // panels and segment offsets, entries of a segment placed for a kernel whose
 // step gives lane ct of the CT compute lanes the positions ct and CT + ct

@@ -249,19 +249,19 @@ static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
   for (uint32_t b0 = 0; b0 < a.nblocks; b0 += chunk) {
     const uint32_t n = a.nblocks - b0 < chunk ? a.nblocks - b0 : chunk;
     if (a.xlane >= 2 && a.max_seg <= 2u * kVcThreads)
-      hipLaunchKernelGGL((k_wgather_pipe<T, 17, 4, 2>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
+      hipLaunchKernelGGL((k_wgather_pipe<T, kWgWindow.colbits, 4, 2>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
                          (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
                          a.npanels, a.npad, a.last, a.beta, b0);
     else if (a.xlane >= 2 && a.max_seg <= 4u * kVcThreads)
-      hipLaunchKernelGGL((k_wgather_pipe<T, 17, 4, 4>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
+      hipLaunchKernelGGL((k_wgather_pipe<T, kWgWindow.colbits, 4, 4>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
                          (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
                          a.npanels, a.npad, a.last, a.beta, b0);
     else if (a.nt_from == 0)
-      hipLaunchKernelGGL((k_wgather<T, 17, 4, 2, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
+      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 4, 2, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
                          (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
                          a.npanels, a.npad, a.last, a.beta, b0);
     else
-      hipLaunchKernelGGL((k_wgather<T, 17, 4, 2>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
+      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 4, 2>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
                          (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
                          a.npanels, a.npad, a.last, a.beta, b0);
     const hipError_t e = hipGetLastError();

@@ -597,6 +597,7 @@ int main(int argc, char** argv) {
       }
       VcacheLayout L;
       build_vcache(cs.A, g, L);
+      if (c.LD == 2) sort_segments_by_line(L);  // the wgather layout as hipspmv_create builds it
       // the launcher's guard (vcache_grid_ok) accepts every product layout
       if (!vcache_grid_ok(cs.A.rows, cs.A.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels, L.npad,
                           L.geom.panel, c.SPLIT, g)) {
