@@ -71,7 +71,7 @@ extern "C" {
                                           chosen by AUTO, layout built only
                                           when HIPSPMV_EXPERIMENTAL=1 at create */
 #define HIPSPMV_KERNEL_WGATHER 6 /* y block in LDS, x gathered from global in
-                                    2^17-column windows (wide x: C4/C5);
+                                    2^16-column windows (wide x: C4/C5);
                                     ordered; experimental like VCACHE_SPLIT4 */
 #define HIPSPMV_KERNEL_WCSR 8 /* csr_vector over the rows cut at 2^20-column
                                  windows (window-major), then each row's window

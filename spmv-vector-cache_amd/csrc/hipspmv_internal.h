@@ -28,16 +28,23 @@ namespace hipspmv {
 struct VcGeom {
   int rows, panel, split;
   int colbits = 16;  // entry code: col_local | row_local << colbits | CONT | MORE
+  int segmax = 256;  // segment offsets per unit the kernel's LDS table holds (npad + 1 <= segmax)
 };
 constexpr VcGeom kVcOrdered{4096, 8128, 1};
 constexpr VcGeom kVcSplit{12352, 4000, 3};
 //   split4 : 16384 rows, 4 parts: 131072 + 2*1984*8 + 1024 (experimental)
 constexpr VcGeom kVcSplit4{16384, 1984, 4};
-// ---- k_wgather: the same segment layout over column WINDOWS of 2^17 columns
-// (1 MiB of x, L2-resident) with x gathered from global memory instead of
+// ---- k_wgather: the same segment layout over column WINDOWS of 2^16 columns
+// (512 KiB of x, L2-resident) with x gathered from global memory instead of
 // staged in LDS -- for matrices whose x is too wide for LDS streaming to pay
-// (C4/C5: 16M columns).  y block in LDS (<= 8192 rows, 13 bits), ORDERED.
-constexpr VcGeom kWgWindow{16384, 1 << 16, 1, 16};
+// (C4/C5: 16M columns).  y block in LDS (<= 16384 rows, 14 bits), ORDERED.
+// Round 4: 16384-row blocks over 2^16-column windows instead of 8192 over
+// 2^17 -- twice the entries per x line in a segment, so more gathers of a
+// wave share a line once the segment is sorted by line (sort_segments_by_line):
+// full C4 3417 us (8192 rows) -> 3296 (sorted) -> 2870 (16384 rows, sorted),
+// profiles/r04/logs/sweep_c4_*.log.  512 windows of 2^16 at 2^24 columns: the
+// kernel's segment table holds 512 offsets (segmax).
+constexpr VcGeom kWgWindow{16384, 1 << 16, 1, 16, 512};
 // Row blocks per k_wgather launch (option "wgather_chunk"): one per CU.  A
 // matrix with more blocks than that (full C4: 2048 blocks of 8192 rows) runs
 // in several launches, so every launch's workgroups are resident together
@@ -152,7 +159,7 @@ inline bool vcache_grid_ok(uint32_t rows, uint32_t cols, uint32_t rows_per_block
   if (npanels == 0 || (uint64_t)npanels * g.panel < cols) return false;
   if (npanels < (uint32_t)split) return false;                         // every part owns a panel
   if (part_panels != (npanels + split - 1) / split) return false;      // the largest part
-  return npad + 1 <= (uint32_t)kVcSegMax && npad >= part_panels;
+  return npad + 1 <= (uint32_t)g.segmax && npad >= part_panels;
 }
 
 // Host arrays the size of the matrix: resize() leaves new elements

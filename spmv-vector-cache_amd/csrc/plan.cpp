@@ -196,7 +196,7 @@ bool vcache_eligible(const HostCSR& a, const VcGeom& g) {
   if (np < (uint32_t)g.split) return false;  // every column part owns >= 1 panel (vc_part_first)
   const uint32_t part = (np + g.split - 1) / g.split;
   const uint32_t npad = part;  // the kernel clamps prefetches past its last panel
-  if (npad + 1 > (uint32_t)kVcSegMax) return false;
+  if (npad + 1 > (uint32_t)g.segmax) return false;
   // panel order must equal each row's summation order: columns non-decreasing
   std::atomic<bool> sorted{true};
   par_rows(a.rowptr.data(), a.rows, [&](unsigned, uint32_t r0, uint32_t r1) {

@@ -1,13 +1,14 @@
-// k_wgather: windowed-gather SpMV for wide x (experimental).
+// k_wgather: windowed-gather SpMV for wide x.
 //
 // When x is too wide for the LDS vector cache to pay (C4/C5: 16M columns,
 // x = 128 MB; every row block would have to stream all of it), x stays in
 // global memory and is gathered per nonzero -- but in column WINDOWS: the
-// entries of row block b that fall into window w (2^CB columns, 1 MiB of x)
+// entries of row block b that fall into window w (2^CB columns, 512 KiB of x)
 // form segment (b, w) of the vcache layout (csrc/plan.cpp build_vcache with
-// kWgWindow), and every workgroup walks the windows in the same order, so the
-// whole chip gathers from one L2-resident window at a time instead of from
-// all 128 MB.  The row block's y accumulators live in LDS as in k_vcache;
+// kWgWindow; row runs sorted by x line, sort_segments_by_line, so the lanes
+// of a gather that hit one line are neighbours), and every workgroup walks
+// the windows in the same order, so the whole chip gathers from one
+// L2-resident window at a time instead of from all 128 MB.  The row block's y accumulators live in LDS as in k_vcache;
 // within a window each row is one run processed by one lane in column order,
 // windows are separated by a barrier, so every row is summed in ascending
 // column order from y_in or +0.0: ORDERED, bit-identical to SoftwareSpMV.
@@ -34,7 +35,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
   constexpr uint32_t W = 1u << CB, CMASK = W - 1, RMASK = (1u << (30 - CB)) - 1;
   constexpr int VR = 1 << (30 - CB);
   __shared__ T ylds[VR];
-  __shared__ uint32_t segl[kVcSegMax];
+  __shared__ uint32_t segl[kWgWindow.segmax];
   const int t = threadIdx.x;
   const uint32_t b = b0 + blockIdx.x;  // this launch's blocks start at b0 (launch chunks, kWgChunk)
   const uint32_t r0 = b * rows_per_block;
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather_pipe(const uint32_t* __r
   constexpr int VR = 1 << (30 - CB);
   static_assert(DE >= 2 && DE % 2 == 0, "ring depth: even, the gather buffer alternates");
   __shared__ T ylds[VR];
-  __shared__ uint32_t segl[kVcSegMax];
+  __shared__ uint32_t segl[kWgWindow.segmax];
   const int t = threadIdx.x;
   const uint32_t lw = t & 63;
   const uint32_t b = b0 + blockIdx.x;

@@ -112,8 +112,8 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
     const uint32_t p0 = vc_part_first(h, npanels, c.SPLIT);
     CHECK(p0 < npanels, "p0 %u >= npanels %u", p0, npanels);
     const uint32_t npu = vc_part_first(h + 1, npanels, c.SPLIT) - p0;
-    CHECK(npu >= 1 && npu <= part && npad + 1 <= (uint32_t)kVcSegMax, "npu %u part %u npad %u", npu, part, npad);
-    std::vector<uint32_t> segl(kVcSegMax, 0xDEADBEEF);
+    CHECK(npu >= 1 && npu <= part && npad + 1 <= (uint32_t)L.geom.segmax, "npu %u part %u npad %u", npu, part, npad);
+    std::vector<uint32_t> segl(L.geom.segmax, 0xDEADBEEF);
     for (uint32_t t = 0; t <= npad; ++t) segl[t] = seg.get(((size_t)b * c.SPLIT + h) * (npad + 1) + t);
     std::vector<double> ylds(c.VR, NAN);
     for (uint32_t i = 0; i < nr; ++i) ylds[i] = (beta && h == 0) ? Yin.get(r0 + i) : 0.0;
@@ -590,7 +590,8 @@ int main(int argc, char** argv) {
     for (uint32_t i = 0; i < cs.A.cols; ++i) x[i] = uniform11(splitmix64_at(3, i));
     for (uint32_t i = 0; i < cs.A.rows; ++i) yin[i] = uniform11(splitmix64_at(5, i));
     for (const Cfg& c : cfgs) {
-      const VcGeom g{c.VR, c.VP, c.SPLIT, c.CB};
+      VcGeom g{c.VR, c.VP, c.SPLIT, c.CB};
+      if (c.LD == 2) g.segmax = kWgWindow.segmax;  // k_wgather's segment table
       if (!vcache_eligible(cs.A, g)) {
         std::printf("%-28s split=%d ld=%d: not eligible\n", cs.name.c_str(), c.SPLIT, c.LD);
         continue;

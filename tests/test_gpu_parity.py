@@ -923,7 +923,7 @@ def test_auto_layouts_built_at_create(gpu):
 def test_wgather_chunked_launches_bit_identical(gpu):
     # k_wgather runs its row blocks in launches of `wgather_chunk` (kWgChunk = 256: one per CU);
     # any chunking gives the single-launch bits, ORDERED == the oracle
-    rows, cols = 1 << 14, 1 << 21
+    rows, cols = 1 << 17, 1 << 21  # 8 row blocks of 16384
     rowptr, colind, vals = hs.gen_stripe_csr(0, rows, cols, 32)
     h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
     assert h.kernel_name(hs.MODE_ORDERED) == "wgather" and h.stat("wgather_chunk") == 256
@@ -931,7 +931,42 @@ def test_wgather_chunked_launches_bit_identical(gpu):
     colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
     y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=rows)
     outs = []
-    for chunk in (0, 256, 7, 1):
+    for chunk in (0, 256, 3, 1):
         h.set_option("wgather_chunk", chunk)
         outs.append(h.exec(x, beta=0, mode=hs.MODE_ORDERED).tobytes())
     assert all(o == y_ref.tobytes() for o in outs)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.uint64])
+def test_wgather_runs_and_line_order(gpu, dtype):
+    # the wgather layout sorts each segment's row runs by x line: rows with several entries in
+    # one 2^16-column window (runs), empty rows, a ragged last block -- ORDERED bit-exact vs
+    # the oracle for beta 0 and 1, u64 exact
+    rng = np.random.default_rng(5)
+    rows, cols = 40001, (1 << 21) + 5
+    per_row = []
+    for r in range(rows):
+        n = int(rng.integers(0, 12))
+        w = rng.integers(0, cols >> 16, 3)  # entries clustered in up to three windows
+        c = (w[rng.integers(0, 3, n)] << 16) + rng.integers(0, 1 << 16, n)
+        per_row.append(np.unique(np.minimum(c, cols - 1)))
+    lens = np.array([c.size for c in per_row], np.int64)
+    rowptr = np.zeros(rows + 1, np.uint32)
+    rowptr[1:] = np.cumsum(lens)
+    colind = np.concatenate(per_row).astype(np.uint32)
+    if dtype == np.float64:
+        vals, x = rng.uniform(-1, 1, colind.size), rng.uniform(-1, 1, cols)
+        y0 = rng.uniform(-1, 1, rows)
+    else:
+        vals = rng.integers(0, 2**64, colind.size, dtype=np.uint64)
+        x = rng.integers(0, 2**64, cols, dtype=np.uint64)
+        y0 = rng.integers(0, 2**64, rows, dtype=np.uint64)
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+    assert h.stat("wgather_eligible")
+    h.set_kernel("wgather")
+    colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+    for beta in (0, 1):
+        y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else None), rows=rows)
+        y = h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_ORDERED)
+        assert y.tobytes() == y_ref.tobytes(), (dtype, beta)
+    h.close()
