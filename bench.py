@@ -512,6 +512,7 @@ def run_strong(a, dist, dev, local: int, rank: int, world: int, stream) -> dict:
                               sample_rows(rowptr, a.parity_rows, seed=rank))
     parities = gather_objects(dist, parity, world)
     setup_ns = h.stat("setup_ns")
+    phases = {k: h.stat(f"setup_{k}_ns") for k in ("csr", "upload", "scan", "layouts")}
     h.close()
     del xd, yd
     torch.cuda.empty_cache()
@@ -524,7 +525,7 @@ def run_strong(a, dist, dev, local: int, rank: int, world: int, stream) -> dict:
             "roofline_frac_rank0": round(alg / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "alg_bytes_rank0": alg, "x_bcast_us": None if bcast_us is None else round(bcast_us, 2),
             "rank_parity": parities, "gen_s": round(gen_s, 3), "setup_s": round(setup_s, 3),
-            "setup_ns_lib": setup_ns}
+            "setup_ns_lib": setup_ns, "setup_phases_ns": phases}
 
 
 def run_c5_shards(a, dev, stream) -> dict:

@@ -147,7 +147,9 @@ int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void 
 
 /* Replaces HardwareSpMV::statInt/statKeys (HardwareSpMV.cpp:41-61,
  * HardwareSpMVNewCache.cpp:130-204).  Keys: "rows" "cols" "nz" "dtype"
- * "device" "kernel" (last kernel run) "setup_ns" "kernel_ns" (last timed
+ * "device" "kernel" (last kernel run) "setup_ns" "create_ns" "layout_ns"
+ * "setup_csr_ns" "setup_upload_ns" "setup_scan_ns" "setup_layouts_ns"
+ * (create's phases) "kernel_ns" (last timed
  * exec) "h2d_ns" "d2h_ns" "alg_bytes" (beta 0) "alg_bytes_beta1" "flops"
  * "device_bytes" "vcache_blocks" "vcache_panels" "vcache_rows_per_block"
  * "vcache_max_segment" "vcache_eligible" "vcache_split_eligible"

@@ -139,6 +139,9 @@ struct hipspmv_handle {
   // layout_ns: layouts built later, on first selection by name (also counted
   // in the "setup_ns" statistic, so the plugin's setupTimeUs covers them)
   uint64_t setup_ns = 0, layout_ns = 0, kernel_ns = 0, h2d_ns = 0, d2h_ns = 0, execs = 0, device_bytes = 0;
+  // create's phases: host CSR (copy or transpose, validation), CSR upload,
+  // scans (eligibility, run and segment counts), layouts (build + upload)
+  uint64_t setup_csr_ns = 0, setup_upload_ns = 0, setup_scan_ns = 0, setup_layouts_ns = 0;
   int auto_fallback = 0;  // AUTO layouts that could not be built (device OOM): the generic kernel runs instead
   int last_beta = 0;
   uint32_t max_row_len = 0, empty_rows = 0;
@@ -500,6 +503,7 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
     h->empty_rows += len == 0;
   }
   int st;
+  uint64_t t0 = now_ns();
   if ((st = dev_upload(&h->d_rowptr, a.rowptr.data(), a.rowptr.size(), h->device_bytes))) return st;
   if ((st = dev_upload(&h->d_colind, a.colind.data(), a.colind.size(), h->device_bytes))) return st;
   if ((st = dev_upload(&h->d_vals, a.vals.data(), a.vals.size(), h->device_bytes))) return st;
@@ -507,6 +511,8 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   build_row_groups(a, groups);
   h->ngroups = (uint32_t)groups.size() - 1;
   if ((st = dev_upload(&h->d_groups, groups.data(), groups.size(), h->device_bytes))) return st;
+  h->setup_upload_ns = now_ns() - t0;
+  t0 = now_ns();
   // the experimental split4 layout is built only on request
   // (HIPSPMV_EXPERIMENTAL=1): each costs another copy of the entries
   const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
@@ -529,16 +535,19 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
     const uint32_t zero = 0;
     if ((st = dev_upload(&h->d_status, &zero, 1, h->device_bytes))) return st;
   }
-  if (vcache_eligible(a, kVcSplit) && (st = upload_vc(h, 1, a, kVcSplit))) return st;
-  // the four-part layout (k_vquad) wherever eligible and every segment fits
-  // the kernel's register window (k_vquad has no slow path for longer ones)
-  if (vcache_eligible(a, kVcQuad)) {
-    st = upload_vc(h, 2, a, kVcQuad, kVqLanes);
-    if (st && st != HIPSPMV_ERR_UNSUPPORTED) return st;
-  }
+  const bool split_ok = vcache_eligible(a, kVcSplit), quad_ok = vcache_eligible(a, kVcQuad);
   h->wg_eligible = vcache_eligible(a, kWgWindow);
   if (h->wg_eligible) h->wg_max_run = vcache_max_run(a, (uint32_t)kWgWindow.panel);
   if (a.cols >= kWcMinCols) h->wc_segments = windowed_segments(a, kWcLog2Window);
+  h->setup_scan_ns = now_ns() - t0;
+  t0 = now_ns();
+  if (split_ok && (st = upload_vc(h, 1, a, kVcSplit))) return st;
+  // the four-part layout (k_vquad) wherever eligible and every segment fits
+  // the kernel's register window (k_vquad has no slow path for longer ones)
+  if (quad_ok) {
+    st = upload_vc(h, 2, a, kVcQuad, kVqLanes);
+    if (st && st != HIPSPMV_ERR_UNSUPPORTED) return st;
+  }
   // the layouts AUTO will run, built now from the host CSR (no copy back off
   // the device at first use, and their time is setup time); device OOM here
   // leaves AUTO on the generic kernels instead of failing the create
@@ -563,6 +572,7 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
     }
   }
   if (experimental && h->wg_eligible && (st = build_vc_layout(h, 3, a))) return st;
+  h->setup_layouts_ns = now_ns() - t0;
   return HIPSPMV_OK;
 }
 
@@ -587,6 +597,7 @@ static int create_common(uint32_t rows, uint32_t cols, uint32_t nnz, int dtype, 
     g_last_error = why;
     return st;
   }
+  const uint64_t csr_ns = now_ns() - t0;
   hipspmv_t* h = new hipspmv_t;
   h->device = device;
   h->dtype = dtype;
@@ -594,6 +605,7 @@ static int create_common(uint32_t rows, uint32_t cols, uint32_t nnz, int dtype, 
   h->rows = rows;
   h->cols = cols;
   h->nnz = nnz;
+  h->setup_csr_ns = csr_ns;
   if (hipDeviceGetAttribute(&h->clock_khz, hipDeviceAttributeClockRate, device) != hipSuccess) h->clock_khz = 0;
   try {
     st = finish_create(h, a);
@@ -1048,6 +1060,10 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "setup_ns") *out = h->setup_ns + h->layout_ns;
   else if (k == "create_ns") *out = h->setup_ns;
   else if (k == "layout_ns") *out = h->layout_ns;
+  else if (k == "setup_csr_ns") *out = h->setup_csr_ns;
+  else if (k == "setup_upload_ns") *out = h->setup_upload_ns;
+  else if (k == "setup_scan_ns") *out = h->setup_scan_ns;
+  else if (k == "setup_layouts_ns") *out = h->setup_layouts_ns;
   else if (k == "auto_fallback") *out = (uint64_t)h->auto_fallback;
   else if (k == "wgather_chunk") *out = h->wgather_chunk;
   else if (k == "kernel_ns") {

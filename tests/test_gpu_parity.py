@@ -914,6 +914,8 @@ def test_auto_layouts_built_at_create(gpu):
     y_o = h.exec(x, beta=0, mode=hs.MODE_ORDERED)
     h.exec(x, beta=0, mode=hs.MODE_FAST)
     assert h.stat("layout_ns") == 0 and h.stat("setup_ns") == h.stat("create_ns") > 0
+    phases = sum(h.stat(f"setup_{k}_ns") for k in ("csr", "upload", "scan", "layouts"))
+    assert 0 < phases <= h.stat("create_ns")  # create's phases lie inside it
     h.set_kernel("sell")  # the SELL layout: built now, from the device CSR copy
     assert h.stat("layout_ns") > 0 and h.stat("setup_ns") == h.stat("create_ns") + h.stat("layout_ns")
     assert h.stat("sell_slices") > 0
