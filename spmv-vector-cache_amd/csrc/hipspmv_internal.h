@@ -2,6 +2,7 @@
 // Not part of the ABI (include/hipspmv.h is).
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -190,10 +191,87 @@ using hvec = std::vector<T, UninitAlloc<T>>;
 // $OMP_NUM_THREADS, else min(16, hardware threads) (plan.cpp).
 unsigned plan_threads();
 
+// A host array that owns its elements (hvec) or borrows the caller's: create
+// from a CSR the caller holds reads it in place instead of copying it (the
+// host CSR lives only for the duration of the create call).  Writes go
+// through the owning storage; a borrowed array is read-only.
+template <class T>
+class HArr {
+ public:
+  HArr() = default;
+  HArr(const HArr& o) { *this = o; }
+  HArr& operator=(const HArr& o) {
+    if (this != &o) {
+      own_.assign(o.begin(), o.end());
+      sync();
+    }
+    return *this;
+  }
+  HArr(HArr&& o) noexcept { *this = std::move(o); }
+  HArr& operator=(HArr&& o) noexcept {
+    const bool borrowed = o.p_ != o.own_.data();
+    own_ = std::move(o.own_);
+    p_ = borrowed ? o.p_ : own_.data();
+    n_ = o.n_;
+    o.own_.clear();
+    o.p_ = nullptr;
+    o.n_ = 0;
+    return *this;
+  }
+  void borrow(const T* p, size_t n) {
+    hvec<T>().swap(own_);
+    p_ = const_cast<T*>(p);
+    n_ = n;
+  }
+  void resize(size_t n) {
+    own_.resize(n);
+    sync();
+  }
+  void assign(size_t n, const T& v) {
+    own_.assign(n, v);
+    sync();
+  }
+  template <class It>
+  void assign(It b, It e) {
+    own_.assign(b, e);
+    sync();
+  }
+  void clear() {
+    own_.clear();
+    sync();
+  }
+  void push_back(const T& v) {  // owning arrays only (tools that build a matrix row by row)
+    own_.push_back(v);
+    sync();
+  }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  const T* data() const { return p_; }
+  T* data() { return p_; }
+  const T& operator[](size_t i) const { return p_[i]; }
+  T& operator[](size_t i) { return p_[i]; }
+  const T* begin() const { return p_; }
+  const T* end() const { return p_ + n_; }
+  T* begin() { return p_; }
+  T* end() { return p_ + n_; }
+  const T& front() const { return p_[0]; }
+  const T& back() const { return p_[n_ - 1]; }
+  bool operator==(const HArr& o) const { return n_ == o.n_ && std::equal(begin(), end(), o.begin()); }
+
+ private:
+  void sync() {
+    p_ = own_.data();
+    n_ = own_.size();
+  }
+  hvec<T> own_;
+  T* p_ = nullptr;
+  size_t n_ = 0;
+};
+
 struct HostCSR {
   uint32_t rows = 0, cols = 0, nnz = 0;
-  hvec<uint32_t> rowptr, colind;
-  hvec<uint64_t> vals;  // 8-byte words (f64 bits or u64)
+  HArr<uint32_t> rowptr, colind;
+  HArr<uint64_t> vals;  // 8-byte words (f64 bits or u64)
 };
 
 struct VcacheLayout {
@@ -215,7 +293,14 @@ struct WinLayout {
   HostCSR seg;                  // A': rows = segments (window-major, then row), cols = the matrix's
   hvec<uint32_t> rowseg;        // rows + 1: row r's segments are segidx[rowseg[r] .. rowseg[r+1])
   hvec<uint32_t> segidx;        // nseg: segment ids of each row, in window order
+  // the direct form (build_windowed_direct): a row with exactly one segment
+  // gets its y from the segment pass, the others from the reduce
+  hvec<uint32_t> dst;           // nseg: row | kWcDirect (one-segment row), else the segment id (partial slot)
+  hvec<uint32_t> mrows;         // rows with 0 or >= 2 segments, ascending
+  hvec<uint32_t> mrowseg;       // mrows + 1: row mrows[i]'s segments are msegidx[mrowseg[i] .. mrowseg[i+1])
+  hvec<uint32_t> msegidx;
 };
+constexpr uint32_t kWcDirect = 1u << 31;
 
 struct SellLayout {
   uint32_t nslices = 0, nhubs = 0, niso = 0;
@@ -235,6 +320,8 @@ struct SellLayout {
 // Returns a HIPSPMV_* status; fills `why` on validation failure.
 int csc_to_csr(const uint32_t* colptr, const uint32_t* rowind, const void* vals, uint32_t rows, uint32_t cols,
                uint32_t nnz, HostCSR& out, std::string& why);
+// CSR given by the caller: validated, then borrowed (out reads the caller's
+// arrays, which must outlive it -- the create call).
 int copy_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, uint32_t rows, uint32_t cols,
              uint32_t nnz, HostCSR& out, std::string& why);
 
@@ -252,6 +339,9 @@ void build_sell(const HostCSR& a, SellLayout& out);
 // The column-windowed segment matrix of `a` (columns sorted within each row:
 // vcache_eligible's condition).  Throws std::bad_alloc on host OOM.
 void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t cap = UINT32_MAX);
+// The reduce-free form of `L` for one-segment rows (fills dst, mrows,
+// mrowseg, msegidx from rowseg / segidx).
+void build_windowed_direct(uint32_t rows, WinLayout& L);
 // Segments build_windowed would make (one pass, no allocation).
 uint64_t windowed_segments(const HostCSR& a, uint32_t log2w);
 // Row groups for csr_vector: group g covers rows [groups[g], groups[g+1]).

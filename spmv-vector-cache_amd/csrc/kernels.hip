@@ -80,11 +80,12 @@ __device__ __forceinline__ T wave_segscan(T v, uint32_t f) {
 // current x window out of L2 (§6.10).  KIND 2: the wcsr reduce -- no values,
 // each "entry" adds x[colind[e]] (a segment partial), so the same balanced
 // groups and segmented scan sum every row's partials in a fixed order.
-template <typename T, int KIND, typename XF>
+// out(r, v, nonempty): the result of row r of the group (v = its sum; a row
+// with no entries passes nonempty false)
+template <typename T, int KIND, typename XF, typename OUT>
 __device__ __forceinline__ void csr_vector_rows(const uint32_t* __restrict__ rowptr,
                                                 const uint32_t* __restrict__ colind, const T* __restrict__ vals,
-                                                XF xv, const T* __restrict__ y_in, T* __restrict__ y_out,
-                                                uint32_t r0, uint32_t r1, int beta, uint32_t* heads) {
+                                                XF xv, OUT out, uint32_t r0, uint32_t r1, uint32_t* heads) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   const uint32_t base = rowptr[r0], n = rowptr[r1] - base;
@@ -108,7 +109,7 @@ __device__ __forceinline__ void csr_vector_rows(const uint32_t* __restrict__ row
     for (; e < n; e += 64) a0 = a0 + term(base + e);
     T s = (a0 + a1) + (a2 + a3);
     s = wave_segscan(s, lane == 0 ? 1u : 0u);  // one segment: lane 63 holds the total
-    if (lane == 63) y_out[r0] = beta ? y_in[r0] + s : s;
+    if (lane == 63) out(r0, s, true);
     return;
   }
 
@@ -148,7 +149,7 @@ __device__ __forceinline__ void csr_vector_rows(const uint32_t* __restrict__ row
       p = wave_segscan(p, f);
       const uint32_t last = re - 1;
       const T tot = __shfl(p, (int)((last - pb) & 63));
-      if (own && re > rs && last >= pb && last < pb + 64) y_out[r0 + lane] = beta ? y_in[r0 + lane] + tot : tot;
+      if (own && re > rs && last >= pb && last < pb + 64) out(r0 + lane, tot, true);
       carry = __shfl(p, 63);
     }
   } else {
@@ -164,12 +165,23 @@ __device__ __forceinline__ void csr_vector_rows(const uint32_t* __restrict__ row
       p = wave_segscan(p, f);
       const uint32_t last = re - 1;  // this lane's row's final element (if its row is non-empty)
       const T tot = __shfl(p, (int)((last - pb) & 63));
-      if (own && re > rs && last >= pb && last < pb + 64) y_out[r0 + lane] = beta ? y_in[r0 + lane] + tot : tot;
+      if (own && re > rs && last >= pb && last < pb + 64) out(r0 + lane, tot, true);
       carry = __shfl(p, 63);
     }
   }
-  if (own && re == rs) y_out[r0 + lane] = beta ? y_in[r0 + lane] : T(0);
+  if (own && re == rs) out(r0 + lane, T(0), false);
 }
+
+// y[r] (+ y_in[r] when beta) for the row sums of a group
+template <typename T>
+struct RowOut {
+  const T* y_in;
+  T* y_out;
+  int beta;
+  __device__ void operator()(uint32_t r, T v, bool nonempty) const {
+    y_out[r] = beta ? (nonempty ? y_in[r] + v : y_in[r]) : (nonempty ? v : T(0));
+  }
+};
 
 // One wave's row group of y = A*x (plus y_in when beta).  KIND 0: plain
 // csr_vector.  KIND 1: the wcsr segment pass -- entry
@@ -188,8 +200,8 @@ __device__ __forceinline__ void csr_vector_group(const uint32_t* __restrict__ ro
   const int w = threadIdx.x >> 6;
   const uint32_t g = blockIdx.x * 4 + w;
   if (g >= ngroups) return;  // wave-uniform; no workgroup barriers below
-  csr_vector_rows<T, KIND>(rowptr, colind, vals, [&](uint32_t c) { return x[c]; }, y_in, y_out, groups[g],
-                           groups[g + 1], beta, heads[w]);
+  csr_vector_rows<T, KIND>(rowptr, colind, vals, [&](uint32_t c) { return x[c]; }, RowOut<T>{y_in, y_out, beta},
+                           groups[g], groups[g + 1], heads[w]);
 }
 
 // k_wseg (wcsr, LDS form): one chunk of one column window's segments per
@@ -211,8 +223,8 @@ __global__ __launch_bounds__(1024) void k_wseg(const uint32_t* __restrict__ chun
   __syncthreads();
   const int w = threadIdx.x >> 6;
   for (uint32_t g = g0 + (uint32_t)w; g < g1; g += 16)
-    csr_vector_rows<T, 3>(rowptr, colind, vals, [&](uint32_t c) { return xw[c - c0]; }, (const T*)nullptr, ypart,
-                          groups[g], groups[g + 1], 0, heads[w]);
+    csr_vector_rows<T, 3>(rowptr, colind, vals, [&](uint32_t c) { return xw[c - c0]; },
+                          RowOut<T>{(const T*)nullptr, ypart, 0}, groups[g], groups[g + 1], heads[w]);
 }
 
 // NTE: the wcsr segment pass (KIND 1 above)
@@ -237,6 +249,51 @@ __global__ __launch_bounds__(256) void k_wreduce(const uint32_t* __restrict__ ro
   csr_vector_group<T, 2>(rowseg, segidx, (const T*)nullptr, ypart, y_in, y_out, groups, ngroups, beta);
 }
 
+// wcsr direct form, segment pass: segment i's sum goes to y[row] when its row
+// has no other segment (dst[i] = row | kWcDirect; + y_in[row] when beta), else
+// to its partial slot ypart[dst[i]] -- the same value and the same add as the
+// reduce would make, so the bits do not change
+template <typename T>
+__global__ __launch_bounds__(256) void k_wseg_direct(const uint32_t* __restrict__ rowptr,
+                                                      const uint32_t* __restrict__ colind,
+                                                      const T* __restrict__ vals, const T* __restrict__ x,
+                                                      const uint32_t* __restrict__ dst, const T* __restrict__ y_in,
+                                                      T* __restrict__ y_out, T* __restrict__ ypart,
+                                                      const uint32_t* __restrict__ groups, uint32_t ngroups, int beta) {
+  __shared__ uint32_t heads[4][kCvGroupNnz / 32];
+  const int w = threadIdx.x >> 6;
+  const uint32_t g = blockIdx.x * 4 + w;
+  if (g >= ngroups) return;
+  auto out = [&](uint32_t i, T v, bool) {
+    const uint32_t d = dst[i];
+    if (d & kWcDirect) {
+      const uint32_t r = d & ~kWcDirect;
+      y_out[r] = beta ? y_in[r] + v : v;
+    } else {
+      ypart[d] = v;
+    }
+  };
+  csr_vector_rows<T, 1>(rowptr, colind, vals, [&](uint32_t c) { return x[c]; }, out, groups[g], groups[g + 1],
+                        heads[w]);
+}
+
+// wcsr direct form, reduce: the rows with 0 or >= 2 segments only (mrows)
+template <typename T>
+__global__ __launch_bounds__(256) void k_wreduce_rows(const uint32_t* __restrict__ mrowseg,
+                                                       const uint32_t* __restrict__ msegidx,
+                                                       const uint32_t* __restrict__ mrows,
+                                                       const T* __restrict__ ypart, const T* __restrict__ y_in,
+                                                       T* __restrict__ y_out, const uint32_t* __restrict__ groups,
+                                                       uint32_t ngroups, int beta) {
+  __shared__ uint32_t heads[4][kCvGroupNnz / 32];
+  const int w = threadIdx.x >> 6;
+  const uint32_t g = blockIdx.x * 4 + w;
+  if (g >= ngroups) return;
+  const RowOut<T> row{y_in, y_out, beta};
+  csr_vector_rows<T, 2>(mrowseg, msegidx, (const T*)nullptr, [&](uint32_t c) { return ypart[c]; },
+                        [&](uint32_t i, T v, bool ne) { row(mrows[i], v, ne); }, groups[g], groups[g + 1], heads[w]);
+}
+
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
@@ -257,6 +314,16 @@ template <typename T>
 hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
   // the segment partials: csr_vector over A', beta 0, entries non-temporal;
   // the LDS form when the layout has window chunks
+  if (a.dst) {  // direct form: one-segment rows written by the segment pass
+    if (a.ngroups)
+      hipLaunchKernelGGL(k_wseg_direct<T>, dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,
+                         (const T*)a.seg_vals, (const T*)a.x, a.dst, (const T*)a.y_in, (T*)a.y_out, (T*)a.ypart,
+                         a.groups, a.ngroups, a.beta);
+    if (a.rgroups)
+      hipLaunchKernelGGL(k_wreduce_rows<T>, dim3((a.rgroups + 3) / 4), dim3(256), 0, s, a.rowseg, a.segidx, a.mrows,
+                         (const T*)a.ypart, (const T*)a.y_in, (T*)a.y_out, a.reduce_groups, a.rgroups, a.beta);
+    return hipGetLastError();
+  }
   if (a.nchunks)
     hipLaunchKernelGGL(k_wseg<T>, dim3(a.nchunks), dim3(1024), 0, s, a.chunks, a.groups, a.seg_rowptr, a.seg_colind,
                        (const T*)a.seg_vals, (const T*)a.x, a.cols, (T*)a.ypart);

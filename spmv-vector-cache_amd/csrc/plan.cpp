@@ -144,17 +144,14 @@ int copy_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, u
   out.rows = rows;
   out.cols = cols;
   out.nnz = nnz;
-  out.rowptr.assign(rowptr, rowptr + (size_t)rows + 1);
-  out.colind.resize(nnz);
-  out.vals.resize(nnz);
-  // copy (first touch of the pages in parallel) and check the column ids
+  // the caller's arrays, read in place for the duration of the create call
+  out.rowptr.borrow(rowptr, (size_t)rows + 1);
+  out.colind.borrow(colind, nnz);
+  out.vals.borrow(static_cast<const uint64_t*>(vals), nnz);
+  // check the column ids
   const unsigned nt = plan_threads();
   std::vector<uint64_t> bad(nt, UINT64_MAX);
-  const uint64_t* v = static_cast<const uint64_t*>(vals);
   par_chunks(nnz, nt, [&](unsigned t, uint64_t lo, uint64_t hi) {
-    if (hi <= lo) return;
-    std::memcpy(out.colind.data() + lo, colind + lo, 4 * (hi - lo));
-    std::memcpy(out.vals.data() + lo, v + lo, 8 * (hi - lo));
     for (uint64_t e = lo; e < hi; ++e)
       if (colind[e] >= cols) {
         bad[t] = e;
@@ -690,6 +687,47 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t c
       }
     }
   });
+}
+
+void build_windowed_direct(uint32_t rows, WinLayout& L) {
+  L.dst.resize(L.nseg);
+  // rows with != 1 segment, in order (serial count, parallel fill)
+  const unsigned nt = std::max(1u, std::min(plan_threads(), std::max(1u, rows / 4096)));
+  std::vector<uint64_t> cnt(nt + 1, 0), scnt(nt + 1, 0);
+  par_chunks(rows, nt, [&](unsigned t, uint64_t lo, uint64_t hi) {
+    uint64_t c = 0, sc = 0;
+    for (uint64_t r = lo; r < hi; ++r) {
+      const uint32_t n = L.rowseg[r + 1] - L.rowseg[r];
+      if (n == 1) {
+        L.dst[L.segidx[L.rowseg[r]]] = (uint32_t)r | kWcDirect;
+      } else {
+        ++c;
+        sc += n;
+        for (uint32_t k = L.rowseg[r]; k < L.rowseg[r + 1]; ++k) L.dst[L.segidx[k]] = L.segidx[k];
+      }
+    }
+    cnt[t + 1] = c;
+    scnt[t + 1] = sc;
+  });
+  for (unsigned t = 0; t < nt; ++t) {
+    cnt[t + 1] += cnt[t];
+    scnt[t + 1] += scnt[t];
+  }
+  L.mrows.resize(cnt[nt]);
+  L.mrowseg.resize(cnt[nt] + 1);
+  L.msegidx.resize(scnt[nt]);
+  par_chunks(rows, nt, [&](unsigned t, uint64_t lo, uint64_t hi) {
+    uint64_t i = cnt[t], k = scnt[t];
+    for (uint64_t r = lo; r < hi; ++r) {
+      const uint32_t n = L.rowseg[r + 1] - L.rowseg[r];
+      if (n == 1) continue;
+      L.mrows[i] = (uint32_t)r;
+      L.mrowseg[i] = (uint32_t)k;
+      for (uint32_t q = L.rowseg[r]; q < L.rowseg[r + 1]; ++q) L.msegidx[k++] = L.segidx[q];
+      ++i;
+    }
+  });
+  L.mrowseg[cnt[nt]] = (uint32_t)scnt[nt];
 }
 
 // Greedy row groups: consecutive rows while the group stays within

@@ -581,6 +581,24 @@ int main(int argc, char** argv) {
         std::vector<uint32_t> gg;
         build_row_groups(G, gg);
         wins = wins && gg.front() == 0 && gg.back() == G.rows;
+        // the direct form: a one-segment row's segment targets the row; every
+        // other row is in mrows once, ascending, with its segments in order
+        build_windowed_direct(A.rows, W);
+        uint32_t mi = 0;
+        for (uint32_t r = 0; r < A.rows && wins; ++r) {
+          const uint32_t n = W.rowseg[r + 1] - W.rowseg[r];
+          if (n == 1) {
+            wins = W.dst[W.segidx[W.rowseg[r]]] == (r | kWcDirect);
+            continue;
+          }
+          wins = mi < W.mrows.size() && W.mrows[mi] == r && W.mrowseg[mi + 1] - W.mrowseg[mi] == n;
+          for (uint32_t k = 0; k < n && wins; ++k) {
+            const uint32_t sg = W.segidx[W.rowseg[r] + k];
+            wins = W.msegidx[W.mrowseg[mi] + k] == sg && W.dst[sg] == sg;
+          }
+          ++mi;
+        }
+        wins = wins && mi == W.mrows.size();
       }
       failures += !(same && tiles && shards && wins);
       std::printf("%-28s csc_to_csr %s, row groups %s, shard groups %s, windowed segments %s\n", cs.name.c_str(),
