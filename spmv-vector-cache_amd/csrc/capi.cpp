@@ -104,9 +104,8 @@ struct hipspmv_handle {
     bool built = false;
     uint32_t *d_rowptr = nullptr, *d_colind = nullptr, *d_groups = nullptr, *d_rowseg = nullptr,
              *d_segidx = nullptr, *d_rgroups = nullptr, *d_chunks = nullptr;
-    uint32_t *d_dst = nullptr, *d_mrows = nullptr;  // direct form (one-segment rows skip the reduce)
     uint64_t *d_vals = nullptr, *d_ypart = nullptr;
-    uint32_t nseg = 0, ngroups = 0, rgroups = 0, max_seg = 0, log2w = 0, nchunks = 0, direct_rows = 0;
+    uint32_t nseg = 0, ngroups = 0, rgroups = 0, max_seg = 0, log2w = 0, nchunks = 0;
   } wc;
   int vcache_dma = -1;   // option "vcache_dma": LDS-DMA x loader (-1 default: on for the split geometry)
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
@@ -190,7 +189,7 @@ static void release(hipspmv_t* h) {
   }
   {
     auto& w = h->wc;
-    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart, w.d_dst, w.d_mrows};
+    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart};
     for (void* p : wp)
       if (p) (void)hipFree(p);
   }
@@ -218,8 +217,7 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
   if (lanes) {  // k_vquad's placement (build_vcache_lanes); false: not placeable, not eligible
     if (!build_vcache_lanes(a, g, lanes, L)) return HIPSPMV_ERR_UNSUPPORTED;
   } else {
-    build_vcache(a, g, L);
-    if (k == 3 && h->wgather_sort) sort_segments_by_line(L);  // k_wgather: gathers of one line side by side
+    build_vcache(a, g, L, k == 3 && h->wgather_sort);  // k_wgather: gathers of one x line side by side
   }
   v.split = g.split;
   v.rows_per_block = L.rows_per_block;
@@ -271,7 +269,7 @@ static void drop_partial_layouts(hipspmv_t* h) {
   }
   if (!h->wc.built) {
     auto& w = h->wc;
-    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart, w.d_dst, w.d_mrows};
+    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart};
     for (void* p : wp)
       if (p) (void)hipFree(p);
     w = hipspmv_handle::Wc{};
@@ -401,7 +399,7 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   const uint64_t bytes0 = h->device_bytes;
   auto fail = [&](int st) {
     void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx,
-                  w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart, w.d_dst, w.d_mrows};
+                  w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart};
     for (void* p : wp)
       if (p) (void)hipFree(p);
     w = hipspmv_handle::Wc{};
@@ -416,25 +414,11 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   if (!chunks.empty() && (st = dev_upload(&w.d_chunks, chunks.data(), chunks.size(), h->device_bytes)))
     return fail(st);
   w.nchunks = (uint32_t)(chunks.size() / 3);
-  if (!lds) {
-    // direct form (round 4): a row with one segment (most rows of the short-row
-    // C5 shards at 2^20 windows) takes its y from the segment pass; the reduce
-    // runs over the other rows only
-    build_windowed_direct(a.rows, L);
-    if ((st = dev_upload(&w.d_dst, L.dst.data(), L.dst.size(), h->device_bytes))) return fail(st);
-    if (!L.mrows.empty() && (st = dev_upload(&w.d_mrows, L.mrows.data(), L.mrows.size(), h->device_bytes)))
-      return fail(st);
-    w.direct_rows = a.rows - (uint32_t)L.mrows.size();
-    L.rowseg.swap(L.mrowseg);  // the reduce's CSR: (mrowseg, msegidx) over mrows
-    L.segidx.swap(L.msegidx);
-  }
-  const uint32_t rrows = lds ? a.rows : (uint32_t)L.mrows.size();
   if ((st = dev_upload(&w.d_rowseg, L.rowseg.data(), L.rowseg.size(), h->device_bytes))) return fail(st);
-  if (!L.segidx.empty() && (st = dev_upload(&w.d_segidx, L.segidx.data(), L.segidx.size(), h->device_bytes)))
-    return fail(st);
+  if ((st = dev_upload(&w.d_segidx, L.segidx.data(), L.segidx.size(), h->device_bytes))) return fail(st);
   {  // the reduce is a csr_vector over (rowseg, segidx) with ypart as x: its own balanced row groups
     std::vector<uint32_t> rg;
-    build_row_groups(L.rowseg.data(), rrows, rg);
+    build_row_groups(L.rowseg.data(), a.rows, rg);
     if ((st = dev_upload(&w.d_rgroups, rg.data(), rg.size(), h->device_bytes))) return fail(st);
     w.rgroups = (uint32_t)rg.size() - 1;
   }
@@ -790,8 +774,6 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     a.chunks = w.d_chunks;
     a.nchunks = w.nchunks;
     a.cols = h->cols;
-    a.dst = w.d_dst;
-    a.mrows = w.d_mrows;
     e = launch_wcsr(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
@@ -1114,7 +1096,6 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "vcache_split4_x_bytes") *out = h->vc[2].ok ? 8ull * h->vc[2].nblocks * h->cols : 0;
   else if (k == "wcsr_segments") *out = h->wc.built ? h->wc.nseg : h->wc_segments;
   else if (k == "wcsr_max_segment") *out = h->wc.max_seg;
-  else if (k == "wcsr_direct_rows") *out = h->wc.direct_rows;
   else if (k == "wcsr_window_log2") *out = h->wc.built ? h->wc.log2w : kWcLog2Window;
   else if (k == "wcsr_chunks") *out = h->wc.nchunks;
   else if (k == "sell_slices") *out = h->sell.nslices;

@@ -293,14 +293,7 @@ struct WinLayout {
   HostCSR seg;                  // A': rows = segments (window-major, then row), cols = the matrix's
   hvec<uint32_t> rowseg;        // rows + 1: row r's segments are segidx[rowseg[r] .. rowseg[r+1])
   hvec<uint32_t> segidx;        // nseg: segment ids of each row, in window order
-  // the direct form (build_windowed_direct): a row with exactly one segment
-  // gets its y from the segment pass, the others from the reduce
-  hvec<uint32_t> dst;           // nseg: row | kWcDirect (one-segment row), else the segment id (partial slot)
-  hvec<uint32_t> mrows;         // rows with 0 or >= 2 segments, ascending
-  hvec<uint32_t> mrowseg;       // mrows + 1: row mrows[i]'s segments are msegidx[mrowseg[i] .. mrowseg[i+1])
-  hvec<uint32_t> msegidx;
 };
-constexpr uint32_t kWcDirect = 1u << 31;
 
 struct SellLayout {
   uint32_t nslices = 0, nhubs = 0, niso = 0;
@@ -330,7 +323,8 @@ bool vcache_eligible(const HostCSR& a, const VcGeom& g);
 // (rows_per_block, nblocks, npanels, part_panels, npad).
 void vcache_geometry(uint32_t rows, uint32_t cols, const VcGeom& g, VcacheLayout& out);
 uint32_t vcache_max_run(const HostCSR& a, uint32_t panel);
-void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out);
+// by_line: each segment's row runs in x-line order (k_wgather; = sort_segments_by_line after)
+void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out, bool by_line = false);
 // k_wgather's segment order: row runs by the x line of their first column (plan.cpp)
 void sort_segments_by_line(VcacheLayout& L);
 // k_vquad's placement of the same entries for CT compute lanes (plan.cpp)
@@ -339,9 +333,6 @@ void build_sell(const HostCSR& a, SellLayout& out);
 // The column-windowed segment matrix of `a` (columns sorted within each row:
 // vcache_eligible's condition).  Throws std::bad_alloc on host OOM.
 void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t cap = UINT32_MAX);
-// The reduce-free form of `L` for one-segment rows (fills dst, mrows,
-// mrowseg, msegidx from rowseg / segidx).
-void build_windowed_direct(uint32_t rows, WinLayout& L);
 // Segments build_windowed would make (one pass, no allocation).
 uint64_t windowed_segments(const HostCSR& a, uint32_t log2w);
 // Row groups for csr_vector: group g covers rows [groups[g], groups[g+1]).

@@ -58,11 +58,6 @@ struct WcsrArgs {  // csr_vector over the column-windowed segment matrix, then k
   uint32_t rows;
   int beta;
   const uint32_t* chunks = nullptr;  // LDS form (k_wseg): (window, first group, end group) per workgroup
-  // direct form (dst != nullptr): the segment pass writes y of one-segment
-  // rows (dst = row | kWcDirect) and the reduce runs over the other rows
-  // only (mrows, with rowseg / segidx / reduce_groups over them)
-  const uint32_t* dst = nullptr;
-  const uint32_t* mrows = nullptr;
   uint32_t nchunks = 0;
   uint32_t cols = 0;
 };

@@ -249,51 +249,6 @@ __global__ __launch_bounds__(256) void k_wreduce(const uint32_t* __restrict__ ro
   csr_vector_group<T, 2>(rowseg, segidx, (const T*)nullptr, ypart, y_in, y_out, groups, ngroups, beta);
 }
 
-// wcsr direct form, segment pass: segment i's sum goes to y[row] when its row
-// has no other segment (dst[i] = row | kWcDirect; + y_in[row] when beta), else
-// to its partial slot ypart[dst[i]] -- the same value and the same add as the
-// reduce would make, so the bits do not change
-template <typename T>
-__global__ __launch_bounds__(256) void k_wseg_direct(const uint32_t* __restrict__ rowptr,
-                                                      const uint32_t* __restrict__ colind,
-                                                      const T* __restrict__ vals, const T* __restrict__ x,
-                                                      const uint32_t* __restrict__ dst, const T* __restrict__ y_in,
-                                                      T* __restrict__ y_out, T* __restrict__ ypart,
-                                                      const uint32_t* __restrict__ groups, uint32_t ngroups, int beta) {
-  __shared__ uint32_t heads[4][kCvGroupNnz / 32];
-  const int w = threadIdx.x >> 6;
-  const uint32_t g = blockIdx.x * 4 + w;
-  if (g >= ngroups) return;
-  auto out = [&](uint32_t i, T v, bool) {
-    const uint32_t d = dst[i];
-    if (d & kWcDirect) {
-      const uint32_t r = d & ~kWcDirect;
-      y_out[r] = beta ? y_in[r] + v : v;
-    } else {
-      ypart[d] = v;
-    }
-  };
-  csr_vector_rows<T, 1>(rowptr, colind, vals, [&](uint32_t c) { return x[c]; }, out, groups[g], groups[g + 1],
-                        heads[w]);
-}
-
-// wcsr direct form, reduce: the rows with 0 or >= 2 segments only (mrows)
-template <typename T>
-__global__ __launch_bounds__(256) void k_wreduce_rows(const uint32_t* __restrict__ mrowseg,
-                                                       const uint32_t* __restrict__ msegidx,
-                                                       const uint32_t* __restrict__ mrows,
-                                                       const T* __restrict__ ypart, const T* __restrict__ y_in,
-                                                       T* __restrict__ y_out, const uint32_t* __restrict__ groups,
-                                                       uint32_t ngroups, int beta) {
-  __shared__ uint32_t heads[4][kCvGroupNnz / 32];
-  const int w = threadIdx.x >> 6;
-  const uint32_t g = blockIdx.x * 4 + w;
-  if (g >= ngroups) return;
-  const RowOut<T> row{y_in, y_out, beta};
-  csr_vector_rows<T, 2>(mrowseg, msegidx, (const T*)nullptr, [&](uint32_t c) { return ypart[c]; },
-                        [&](uint32_t i, T v, bool ne) { row(mrows[i], v, ne); }, groups[g], groups[g + 1], heads[w]);
-}
-
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
@@ -314,16 +269,6 @@ template <typename T>
 hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
   // the segment partials: csr_vector over A', beta 0, entries non-temporal;
   // the LDS form when the layout has window chunks
-  if (a.dst) {  // direct form: one-segment rows written by the segment pass
-    if (a.ngroups)
-      hipLaunchKernelGGL(k_wseg_direct<T>, dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,
-                         (const T*)a.seg_vals, (const T*)a.x, a.dst, (const T*)a.y_in, (T*)a.y_out, (T*)a.ypart,
-                         a.groups, a.ngroups, a.beta);
-    if (a.rgroups)
-      hipLaunchKernelGGL(k_wreduce_rows<T>, dim3((a.rgroups + 3) / 4), dim3(256), 0, s, a.rowseg, a.segidx, a.mrows,
-                         (const T*)a.ypart, (const T*)a.y_in, (T*)a.y_out, a.reduce_groups, a.rgroups, a.beta);
-    return hipGetLastError();
-  }
   if (a.nchunks)
     hipLaunchKernelGGL(k_wseg<T>, dim3(a.nchunks), dim3(1024), 0, s, a.chunks, a.groups, a.seg_rowptr, a.seg_colind,
                        (const T*)a.seg_vals, (const T*)a.x, a.cols, (T*)a.ypart);

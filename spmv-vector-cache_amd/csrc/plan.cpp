@@ -229,13 +229,68 @@ uint32_t vcache_max_run(const HostCSR& a, uint32_t panel) {
   return *std::max_element(best.begin(), best.end());
 }
 
+// Row-run sort by x line (k_wgather's segment order, sort_segments_by_line)
+namespace {
+struct LineSort {
+  uint32_t colmask, lo_bits, nlo, nhi;
+  std::vector<uint32_t> key, start, len, o1, o2, clo, chi, code;
+  std::vector<uint64_t> vals;
+  explicit LineSort(uint32_t colbits) : colmask((1u << colbits) - 1) {
+    const uint32_t kb = colbits > 4 ? colbits - 4 : 1;
+    lo_bits = (kb + 1) / 2;
+    nlo = 1u << lo_bits;
+    nhi = 1u << (kb - lo_bits);
+    clo.resize(nlo + 1);
+    chi.resize(nhi + 1);
+  }
+  void operator()(uint32_t* C, uint64_t* V, uint32_t s0, uint32_t s1) {
+    if (s1 - s0 < 2) return;
+    key.clear();
+    start.clear();
+    len.clear();
+    for (uint32_t e = s0; e < s1;) {
+      uint32_t f = e + 1;
+      while (f < s1 && (C[f] & kVcCont)) ++f;
+      key.push_back((C[e] & colmask) >> 4);
+      start.push_back(e - s0);
+      len.push_back(f - e);
+      e = f;
+    }
+    const uint32_t m = (uint32_t)key.size();
+    o1.resize(m);
+    o2.resize(m);
+    std::fill(clo.begin(), clo.end(), 0u);  // pass 1: low bits (stable)
+    for (uint32_t k = 0; k < m; ++k) clo[(key[k] & (nlo - 1)) + 1]++;
+    for (uint32_t b = 0; b < nlo; ++b) clo[b + 1] += clo[b];
+    for (uint32_t k = 0; k < m; ++k) o1[clo[key[k] & (nlo - 1)]++] = k;
+    std::fill(chi.begin(), chi.end(), 0u);  // pass 2: high bits (stable)
+    for (uint32_t k = 0; k < m; ++k) chi[(key[k] >> lo_bits) + 1]++;
+    for (uint32_t b = 0; b < nhi; ++b) chi[b + 1] += chi[b];
+    for (uint32_t k = 0; k < m; ++k) {
+      const uint32_t r = o1[k];
+      o2[chi[key[r] >> lo_bits]++] = r;
+    }
+    code.assign(C + s0, C + s1);
+    vals.assign(V + s0, V + s1);
+    uint32_t d = s0;
+    for (uint32_t k = 0; k < m; ++k) {
+      const uint32_t r = o2[k];
+      for (uint32_t q = 0; q < len[r]; ++q, ++d) {
+        C[d] = code[start[r] + q];
+        V[d] = vals[start[r] + q];
+      }
+    }
+  }
+};
+}  // namespace
+
 // Entries of row block b that fall into column panel p form segment (b, p),
 // ordered by (row, column); each row's entries keep their CSR order, so a
 // thread that walks a row run in a segment, and the panels in ascending
 // order, adds the row's products in ascending column order.  A work unit
 // (b, h) covers panels [vc_part_first(h), vc_part_first(h+1)); its seg row
 // lists npad+1 offsets (empty segments past its last panel).
-void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
+void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out, bool by_line) {
   const uint32_t P = (uint32_t)g.panel, S = (uint32_t)g.split;
   vcache_geometry(a.rows, a.cols, g, out);
   const uint32_t R = out.rows_per_block, nb = out.nblocks, np = out.npanels, npad = out.npad;
@@ -256,6 +311,7 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
   std::vector<uint64_t> tcont(nt, 0);
   std::vector<std::vector<uint32_t>> tcnt(nt, std::vector<uint32_t>(np + 1)), tcur(nt, std::vector<uint32_t>(np));
   par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
+    LineSort sort((uint32_t)g.colbits);
     for (uint64_t t = t0; t < t1; ++t) {
       std::vector<uint32_t>& cnt = tcnt[t];
       std::vector<uint32_t>& cur = tcur[t];
@@ -290,6 +346,8 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
             prev_p = p;
           }
         }
+        if (by_line)  // the block's segments while they are still in cache (sort_segments_by_line)
+          for (uint32_t p = 0; p < np; ++p) sort(out.code.data(), out.vals.data(), base + cnt[p], base + cnt[p + 1]);
       }
     }
   });
@@ -304,47 +362,17 @@ void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out) {
 // x line of their first column, so lanes of a wave that gather from one line
 // sit next to each other and the gather instruction merges them into one L2
 // request.  Rows stay one run per segment and keep their column order inside
-// it: ORDERED sums are unchanged.
+// it: ORDERED sums are unchanged.  Per segment an LSD radix sort of the runs
+// (two passes of half the line bits), buffers reused across segments.
 void sort_segments_by_line(VcacheLayout& L) {
-  const uint32_t colmask = (1u << L.geom.colbits) - 1, units = L.nblocks * (uint32_t)L.geom.split;
-  const uint32_t npad = L.npad;
+  const uint32_t units = L.nblocks * (uint32_t)L.geom.split, npad = L.npad;
   const unsigned nt = std::max(1u, std::min(plan_threads(), units));
   par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
-    std::vector<uint64_t> runs;  // line << 40 | start << 20 ... packed below
-    std::vector<uint32_t> code;
-    std::vector<uint64_t> vals;
+    LineSort sort((uint32_t)L.geom.colbits);
     for (uint64_t t = t0; t < t1; ++t)
       for (uint32_t u = (uint32_t)t; u < units; u += nt) {
         const uint32_t* sg = &L.seg[(size_t)u * (npad + 1)];
-        for (uint32_t i = 0; i < npad; ++i) {
-          const uint32_t s0 = sg[i], s1 = sg[i + 1], n = s1 - s0;
-          if (n < 2) continue;
-          // (line, position of the run's first entry); positions are < 2^32 - s0
-          std::vector<std::pair<uint32_t, uint32_t>> rk;
-          rk.reserve(n);
-          for (uint32_t e = s0; e < s1;) {
-            rk.emplace_back((L.code[e] & colmask) >> 4, e);
-            uint32_t f = e + 1;
-            while (f < s1 && (L.code[f] & kVcCont)) ++f;
-            e = f;
-          }
-          std::stable_sort(rk.begin(), rk.end(),
-                           [](const std::pair<uint32_t, uint32_t>& p, const std::pair<uint32_t, uint32_t>& q) {
-                             return p.first < q.first;
-                           });
-          code.assign(L.code.begin() + s0, L.code.begin() + s1);
-          vals.assign(L.vals.begin() + s0, L.vals.begin() + s1);
-          uint32_t d = s0;
-          for (const auto& r : rk) {
-            uint32_t e = r.second;
-            do {
-              L.code[d] = code[e - s0];
-              L.vals[d] = vals[e - s0];
-              ++d;
-              ++e;
-            } while (e < s1 && (code[e - s0] & kVcCont));
-          }
-        }
+        for (uint32_t i = 0; i < npad; ++i) sort(L.code.data(), L.vals.data(), sg[i], sg[i + 1]);
       }
   });
 }
@@ -687,47 +715,6 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t c
       }
     }
   });
-}
-
-void build_windowed_direct(uint32_t rows, WinLayout& L) {
-  L.dst.resize(L.nseg);
-  // rows with != 1 segment, in order (serial count, parallel fill)
-  const unsigned nt = std::max(1u, std::min(plan_threads(), std::max(1u, rows / 4096)));
-  std::vector<uint64_t> cnt(nt + 1, 0), scnt(nt + 1, 0);
-  par_chunks(rows, nt, [&](unsigned t, uint64_t lo, uint64_t hi) {
-    uint64_t c = 0, sc = 0;
-    for (uint64_t r = lo; r < hi; ++r) {
-      const uint32_t n = L.rowseg[r + 1] - L.rowseg[r];
-      if (n == 1) {
-        L.dst[L.segidx[L.rowseg[r]]] = (uint32_t)r | kWcDirect;
-      } else {
-        ++c;
-        sc += n;
-        for (uint32_t k = L.rowseg[r]; k < L.rowseg[r + 1]; ++k) L.dst[L.segidx[k]] = L.segidx[k];
-      }
-    }
-    cnt[t + 1] = c;
-    scnt[t + 1] = sc;
-  });
-  for (unsigned t = 0; t < nt; ++t) {
-    cnt[t + 1] += cnt[t];
-    scnt[t + 1] += scnt[t];
-  }
-  L.mrows.resize(cnt[nt]);
-  L.mrowseg.resize(cnt[nt] + 1);
-  L.msegidx.resize(scnt[nt]);
-  par_chunks(rows, nt, [&](unsigned t, uint64_t lo, uint64_t hi) {
-    uint64_t i = cnt[t], k = scnt[t];
-    for (uint64_t r = lo; r < hi; ++r) {
-      const uint32_t n = L.rowseg[r + 1] - L.rowseg[r];
-      if (n == 1) continue;
-      L.mrows[i] = (uint32_t)r;
-      L.mrowseg[i] = (uint32_t)k;
-      for (uint32_t q = L.rowseg[r]; q < L.rowseg[r + 1]; ++q) L.msegidx[k++] = L.segidx[q];
-      ++i;
-    }
-  });
-  L.mrowseg[cnt[nt]] = (uint32_t)scnt[nt];
 }
 
 // Greedy row groups: consecutive rows while the group stays within

@@ -80,6 +80,13 @@ int main(int argc, char** argv) {
     VcacheLayout W;
     build_vcache(a, kWgWindow, W);
     phase("build_vcache wgather", t);
+    t = now_s();
+    sort_segments_by_line(W);
+    phase("sort_segments_by_line", t);
+    t = now_s();
+    VcacheLayout W2;
+    build_vcache(a, kWgWindow, W2, true);
+    phase("build_vcache wgather by line", t);
   }
   if (which == "c5") {
     t = now_s();

@@ -66,6 +66,34 @@ struct Cfg {
   int CX = 0;   // 1/2: cross-lane run continuation (needs every segment in the register window)
 };
 
+// sort_segments_by_line's specification: each segment's row runs stably
+// sorted by the x line (column >> 4) of their first entry
+static void ref_sort_by_line(VcacheLayout& L) {
+  const uint32_t colmask = (1u << L.geom.colbits) - 1, units = L.nblocks * (uint32_t)L.geom.split;
+  for (uint32_t u = 0; u < units; ++u)
+    for (uint32_t i = 0; i < L.npad; ++i) {
+      const uint32_t s0 = L.seg[(size_t)u * (L.npad + 1) + i], s1 = L.seg[(size_t)u * (L.npad + 1) + i + 1];
+      std::vector<std::vector<std::pair<uint32_t, uint64_t>>> runs;
+      std::vector<uint32_t> keys;
+      for (uint32_t e = s0; e < s1; ++e) {
+        if (e == s0 || !(L.code[e] & kVcCont)) {
+          runs.emplace_back();
+          keys.push_back((L.code[e] & colmask) >> 4);
+        }
+        runs.back().emplace_back(L.code[e], L.vals[e]);
+      }
+      std::vector<size_t> ord(runs.size());
+      for (size_t k = 0; k < ord.size(); ++k) ord[k] = k;
+      std::stable_sort(ord.begin(), ord.end(), [&](size_t p, size_t q) { return keys[p] < keys[q]; });
+      uint32_t d = s0;
+      for (size_t k : ord)
+        for (auto& cv : runs[k]) {
+          L.code[d] = cv.first;
+          L.vals[d++] = cv.second;
+        }
+    }
+}
+
 static double madd(double acc, double a, double b) {
   volatile double p = a * b;  // rounded product, then the add (no contraction)
   return acc + p;
@@ -581,24 +609,6 @@ int main(int argc, char** argv) {
         std::vector<uint32_t> gg;
         build_row_groups(G, gg);
         wins = wins && gg.front() == 0 && gg.back() == G.rows;
-        // the direct form: a one-segment row's segment targets the row; every
-        // other row is in mrows once, ascending, with its segments in order
-        build_windowed_direct(A.rows, W);
-        uint32_t mi = 0;
-        for (uint32_t r = 0; r < A.rows && wins; ++r) {
-          const uint32_t n = W.rowseg[r + 1] - W.rowseg[r];
-          if (n == 1) {
-            wins = W.dst[W.segidx[W.rowseg[r]]] == (r | kWcDirect);
-            continue;
-          }
-          wins = mi < W.mrows.size() && W.mrows[mi] == r && W.mrowseg[mi + 1] - W.mrowseg[mi] == n;
-          for (uint32_t k = 0; k < n && wins; ++k) {
-            const uint32_t sg = W.segidx[W.rowseg[r] + k];
-            wins = W.msegidx[W.mrowseg[mi] + k] == sg && W.dst[sg] == sg;
-          }
-          ++mi;
-        }
-        wins = wins && mi == W.mrows.size();
       }
       failures += !(same && tiles && shards && wins);
       std::printf("%-28s csc_to_csr %s, row groups %s, shard groups %s, windowed segments %s\n", cs.name.c_str(),
@@ -616,7 +626,17 @@ int main(int argc, char** argv) {
       }
       VcacheLayout L;
       build_vcache(cs.A, g, L);
-      if (c.LD == 2) sort_segments_by_line(L);  // the wgather layout as hipspmv_create builds it
+      if (c.LD == 2) {  // the wgather layout as hipspmv_create builds it; against a plain stable sort
+        VcacheLayout R = L, D;
+        ref_sort_by_line(R);
+        sort_segments_by_line(L);
+        build_vcache(cs.A, g, D, true);
+        if (!(R.code == L.code && R.vals == L.vals && R.seg == L.seg && D.code == L.code && D.vals == L.vals &&
+              D.seg == L.seg)) {
+          std::printf("%-28s sort_segments_by_line differs from the stable-sort reference\n", cs.name.c_str());
+          ++failures;
+        }
+      }
       // the launcher's guard (vcache_grid_ok) accepts every product layout
       if (!vcache_grid_ok(cs.A.rows, cs.A.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels, L.npad,
                           L.geom.panel, c.SPLIT, g)) {
