@@ -23,7 +23,11 @@
 
 namespace hipspmv {
 
-template <typename T, int CB, int DE, int EPT, bool NTE = false>
+// MSK: entry loads masked past each step's segment (a buffer descriptor over
+// the block's entries; an out-of-range lane issues no request), so a register
+// window wider than the mean segment costs no over-read -- the launcher sizes
+// EPT to the layout's longest segment and no step takes the slow path.
+template <typename T, int CB, int DE, int EPT, bool NTE = false, bool MSK = false>
 __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restrict__ seg,
                                                          const uint32_t* __restrict__ ecode,
                                                          const T* __restrict__ evals, const T* __restrict__ x,
@@ -46,8 +50,24 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
   for (uint32_t i = t; i < nr; i += VT) ylds[i] = beta ? y_in[r0 + i] : T(0);
   __syncthreads();
 
+  const uint32_t e0 = __builtin_amdgcn_readfirstlane(segl[0]);
+  const uint32_t ne = __builtin_amdgcn_readfirstlane(segl[npad]) - e0;
+  const __amdgpu_buffer_rsrc_t dcode = buf_rsrc(ecode + e0, 4 * ne), dvals = buf_rsrc(evals + e0, 8 * ne);
   auto load_e = [&](uint32_t s, uint32_t* c, T* v) {
     const uint32_t beg = segl[min(s, npad)];
+    if constexpr (MSK) {
+      const uint32_t end = segl[min(s + 1, npad)] - e0;
+      constexpr int aux = NTE ? 2 : 0;  // nt
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        const uint32_t q = beg - e0 + t + j * VT;
+        const bool in = q < end;
+        c[j] = __builtin_amdgcn_raw_buffer_load_b32(dcode, in ? (int)(4 * q) : (int)0x80000000, 0, aux);
+        v[j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(dvals, in ? (int)(8 * q) : (int)0x80000000,
+                                                                           0, aux));
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const uint32_t i = min(beg + t + j * VT, last);  // clamped, validity checked at use
@@ -84,10 +104,11 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
       const uint32_t q = beg + t + j * VT;
       if (q < end && !(c[j] & kVcCont)) run(q, c[j], v[j], xv[j], xs);
     }
-    for (uint32_t q = beg + EPT * VT + t; q < end; q += VT) {  // beyond the register window
-      const uint32_t code = ecode[q];
-      if (!(code & kVcCont)) run(q, code, evals[q], xs[code & CMASK], xs);
-    }
+    if (!MSK)  // (masked: the launcher sized EPT to the longest segment)
+      for (uint32_t q = beg + EPT * VT + t; q < end; q += VT) {  // beyond the register window
+        const uint32_t code = ecode[q];
+        if (!(code & kVcCont)) run(q, code, evals[q], xs[code & CMASK], xs);
+      }
   };
 
   uint32_t EC[DE][EPT];
@@ -257,6 +278,22 @@ static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
       hipLaunchKernelGGL((k_wgather_pipe<T, kWgWindow.colbits, 4, 4>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
                          (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
                          a.npanels, a.npad, a.last, a.beta, b0);
+    else if (a.nt_from == 0 && a.max_seg <= 2u * kVcThreads)
+      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 4, 2, true, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg,
+                         a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
+                         a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0);
+    else if (a.nt_from == 0 && a.max_seg <= 3u * kVcThreads)
+      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 4, 3, true, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg,
+                         a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
+                         a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0);
+    else if (a.nt_from == 0 && a.max_seg <= 6u * kVcThreads)
+      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 2, 6, true, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg,
+                         a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
+                         a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0);
+    else if (a.nt_from == 0 && a.max_seg <= 9u * kVcThreads)
+      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 2, 9, true, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg,
+                         a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
+                         a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0);
     else if (a.nt_from == 0)
       hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 4, 2, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
                          (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,

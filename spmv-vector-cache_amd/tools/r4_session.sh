@@ -9,3 +9,7 @@ st=d['strong']; print('C3', d['roofline']['frac'], d['roofline']['kernel_us']); 
 c=d['c5_shards']; print('C5', c.get('max_over_min'), c.get('slowest_us'), c.get('min_roofline_frac'))
 for s in c.get('shards', []): print(s['shard'], s['nnz'], s['kernel'], s.get('kernel_us'), s.get('roofline_frac'), s.get('segments'), s.get('parity'))
 "
+timeout -k 10 300 python spmv-vector-cache_amd/tools/kernel_sweep.py --log2-rows 24 --log2-cols 24 --only "=wgather" --rounds 2 --reps 10 > gpurun_out/sweep_c4_masked.log 2>&1 || { echo sweep c4 failed; tail -5 gpurun_out/sweep_c4_masked.log; exit 1; }
+tail -n 1 gpurun_out/sweep_c4_masked.log
+timeout -k 10 300 python spmv-vector-cache_amd/tools/kernel_sweep.py --only "=wgather,=sell" --rounds 2 --reps 20 > gpurun_out/sweep_c3_wgather.log 2>&1 || { echo sweep c3 failed; tail -5 gpurun_out/sweep_c3_wgather.log; exit 1; }
+tail -n 3 gpurun_out/sweep_c3_wgather.log
