@@ -124,6 +124,9 @@ struct hipspmv_handle {
   // env HIPSPMV_WGATHER_SORT=0 at create: the wgather layout keeps (row, column) order in
   // each segment instead of sorting row runs by x line (probe)
   bool wgather_sort = true;
+  // env HIPSPMV_WCSR_LINE=0 at create: wcsr segments by row inside a window
+  // instead of by the x line of their first column (probe)
+  bool wcsr_line_order = true;
   // option "vcache_nt": row blocks b >= vcache_nt load their entries
   // non-temporally; -1 default: every block for the split
   // geometry, the second half of the blocks for the ordered one
@@ -370,7 +373,7 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   uint32_t cap = (uint32_t)kCvGroupNnz;
   if (const char* e = std::getenv("HIPSPMV_WCSR_MAXSEG")) cap = (uint32_t)std::max(64, std::atoi(e));
   WinLayout L;
-  build_windowed(a, log2w, L, cap);
+  build_windowed(a, log2w, L, cap, !lds && h->wcsr_line_order);
   std::vector<uint32_t> groups, chunks;
   if (lds) {  // csr_vector groups inside each window, cut into chunks of <= kWsChunkNnz entries
     const auto& rp = L.seg.rowptr;
@@ -601,6 +604,7 @@ static int create_common(uint32_t rows, uint32_t cols, uint32_t nnz, int dtype, 
   h->device = device;
   h->dtype = dtype;
   if (const char* e = std::getenv("HIPSPMV_WGATHER_SORT")) h->wgather_sort = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("HIPSPMV_WCSR_LINE")) h->wcsr_line_order = std::strcmp(e, "0") != 0;
   h->rows = rows;
   h->cols = cols;
   h->nnz = nnz;

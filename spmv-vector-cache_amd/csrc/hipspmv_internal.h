@@ -332,7 +332,10 @@ bool build_vcache_lanes(const HostCSR& a, const VcGeom& g, uint32_t CT, VcacheLa
 void build_sell(const HostCSR& a, SellLayout& out);
 // The column-windowed segment matrix of `a` (columns sorted within each row:
 // vcache_eligible's condition).  Throws std::bad_alloc on host OOM.
-void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t cap = UINT32_MAX);
+// by_line: inside a window, segments ordered by the x line of their first
+// column (then row), so a wave's gathers share lines; else by row
+void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t cap = UINT32_MAX,
+                    bool by_line = false);
 // Segments build_windowed would make (one pass, no allocation).
 uint64_t windowed_segments(const HostCSR& a, uint32_t log2w);
 // Row groups for csr_vector: group g covers rows [groups[g], groups[g+1]).

@@ -604,10 +604,15 @@ uint64_t windowed_segments(const HostCSR& a, uint32_t log2w) {
 // In parallel over entry-balanced row ranges (thread t: rows [rb[t], rb[t+1])):
 // a window's segments are numbered by rows ascending, so thread t's first
 // segment of window w follows every earlier thread's segments of w.
-void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t cap) {
+void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t cap, bool by_line) {
   out = WinLayout{};
   out.log2w = log2w;
   const uint32_t nwin = (uint32_t)(((uint64_t)a.cols + (1ull << log2w) - 1) >> log2w);
+  // segment order: window-major, then (by_line) the 128-byte x line of the
+  // segment's first column, then row -- one counting sort over the buckets
+  // (lines, or windows); a window's buckets are contiguous either way
+  const uint32_t bsh = by_line && log2w >= 4 ? 4 : log2w;
+  const uint32_t nbk = (uint32_t)(((uint64_t)a.cols + (1ull << bsh) - 1) >> bsh);
   const unsigned nt = std::max(1u, std::min(plan_threads(), std::max(1u, a.rows / 64)));
   const std::vector<uint32_t> rb = row_chunks(a.rowptr.data(), a.rows, nt);
   auto each_thread = [&](auto&& fn) {
@@ -615,8 +620,8 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t c
       for (uint64_t t = t0; t < t1; ++t) fn((unsigned)t, rb[t], rb[t + 1]);
     });
   };
-  // pass 1: segments per row and per (thread, window)
-  std::vector<std::vector<uint64_t>> wcnt(nt, std::vector<uint64_t>(nwin, 0));
+  // pass 1: segments per row and per (thread, bucket)
+  std::vector<std::vector<uint32_t>> wcnt(nt, std::vector<uint32_t>(nbk, 0));
   out.rowseg.resize((size_t)a.rows + 1);
   each_thread([&](unsigned t, uint32_t r0, uint32_t r1) {
     for (uint32_t r = r0; r < r1; ++r) {
@@ -624,7 +629,7 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t c
       for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
         const uint32_t w = a.colind[e] >> log2w;
         if (w != prev || run == cap) {  // a new window, or the segment is full
-          wcnt[t][w]++;
+          wcnt[t][a.colind[e] >> bsh]++;
           ++n;
           prev = w;
           run = 0;
@@ -635,16 +640,20 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t c
   });
   out.rowseg[0] = 0;
   for (uint32_t r = 0; r < a.rows; ++r) out.rowseg[r + 1] += out.rowseg[r];
-  std::vector<uint64_t> wstart((size_t)nwin + 1, 0);
-  std::vector<std::vector<uint64_t>> cursor(nt, std::vector<uint64_t>(nwin));
-  for (uint32_t w = 0; w < nwin; ++w) {
-    uint64_t c = wstart[w];
+  std::vector<uint64_t> bstart((size_t)nbk + 1, 0);
+  std::vector<std::vector<uint32_t>>& cursor = wcnt;  // counts -> cursors in place
+  for (uint32_t k = 0; k < nbk; ++k) {
+    uint64_t c = bstart[k];
     for (unsigned t = 0; t < nt; ++t) {
-      cursor[t][w] = c;
-      c += wcnt[t][w];
+      const uint32_t n = wcnt[t][k];
+      cursor[t][k] = (uint32_t)c;
+      c += n;
     }
-    wstart[w + 1] = c;
+    bstart[k + 1] = c;
   }
+  std::vector<uint64_t> wstart((size_t)nwin + 1, 0);
+  for (uint32_t w = 0; w <= nwin; ++w)
+    wstart[w] = bstart[std::min<uint64_t>((uint64_t)w << (log2w - bsh), nbk)];
   out.nseg = (uint32_t)wstart[nwin];
   out.winseg.assign(wstart.begin(), wstart.end());
   // pass 2: each segment's id (rows ascend, so ids ascend within a window) and length
@@ -656,7 +665,7 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t c
       for (uint32_t e = a.rowptr[r]; e < a.rowptr[r + 1]; ++e, ++run) {
         const uint32_t w = a.colind[e] >> log2w;
         if (w != prev || run == cap) {
-          out.segidx[k] = (uint32_t)cursor[t][w]++;
+          out.segidx[k] = cursor[t][a.colind[e] >> bsh]++;
           len[out.segidx[k]] = 0;
           ++k;
           prev = w;

@@ -573,9 +573,10 @@ int main(int argc, char** argv) {
       // consecutive, every piece but its last holds exactly cap entries)
       const std::pair<uint32_t, uint32_t> forms[] = {
           {8u, UINT32_MAX}, {12u, UINT32_MAX}, {kWcLog2Window, UINT32_MAX}, {8u, 3u}, {12u, 5u}};
+      for (const bool by_line : {false, true})
       for (const auto& [lw, cap] : forms) {
         WinLayout W;
-        build_windowed(A, lw, W, cap);
+        build_windowed(A, lw, W, cap, by_line);
         const HostCSR& G = W.seg;
         wins = wins && G.rows == W.nseg && G.nnz == A.nnz && G.rowptr.size() == (size_t)W.nseg + 1 &&
                G.rowptr[0] == 0 && G.rowptr[W.nseg] == A.nnz && W.rowseg.size() == (size_t)A.rows + 1 &&
@@ -601,11 +602,17 @@ int main(int argc, char** argv) {
           }
           wins = wins && e == A.rowptr[r + 1];
         }
-        for (uint32_t sg = 1; sg < W.nseg && wins; ++sg) {  // window-major, rows ascending in a window
-          const uint32_t w0 = G.colind[G.rowptr[sg - 1]] >> lw, w1 = G.colind[G.rowptr[sg]] >> lw;
-          wins = w0 < w1 || (w0 == w1 && (owner[sg - 1] < owner[sg] ||
+        // window-major; in a window rows ascending, or (by_line) first-column
+        // lines ascending and rows ascending within a line
+        const uint32_t ksh = by_line && lw >= 4 ? 4 : lw;
+        for (uint32_t sg = 1; sg < W.nseg && wins; ++sg) {
+          const uint32_t k0 = G.colind[G.rowptr[sg - 1]] >> ksh, k1 = G.colind[G.rowptr[sg]] >> ksh;
+          wins = k0 < k1 || (k0 == k1 && (owner[sg - 1] < owner[sg] ||
                                            (cap != UINT32_MAX && owner[sg - 1] == owner[sg])));
         }
+        for (uint32_t w = 0; w + 1 < W.winseg.size() && wins; ++w)  // window w's segments, [winseg[w], winseg[w+1])
+          for (uint32_t sg = W.winseg[w]; sg < W.winseg[w + 1] && wins; ++sg)
+            wins = (G.colind[G.rowptr[sg]] >> lw) == w;
         std::vector<uint32_t> gg;
         build_row_groups(G, gg);
         wins = wins && gg.front() == 0 && gg.back() == G.rows;
