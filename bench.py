@@ -652,12 +652,13 @@ def main():
         scaling = "strong"
     else:
         n = 1 << a.scale
-        bounds = hs.partition_row_counts(hs.gen_rmat_row_counts(a.scale, 16, 4), pworld)
+        # the cost partition of the c5_shards block (wcsr's measured cost model), or --c5-partition nnz
+        bounds, _ = hs.c5_partition(a.scale, pworld, model=a.c5_partition)
         row0, row1 = int(bounds[prank]), int(bounds[prank + 1])
         rows, cols = row1 - row0, n
         rowptr, colind, vals = hs.gen_rmat_rows(a.scale, row0, row1, 16, 4)
         workload = (f"C5 R-MAT scale {a.scale} (a,b,c=0.57,0.19,0.19), edge factor 16, "
-                    f"{pworld} nnz-balanced row blocks")
+                    f"{pworld} row blocks ({a.c5_partition} partition)")
         scaling = "strong"
     if a.shard:
         workload += f" -- shard {prank} of {pworld} alone on one GPU (rows [{row0},{row1}))"
