@@ -420,12 +420,11 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   w.nchunks = (uint32_t)(chunks.size() / 3);
   if ((st = dev_upload(&w.d_rowseg, L.rowseg.data(), L.rowseg.size(), h->device_bytes))) return fail(st);
   if ((st = dev_upload(&w.d_segidx, L.segidx.data(), L.segidx.size(), h->device_bytes))) return fail(st);
-  {  // the reduce: a lane per row of <= kWrLaneMax segments, a wave per longer row (their ids here)
-    std::vector<uint32_t> lr;
-    for (uint32_t r = 0; r < a.rows; ++r)
-      if (L.rowseg[r + 1] - L.rowseg[r] > (uint32_t)kWrLaneMax) lr.push_back(r);
-    if ((st = dev_upload(&w.d_rgroups, lr.data(), lr.size(), h->device_bytes))) return fail(st);
-    w.rgroups = (uint32_t)lr.size();
+  {  // the reduce is a csr_vector over (rowseg, segidx) with ypart as x: its own balanced row groups
+    std::vector<uint32_t> rg;
+    build_row_groups(L.rowseg.data(), a.rows, rg);
+    if ((st = dev_upload(&w.d_rgroups, rg.data(), rg.size(), h->device_bytes))) return fail(st);
+    w.rgroups = (uint32_t)rg.size() - 1;
   }
   {
     const uint64_t b = 8ull * std::max<uint32_t>(L.nseg, 1);

@@ -95,9 +95,6 @@ constexpr uint32_t kWsChunkNnz = 49152;
 constexpr uint32_t kWcMinCols = 1u << 21;
 
 // ---- csr_vector geometry ---------------------------------------------------
-// wcsr reduce: rows of at most this many segments are summed by one lane
-// (k_wreduce_lane), longer ones by a wave (k_wreduce_long)
-constexpr int kWrLaneMax = 8;
 constexpr int kCvGroupNnz = 256;  // max nnz of a multi-row group (4 per lane)
 constexpr int kCvGroupRows = 64;  // max rows of a multi-row group (1 per lane)
 

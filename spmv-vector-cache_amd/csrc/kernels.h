@@ -49,8 +49,8 @@ struct WcsrArgs {  // csr_vector over the column-windowed segment matrix, then k
   uint32_t ngroups;
   const uint32_t* rowseg;         // [rows + 1]: row r's segments are segidx[rowseg[r] .. rowseg[r+1])
   const uint32_t* segidx;         // [nseg]: each row's segment ids, in window order
-  const uint32_t* reduce_groups;  // the rows of more than kWrLaneMax segments (k_wreduce_long, a wave each)
-  uint32_t rgroups;               // their count (the others: k_wreduce_lane, a lane each)
+  const uint32_t* reduce_groups;  // csr_vector row groups of the (rowseg, segidx) reduce
+  uint32_t rgroups;
   void* ypart;                    // [nseg] segment partials, in segment order
   const void* x;
   const void* y_in;

@@ -237,45 +237,16 @@ __global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__
   csr_vector_group<T, NTE ? 1 : 0>(rowptr, colind, vals, x, y_in, y_out, groups, ngroups, beta);
 }
 
-// wcsr reduce, short rows (<= kWrLaneMax segments, nearly every row of the
-// short-row C5 shards): one lane per row adds its partials in window order,
-// y = (y_in +) p0 + p1 + ...; longer rows are left to k_wreduce_long
+// k_wreduce (wcsr): y[r] = (y_in[r] +) the sum of row r's segment partials
+// ypart[segidx[k]], k in [rowseg[r], rowseg[r+1]) (window order), over the
+// reduce's own balanced row groups -- a fixed order, so wcsr is
+// deterministic; a row with no segment gets y_in[r] (beta 1) or +0.0.
 template <typename T>
-__global__ __launch_bounds__(256) void k_wreduce_lane(const uint32_t* __restrict__ rowseg,
-                                                       const uint32_t* __restrict__ segidx,
-                                                       const T* __restrict__ ypart, const T* __restrict__ y_in,
-                                                       T* __restrict__ y_out, uint32_t rows, int beta) {
-#pragma clang fp contract(off)
-  const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= rows) return;
-  const uint32_t k0 = rowseg[r], n = rowseg[r + 1] - k0;
-  if (n > (uint32_t)kWrLaneMax) return;
-  T v[kWrLaneMax];
-#pragma unroll
-  for (int k = 0; k < kWrLaneMax; ++k)  // every partial's load in flight before the adds
-    if ((uint32_t)k < n) v[k] = ypart[segidx[k0 + k]];
-  T tot = T(0);
-#pragma unroll
-  for (int k = 0; k < kWrLaneMax; ++k)
-    if ((uint32_t)k < n) tot = k == 0 ? v[0] : tot + v[k];
-  y_out[r] = beta ? (n ? y_in[r] + tot : y_in[r]) : tot;
-}
-
-// wcsr reduce, long rows (> kWrLaneMax segments): a wave per row, the
-// segmented-scan sum of csr_vector_rows (KIND 2) over its partials
-template <typename T>
-__global__ __launch_bounds__(256) void k_wreduce_long(const uint32_t* __restrict__ rowseg,
-                                                       const uint32_t* __restrict__ segidx,
-                                                       const T* __restrict__ ypart, const T* __restrict__ y_in,
-                                                       T* __restrict__ y_out, const uint32_t* __restrict__ long_rows,
-                                                       uint32_t nlong, int beta) {
-  __shared__ uint32_t heads[4][kCvGroupNnz / 32];
-  const int w = threadIdx.x >> 6;
-  const uint32_t g = blockIdx.x * 4 + w;
-  if (g >= nlong) return;
-  const uint32_t r = long_rows[g];
-  csr_vector_rows<T, 2>(rowseg, segidx, (const T*)nullptr, [&](uint32_t c) { return ypart[c]; },
-                        RowOut<T>{y_in, y_out, beta}, r, r + 1, heads[w]);
+__global__ __launch_bounds__(256) void k_wreduce(const uint32_t* __restrict__ rowseg,
+                                                  const uint32_t* __restrict__ segidx, const T* __restrict__ ypart,
+                                                  const T* __restrict__ y_in, T* __restrict__ y_out,
+                                                  const uint32_t* __restrict__ groups, uint32_t ngroups, int beta) {
+  csr_vector_group<T, 2>(rowseg, segidx, (const T*)nullptr, ypart, y_in, y_out, groups, ngroups, beta);
 }
 
 // ---------------------------------------------------------------------------
@@ -305,14 +276,8 @@ hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((k_csr_vector<T, true>), dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr,
                        a.seg_colind, (const T*)a.seg_vals, (const T*)a.x, (const T*)nullptr, (T*)a.ypart,
                        a.groups, a.ngroups, 0);
-  // the reduce: a lane per short row, a wave per long row (reduce_groups: the
-  // long rows' ids, rgroups of them)
-  if (a.rows)
-    hipLaunchKernelGGL(k_wreduce_lane<T>, dim3((a.rows + 255) / 256), dim3(256), 0, s, a.rowseg, a.segidx,
-                       (const T*)a.ypart, (const T*)a.y_in, (T*)a.y_out, a.rows, a.beta);
-  if (a.rgroups)
-    hipLaunchKernelGGL(k_wreduce_long<T>, dim3((a.rgroups + 3) / 4), dim3(256), 0, s, a.rowseg, a.segidx,
-                       (const T*)a.ypart, (const T*)a.y_in, (T*)a.y_out, a.reduce_groups, a.rgroups, a.beta);
+  hipLaunchKernelGGL(k_wreduce<T>, dim3((a.rgroups + 3) / 4), dim3(256), 0, s, a.rowseg, a.segidx,
+                     (const T*)a.ypart, (const T*)a.y_in, (T*)a.y_out, a.reduce_groups, a.rgroups, a.beta);
   return hipGetLastError();
 }
 hipError_t launch_wcsr(int dtype, const WcsrArgs& a, hipStream_t s) {

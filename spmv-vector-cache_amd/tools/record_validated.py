@@ -28,7 +28,7 @@ PRODUCT = [f"void hipspmv::k_{k}<{t}{a}>" for t in ("double", "unsigned long")
            ("double, true", "double, false", "unsigned long, false")] + \
           ["void hipspmv::(anonymous namespace)::k_sell_iso<45>"] + \
           [f"void hipspmv::k_{k}" for t in ("double", "unsigned long")
-           for k in (f"csr_vector<{t}, true>", f"wreduce_lane<{t}>", f"wreduce_long<{t}>")]
+           for k in (f"csr_vector<{t}, true>", f"wreduce<{t}>")]
 
 
 def main():
