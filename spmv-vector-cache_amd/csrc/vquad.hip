@@ -59,18 +59,6 @@ __device__ __forceinline__ void tie(R& r) {
 __device__ __forceinline__ void tie(u64x2& r) {
   asm volatile("" : "+v"(r));
 }
-__device__ __forceinline__ uint32_t ald_u32_nt(const uint32_t* p) {
-  uint32_t r;
-  asm volatile("global_load_dword %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
-  return r;
-}
-template <typename T>
-__device__ __forceinline__ T ald_64_nt(const T* p) {
-  uint64_t r;
-  asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
-  return __builtin_bit_cast(T, r);
-}
-
 // entry loads through a buffer descriptor of the unit's entries: a lane past
 // its step's segment gets an out-of-range offset and the load returns 0
 // without a memory request, while every lane still issues the instruction
