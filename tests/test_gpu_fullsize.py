@@ -153,3 +153,31 @@ def test_full_size_u64_exact_properties(request, which):
         assert len(ran) == len(U64_KERNELS[which]), ran  # distinct kernels, none silently substituted
     finally:
         h.close()
+
+
+@pytest.fixture(scope="module")
+def c5_bounds(gpu):
+    bounds, _ = hs.c5_partition(24, 8)  # bench.py's c5_shards partition (wcsr cost model)
+    return bounds
+
+
+@pytest.mark.parametrize("shard", [0, 3, 7])
+def test_c5_shard_auto_picks_wcsr(c5_bounds, shard):
+    """C5 as the 8-GPU job runs it: shards of the cost partition, each created alone.  AUTO's FAST
+    kernel is wcsr on the hub-row shard 0, a middle shard and the short-row shard 7 (the bench's
+    c5_shards block records it for all eight), and sampled rows meet the FAST bound."""
+    r0, r1 = int(c5_bounds[shard]), int(c5_bounds[shard + 1])
+    n = 1 << 24
+    rowptr, colind, vals = hs.gen_rmat_rows(24, r0, r1, 16, 4)
+    rows = r1 - r0
+    x = hs.gen_vector(n, 3)
+    sample = _sample(rowptr, rows, k=400)
+    want, absprod = _sequential(rowptr, colind, vals, x, sample)
+    lens = np.diff(rowptr.astype(np.int64))
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, n)
+    try:
+        assert h.kernel_name(hs.MODE_FAST) == "wcsr", (shard, h.kernel_name(hs.MODE_FAST))
+        assert h.stat("wcsr_window_log2") == 20
+        _check(h, x, sample, want, absprod, lens, "auto", hs.MODE_FAST)
+    finally:
+        h.close()
