@@ -350,13 +350,21 @@ def host_transfer_us(xd, yd, reps: int = 5):
     return out[0], out[1]
 
 
+GRAPH_MIN_STEPS = 64
+
+
 def time_steps(a, h, xd, yd, mode: int, stream, dev, dist, world: int, graph_info: dict):
     """W warmup + K timed steps of h on (xd -> yd); returns (max-over-ranks wall s, this rank's kernel
     ms/launch from HIP events, every rank's kernel ms/launch).  With --graph (default) the K launches are
     captured once into a HIP graph on a side stream and the timed region replays it: the same K kernels,
     without K host launch gaps."""
     run_stream, g = stream, None
-    if not a.no_graph:
+    # short runs launch eagerly: a replayed graph pays its launch latency once per replay, which K
+    # launches of ~0.1 ms do not amortise (C3 at K = 20: graph 130-132 us per launch, eager
+    # 120-124; at K = 200 the graph's 106 us is the faster; profiles/r04/logs/bench_20steps_*.log)
+    if not a.no_graph and a.steps < GRAPH_MIN_STEPS:
+        graph_info[mode] = f"{a.steps} plain launches (graphs from {GRAPH_MIN_STEPS} steps)"
+    elif not a.no_graph:
         gs = torch.cuda.Stream(dev)
         for _ in range(a.warmup):  # eager launches on the capture stream, synchronised before the capture
             h.exec_device(xd, yd, beta=0, mode=mode, stream=gs)
