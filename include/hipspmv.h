@@ -64,15 +64,16 @@ extern "C" {
 #define HIPSPMV_KERNEL_VCACHE 1     /* x panels + y block staged in LDS; ordered */
 #define HIPSPMV_KERNEL_CSR_LANE 2   /* one lane per row over CSR; ordered */
 #define HIPSPMV_KERNEL_CSR_VECTOR 3 /* wave segmented DPP reduction over CSR; fast */
-#define HIPSPMV_KERNEL_VCACHE_SPLIT 4 /* vcache over two column halves, fixed-order
-                                         combine p0 + p1; fast, deterministic */
+#define HIPSPMV_KERNEL_VCACHE_SPLIT 4 /* vcache over three column parts, fixed-order
+                                         combine p0 + p1 + p2; fast, deterministic */
 #define HIPSPMV_KERNEL_VCACHE_SPLIT4 5 /* four column parts, p0+p1+p2+p3; fast,
-                                          deterministic; experimental: never
-                                          chosen by AUTO, layout built only
-                                          when HIPSPMV_EXPERIMENTAL=1 at create */
+                                          deterministic; never chosen by AUTO,
+                                          its layout is built on first selection
+                                          by name (option "kernel", or the stat
+                                          "vcache_split4_eligible") */
 #define HIPSPMV_KERNEL_WGATHER 6 /* y block in LDS, x gathered from global in
-                                    2^16-column windows (wide x: C4/C5);
-                                    ordered; experimental like VCACHE_SPLIT4 */
+                                    2^16-column windows (wide x: C4);
+                                    ordered; chosen by AUTO for wide x */
 #define HIPSPMV_KERNEL_WCSR 8 /* csr_vector over the rows cut at 2^20-column
                                  windows (window-major), then each row's window
                                  partials summed in a fixed order; fast,
@@ -120,7 +121,13 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
  * default: every block for VCACHE_SPLIT, the second half for VCACHE; WGATHER:
  * 0 or -1 non-temporal, > 0 the default policy), "sell_nt" (SELL slices s >=
  * sell_nt likewise; -1 default: the second half).  The cache policy never
- * changes a result bit.  Experimental (HIPSPMV_EXPERIMENTAL=1): "sell_chain"
+ * changes a result bit.  "vquad_variant" (VCACHE_SPLIT4 configuration,
+ * csrc/vquad.hip: 0 default; 1-5, 17-19 other x / entry ring depths; 20 every
+ * column-part owner gives up waiting, so the publish-and-count combine runs --
+ * exact, counted by the stat "handoff_fallbacks"; 21 XCD placement; 22 / 23
+ * with / without it, the entries of row blocks below "vcache_nt" in the
+ * Infinity Cache; 24-26 y updated by LDS atomics; 6-16 are timing ablations
+ * whose y is wrong: HIPSPMV_EXPERIMENTAL=1 only).  Experimental (HIPSPMV_EXPERIMENTAL=1): "sell_chain"
  * (ORDERED hub chains: 1 = no isolated chains, 2 / 3 = isolated stages of 12 /
  * 30 products per lane instead of 45; the same bits), "sell_only" (timing
  * probe, y incomplete: 1 hub rows only, 2 slices only, 3 the longest row). */
@@ -160,7 +167,8 @@ int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void 
  * "sell_padding" "sell_iso_hubs" (SELL layout, 0 until the sell kernel is
  * selected) "wcsr_segments" "wcsr_max_segment" "wcsr_window_log2"
  * "wcsr_chunks" (wcsr layout)
- * "max_row_len" "empty_rows" "execs"; the reference accelerator's cache
+ * "max_row_len" "empty_rows" "execs" "handoff_fallbacks" (VCACHE_SPLIT4
+ * combine owners that gave up waiting, since create); the reference accelerator's cache
  * statistics for the last launch: "total_cycles" "active_cycles" "read_misses"
  * "hazard_stalls" "ocm_depth" "issue_window" "capacity_stalls" "cms"; measured
  * by the last launch run with option "profile" (means over its workgroups, in
@@ -234,9 +242,20 @@ int hipspmv_mark_row_starts(const uint32_t *rowind, uint32_t *rowind_out, uint32
  * host partition helpers cut at such rows. */
 #define HIPSPMV_SHARD_ALIGN 64
 
+/* Row partition used by hipspmv_multi_create (and bench.py's C5 shards):
+ * `parts` contiguous blocks of about equal cost, a row costing its entries +
+ * its segments at the wcsr kernel's 2^20-column windows (runs of more than 256
+ * entries in a window cut into pieces) + 1, interior bounds snapped to the
+ * nearer multiple of HIPSPMV_SHARD_ALIGN.  CSR input (rowptr[rows + 1],
+ * colind[nnz]); writes bounds[parts + 1] (bounds[0] = 0, bounds[parts] =
+ * rows).  Host only, no device.  Replaces the nnz-balanced partitionRows of
+ * ref:software/main.cpp-style drivers for skewed matrices. */
+int hipspmv_partition_rows(const uint32_t *rowptr, const uint32_t *colind, uint32_t rows, uint32_t cols,
+                           uint32_t parts, uint32_t *bounds);
+
 /* ---- several devices of one process ---------------------------------------
  * One matrix row-partitioned over ndev devices (rows cut into contiguous,
- * nnz-balanced blocks starting at multiples of HIPSPMV_SHARD_ALIGN; block i
+ * cost-balanced blocks by hipspmv_partition_rows; block i
  * on devices[i]): the single-host-thread
  * multi-GPU form of SURVEY.md §8(b)/(e), for HIPSpMV (register num_devices)
  * and C callers.  exec copies x to devices[0], broadcasts it device to device
@@ -252,6 +271,14 @@ typedef struct hipspmv_multi hipspmv_multi_t;
 int hipspmv_multi_create(const uint32_t *colptr, const uint32_t *rowind, const void *vals, uint32_t rows,
                          uint32_t cols, uint32_t nnz, int dtype, const int *devices, int ndev,
                          hipspmv_multi_t **out);
+/* The same from a CSR (rowptr[rows + 1], colind[nnz] ascending within each
+ * row, vals[nnz]); the arrays are read during the call only. */
+int hipspmv_multi_create_csr(const uint32_t *rowptr, const uint32_t *colind, const void *vals, uint32_t rows,
+                             uint32_t cols, uint32_t nnz, int dtype, const int *devices, int ndev,
+                             hipspmv_multi_t **out);
+/* Block i's own handle (NULL for a block without rows), owned by m: its
+ * hipspmv_exec_device / hipspmv_stat run that block alone (per-block timing). */
+int hipspmv_multi_shard(hipspmv_multi_t *m, int i, hipspmv_t **out);
 int hipspmv_multi_set_option(hipspmv_multi_t *m, const char *key, int64_t value);
 int hipspmv_multi_exec(hipspmv_multi_t *m, const void *x, void *y, int beta, int mode);
 int hipspmv_multi_stat(hipspmv_multi_t *m, const char *key, uint64_t *out);

@@ -85,6 +85,9 @@ struct hipspmv_handle {
   // The ordered vcache layout is only ever selected by name: its eligibility
   // and geometry are known at create, its entries built on first selection.
   bool vc0_eligible = false;
+  // the four-part geometry's eligibility (create; the k_vquad layout itself is
+  // built on first selection, ensure_layout, and may then prove unplaceable)
+  bool vq_eligible = false;
   // k_wgather (x wider than the vcache geometries): eligibility and longest
   // in-window run measured at create; the layout is built at create when AUTO
   // picks the kernel, else on first selection by name
@@ -516,8 +519,8 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   if ((st = dev_upload(&h->d_groups, groups.data(), groups.size(), h->device_bytes))) return st;
   h->setup_upload_ns = now_ns() - t0;
   t0 = now_ns();
-  // the experimental split4 layout is built only on request
-  // (HIPSPMV_EXPERIMENTAL=1): each costs another copy of the entries
+  // experimental builds (HIPSPMV_EXPERIMENTAL=1) also build the wgather
+  // window layout at create (below)
   const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
   const bool experimental = exp && std::strcmp(exp, "1") == 0;
   // ordered vcache: geometry now, entries on first selection by name
@@ -545,12 +548,9 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   h->setup_scan_ns = now_ns() - t0;
   t0 = now_ns();
   if (split_ok && (st = upload_vc(h, 1, a, kVcSplit))) return st;
-  // the four-part layout (k_vquad) wherever eligible and every segment fits
-  // the kernel's register window (k_vquad has no slow path for longer ones)
-  if (quad_ok) {
-    st = upload_vc(h, 2, a, kVcQuad, kVqLanes);
-    if (st && st != HIPSPMV_ERR_UNSUPPORTED) return st;
-  }
+  // the four-part layout (k_vquad, never chosen by AUTO) is built on first
+  // selection by name (ensure_layout), like the ordered vcache's
+  h->vq_eligible = quad_ok;
   // the layouts AUTO will run, built now from the host CSR (no copy back off
   // the device at first use, and their time is setup time); device OOM here
   // leaves AUTO on the generic kernels instead of failing the create
@@ -640,7 +640,7 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
       return h->vc[1].ok ? HIPSPMV_KERNEL_VCACHE_SPLIT : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_VCACHE_SPLIT4:
       if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
-      return h->vc[2].ok ? HIPSPMV_KERNEL_VCACHE_SPLIT4 : -HIPSPMV_ERR_UNSUPPORTED;
+      return h->vc[2].ok || h->vq_eligible ? HIPSPMV_KERNEL_VCACHE_SPLIT4 : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_WGATHER:  // ordered: valid in both modes
       return h->vc[3].ok || h->wg_eligible ? HIPSPMV_KERNEL_WGATHER : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_LANE:
@@ -665,6 +665,7 @@ static int ensure_layout(hipspmv_t* h, int kernel) {
   const bool need = (kernel == HIPSPMV_KERNEL_SELL && !h->sell.built) ||
                     (kernel == HIPSPMV_KERNEL_WGATHER && !h->vc[3].ok) ||
                     (kernel == HIPSPMV_KERNEL_VCACHE && !h->vc[0].ok) ||
+                    (kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4 && !h->vc[2].ok) ||
                     (kernel == HIPSPMV_KERNEL_WCSR && !h->wc.built);
   if (!need) return HIPSPMV_OK;
   const uint64_t t0 = now_ns();
@@ -676,7 +677,12 @@ static int ensure_layout(hipspmv_t* h, int kernel) {
     if (!st) {
       if (kernel == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
       else if (kernel == HIPSPMV_KERNEL_WCSR) st = build_wcsr_layout(h, a);
-      else st = build_vc_layout(h, kernel == HIPSPMV_KERNEL_WGATHER ? 3 : 0, a);
+      else if (kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
+        // every segment inside the kernel's register window, runs placeable
+        // (build_vcache_lanes); otherwise not eligible from now on
+        st = h->vq_eligible ? upload_vc(h, 2, a, kVcQuad, kVqLanes) : HIPSPMV_ERR_UNSUPPORTED;
+        if (st == HIPSPMV_ERR_UNSUPPORTED) h->vq_eligible = false;
+      } else st = build_vc_layout(h, kernel == HIPSPMV_KERNEL_WGATHER ? 3 : 0, a);
     }
   } catch (const std::bad_alloc&) {
     drop_partial_layouts(h);
@@ -796,19 +802,16 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   return HIPSPMV_OK;
 }
 
-// k_vquad's combine status (bit 0: a hand-off wait timed out, the launch's y
-// is wrong): read after a synchronous exec and by the stat key
-// "handoff_timeouts"; a set bit resets the scratch counters and the word.
+// k_vquad's combine fallbacks: owners that gave up waiting for their share's
+// publishers and published their own share too (csrc/combine.h) since create.
+// The result is exact on either path; the count says which one ran (variant 20
+// forces it).  Read by the stat key "handoff_fallbacks" only, never per exec.
 static int read_status(hipspmv_t* h, uint32_t* out) {
   *out = 0;
   if (!h->d_status) return HIPSPMV_OK;
   DeviceGuard g(h->device);
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(out, h->d_status, 4, hipMemcpyDeviceToHost));
-  if (*out) {
-    if (h->vc[2].d_tickets) HIP_TRY(hipMemset(h->vc[2].d_tickets, 0, 16ull * h->vc[2].nblocks));
-    HIP_TRY(hipMemset(h->d_status, 0, 4));
-  }
   return HIPSPMV_OK;
 }
 
@@ -937,7 +940,10 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "vcache_map") {
     h->vcache_map = value ? 1 : 0;
   } else if (k == "vquad_variant") {  // k_vquad configuration (csrc/vquad.hip)
-    if (value < 0 || value > 20) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < 0 || value > 26) return HIPSPMV_ERR_INVALID_ARG;
+    // 6-16 are timing ablations that give wrong y (or race): experimental builds only
+    const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
+    if (value >= 6 && value <= 16 && !(exp && std::strcmp(exp, "1") == 0)) return HIPSPMV_ERR_UNSUPPORTED;
     if (h->vc[2].ok && h->vc[2].max_seg > vquad_max_window((int)value)) return HIPSPMV_ERR_UNSUPPORTED;
     h->vquad_variant = (int)value;
   } else if (k == "wgather_chunk") {  // row blocks per k_wgather launch (0: all in one launch)
@@ -1016,14 +1022,6 @@ int hipspmv_exec(hipspmv_t* h, const void* x, void* y, int beta, int mode) {
     HIP_TRY(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
     h->d2h_ns = (uint64_t)(ms * 1e6);
     h->pending = false;
-    if (kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
-      uint32_t bad = 0;
-      if (int st2 = read_status(h, &bad)) return st2;
-      if (bad) {
-        set_last_error("k_vquad: a column-part hand-off timed out; this exec's y is wrong (scratch reset)");
-        return HIPSPMV_ERR_HIP;
-      }
-    }
     return HIPSPMV_OK;
   } catch (const std::bad_alloc&) {
     return HIPSPMV_ERR_OOM;
@@ -1092,7 +1090,13 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   // columns once (split: its two halves read one half each)
   else if (k == "vcache_x_bytes") *out = h->vc0_eligible ? 8ull * h->vc[0].nblocks * h->cols : 0;
   else if (k == "vcache_split_x_bytes") *out = h->vc[1].ok ? 8ull * h->vc[1].nblocks * h->cols : 0;
-  else if (k == "vcache_split4_eligible") *out = h->vc[2].ok;
+  else if (k == "vcache_split4_eligible") {  // builds the k_vquad layout if it is not built yet
+    if (!h->vc[2].ok && h->vq_eligible) {
+      const int st = ensure_layout(h, HIPSPMV_KERNEL_VCACHE_SPLIT4);
+      if (st && st != HIPSPMV_ERR_UNSUPPORTED) return st;
+    }
+    *out = h->vc[2].ok;
+  }
   else if (k == "wgather_eligible") *out = h->vc[3].ok || h->wg_eligible;
   else if (k == "wgather_max_run") *out = h->wg_max_run;
   else if (k == "vcache_max_run") *out = h->vc[0].max_run;
@@ -1112,7 +1116,7 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "max_row_len") *out = h->max_row_len;
   else if (k == "empty_rows") *out = h->empty_rows;
   else if (k == "execs") *out = h->execs;
-  else if (k == "handoff_timeouts") {  // k_vquad combine waits that timed out since the last read (0)
+  else if (k == "handoff_fallbacks") {  // k_vquad owners that gave up waiting (publish-and-count path), since create
     uint32_t v = 0;
     if (int st = read_status(h, &v)) return st;
     *out = v;

@@ -31,10 +31,13 @@ namespace hipspmv {
 // partial + (o * nblocks + b) * VRP; scratch: SPLIT + 2 LDS words no lane
 // reads any more; y: the block's first row.  Call from every lane of the
 // workgroup after the last write of ylds and a barrier; NOWAIT (test hook)
-// makes every owner give up at once.
+// makes every owner give up at once.  fallbacks (optional): counts the owners
+// that gave up waiting and published their own share (results are exact either
+// way; the count only says which path ran).
 template <typename T, int SPLIT, int VT, uint32_t VRP, bool NOWAIT = false>
 __device__ __forceinline__ void owner_combine(const T* ylds, uint32_t* scratch, T* partial, uint32_t* published,
-                                              uint32_t b, uint32_t h, uint32_t nblocks, uint32_t nr, T* y, int t) {
+                                              uint32_t b, uint32_t h, uint32_t nblocks, uint32_t nr, T* y, int t,
+                                              uint32_t* fallbacks = nullptr) {
   constexpr uint32_t PAIRS = VRP / 2;
   constexpr uint32_t QP = (PAIRS + SPLIT - 1) / SPLIT;  // row pairs per share
   constexpr int NQ = (QP + VT - 1) / VT;                // per lane
@@ -112,7 +115,10 @@ __device__ __forceinline__ void owner_combine(const T* ylds, uint32_t* scratch, 
     publish(h);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t == 0) scratch[SPLIT + 1] = __hip_atomic_fetch_add(published + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) {
+      scratch[SPLIT + 1] = __hip_atomic_fetch_add(published + h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (fallbacks) __hip_atomic_fetch_add(fallbacks, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __syncthreads();
     if (scratch[SPLIT + 1] == (uint32_t)SPLIT - 1) todo |= 1u << h;
   }

@@ -338,6 +338,10 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t c
                     bool by_line = false);
 // Segments build_windowed would make (one pass, no allocation).
 uint64_t windowed_segments(const HostCSR& a, uint32_t log2w);
+// Cost-balanced contiguous row partition (plan.cpp; hipspmv_partition_rows):
+// bounds[parts + 1], interior bounds at multiples of HIPSPMV_SHARD_ALIGN.
+void partition_rows_cost(const uint32_t* rowptr, const uint32_t* colind, uint32_t rows, uint32_t parts,
+                         uint32_t* bounds);
 // Row groups for csr_vector: group g covers rows [groups[g], groups[g+1]).
 void build_row_groups(const HostCSR& a, std::vector<uint32_t>& groups);
 void build_row_groups(const uint32_t* rowptr, uint32_t rows, std::vector<uint32_t>& groups);

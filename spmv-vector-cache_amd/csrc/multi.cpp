@@ -3,8 +3,10 @@
 // bench.py's one-process-per-GPU run.  Built only on the public C ABI (one
 // hipspmv_t per shard) plus the HIP runtime and RCCL.
 //
-//   create: CSC -> CSR once, rows cut into ndev contiguous nnz-balanced
-//           blocks starting at multiples of HIPSPMV_SHARD_ALIGN rows, block i
+//   create: CSC -> CSR once (or a CSR taken as is), rows cut into ndev
+//           contiguous cost-balanced blocks starting at multiples of
+//           HIPSPMV_SHARD_ALIGN rows (hipspmv_partition_rows: entries +
+//           wcsr segments + rows, plan.cpp partition_rows_cost), block i
 //           uploaded to devices[i].
 //   exec:   x host -> devices[0]; broadcast devices[0] -> all others (RCCL
 //           ncclBroadcast over xGMI, one communicator per device, from one
@@ -125,11 +127,10 @@ static void release_multi(hipspmv_multi_t* m) {
   delete m;
 }
 
-static int multi_create(const uint32_t* colptr, const uint32_t* rowind, const void* vals, uint32_t rows,
-                        uint32_t cols, uint32_t nnz, int dtype, const int* devices, int ndev,
-                        hipspmv_multi_t** out) {
-  if (!out || !devices || ndev < 1 || ndev > 64 || !colptr || (nnz && (!rowind || !vals)))
-    return HIPSPMV_ERR_INVALID_ARG;
+template <class Build>
+static int multi_create(uint32_t rows, uint32_t cols, uint32_t nnz, int dtype, const int* devices, int ndev,
+                        hipspmv_multi_t** out, Build&& build) {
+  if (!out || !devices || ndev < 1 || ndev > 64) return HIPSPMV_ERR_INVALID_ARG;
   *out = nullptr;
   if (dtype != HIPSPMV_F64 && dtype != HIPSPMV_U64) return HIPSPMV_ERR_INVALID_ARG;
   if (rows == 0 || cols == 0) return HIPSPMV_ERR_INVALID_ARG;
@@ -143,23 +144,14 @@ static int multi_create(const uint32_t* colptr, const uint32_t* rowind, const vo
   const auto t0 = std::chrono::steady_clock::now();
   HostCSR a;
   std::string why;
-  if (int st = csc_to_csr(colptr, rowind, vals, rows, cols, nnz, a, why)) {
+  if (int st = build(a, why)) {
     set_last_error(why);
     return st;
   }
-  // nnz-balanced contiguous blocks (the rule of host/Synthetic.cpp partitionRows)
+  // cost-balanced contiguous blocks at multiples of HIPSPMV_SHARD_ALIGN, so
+  // every kernel gives the single-device bits (include/hipspmv.h)
   std::vector<uint32_t> bounds(ndev + 1, 0);
-  for (int p = 1; p < ndev; ++p) {
-    const uint64_t target = (uint64_t)nnz * p / ndev;
-    const uint32_t r = (uint32_t)(std::lower_bound(a.rowptr.begin(), a.rowptr.end(), (uint32_t)target) -
-                                  a.rowptr.begin());
-    // blocks start at multiples of HIPSPMV_SHARD_ALIGN (the nearer one), so
-    // every kernel gives the single-device bits (include/hipspmv.h)
-    const uint32_t A = HIPSPMV_SHARD_ALIGN, lo = std::min(r, rows) / A * A;
-    const uint32_t snap = std::min(rows, std::min(r, rows) - lo <= A / 2 ? lo : lo + A);
-    bounds[p] = std::max(snap, bounds[p - 1]);
-  }
-  bounds[ndev] = rows;
+  partition_rows_cost(a.rowptr.data(), a.colind.data(), rows, (uint32_t)ndev, bounds.data());
   auto* m = new hipspmv_multi;
   m->rows = rows;
   m->cols = cols;
@@ -302,13 +294,54 @@ extern "C" {
 int hipspmv_multi_create(const uint32_t* colptr, const uint32_t* rowind, const void* vals, uint32_t rows,
                          uint32_t cols, uint32_t nnz, int dtype, const int* devices, int ndev,
                          hipspmv_multi_t** out) {
+  if (!colptr || (nnz && (!rowind || !vals))) return HIPSPMV_ERR_INVALID_ARG;
   try {
-    return multi_create(colptr, rowind, vals, rows, cols, nnz, dtype, devices, ndev, out);
+    return multi_create(rows, cols, nnz, dtype, devices, ndev, out, [&](HostCSR& a, std::string& why) {
+      return csc_to_csr(colptr, rowind, vals, rows, cols, nnz, a, why);
+    });
   } catch (const std::bad_alloc&) {
     return HIPSPMV_ERR_OOM;
   } catch (...) {
     return HIPSPMV_ERR_INVALID_ARG;
   }
+}
+
+int hipspmv_multi_create_csr(const uint32_t* rowptr, const uint32_t* colind, const void* vals, uint32_t rows,
+                             uint32_t cols, uint32_t nnz, int dtype, const int* devices, int ndev,
+                             hipspmv_multi_t** out) {
+  if (!rowptr || (nnz && (!colind || !vals))) return HIPSPMV_ERR_INVALID_ARG;
+  try {
+    return multi_create(rows, cols, nnz, dtype, devices, ndev, out, [&](HostCSR& a, std::string& why) {
+      return copy_csr(rowptr, colind, vals, rows, cols, nnz, a, why);
+    });
+  } catch (const std::bad_alloc&) {
+    return HIPSPMV_ERR_OOM;
+  } catch (...) {
+    return HIPSPMV_ERR_INVALID_ARG;
+  }
+}
+
+int hipspmv_multi_shard(hipspmv_multi_t* m, int i, hipspmv_t** out) {
+  if (!m || !out || i < 0 || (size_t)i >= m->shards.size()) return HIPSPMV_ERR_INVALID_ARG;
+  *out = m->shards[i].h;  // NULL for a block without rows
+  return HIPSPMV_OK;
+}
+
+int hipspmv_partition_rows(const uint32_t* rowptr, const uint32_t* colind, uint32_t rows, uint32_t cols,
+                           uint32_t parts, uint32_t* bounds) {
+  if (!rowptr || !bounds || parts < 1 || rows == 0) return HIPSPMV_ERR_INVALID_ARG;
+  const uint32_t nnz = rowptr[rows];
+  if (nnz && !colind) return HIPSPMV_ERR_INVALID_ARG;
+  for (uint32_t r = 0; r < rows; ++r)
+    if (rowptr[r] > rowptr[r + 1]) return HIPSPMV_ERR_INVALID_MATRIX;
+  for (uint32_t e = 0; e < nnz; ++e)
+    if (colind[e] >= cols) return HIPSPMV_ERR_INVALID_MATRIX;
+  try {
+    partition_rows_cost(rowptr, colind, rows, parts, bounds);
+  } catch (const std::bad_alloc&) {
+    return HIPSPMV_ERR_OOM;
+  }
+  return HIPSPMV_OK;
 }
 
 int hipspmv_multi_set_option(hipspmv_multi_t* m, const char* key, int64_t value) {

@@ -601,6 +601,50 @@ uint64_t windowed_segments(const HostCSR& a, uint32_t log2w) {
   return s;
 }
 
+// The row partition of a multi-device handle (hipspmv_partition_rows; VERDICT
+// r04 item 3): contiguous blocks of about equal cost, where a row costs
+//   entries + segments + 1
+// in units of one entry's time, with its segments counted exactly as
+// build_windowed cuts them for the wcsr kernel: one per run of the row inside a
+// 2^kWcLog2Window-column window, runs longer than kCvGroupNnz cut into pieces.
+// The unit weights are wcsr's measured costs rounded (per entry, per segment
+// partial, per row of output: 7.08 / 6.77 / 7.51 us per million on an MI355X,
+// profiles/r04/logs/bench_c5_w20.log) -- constants of the kernel, not of a
+// matrix.  On rows of equal shape (the stripe matrices, whose kernels stream
+// entries) the cost is proportional to the entries, so the partition is the
+// entry-balanced one; on R-MAT it charges the short-row blocks their segments
+// and rows (C5: the nnz-balanced cut spread the shard times 1.66x).
+// Interior bounds snap to the nearer multiple of HIPSPMV_SHARD_ALIGN.
+void partition_rows_cost(const uint32_t* rowptr, const uint32_t* colind, uint32_t rows, uint32_t parts,
+                         uint32_t* bounds) {
+  std::vector<double> cum((size_t)rows + 1, 0.0);
+  par_rows(rowptr, rows, [&](unsigned, uint32_t r0, uint32_t r1) {
+    for (uint32_t r = r0; r < r1; ++r) {
+      uint64_t seg = 0;
+      for (uint32_t e = rowptr[r]; e < rowptr[r + 1];) {
+        const uint32_t w = colind[e] >> kWcLog2Window;
+        uint32_t f = e + 1;
+        while (f < rowptr[r + 1] && (colind[f] >> kWcLog2Window) == w) ++f;
+        seg += (f - e + kCvGroupNnz - 1) / kCvGroupNnz;
+        e = f;
+      }
+      cum[(size_t)r + 1] = (double)(rowptr[r + 1] - rowptr[r]) + (double)seg + 1.0;
+    }
+  });
+  for (uint32_t r = 0; r < rows; ++r) cum[(size_t)r + 1] += cum[r];
+  const uint32_t A = HIPSPMV_SHARD_ALIGN;
+  bounds[0] = 0;
+  for (uint32_t p = 1; p < parts; ++p) {
+    const double target = cum[rows] * p / parts;
+    uint32_t r = (uint32_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+    r = std::min(r, rows);
+    const uint32_t lo = r / A * A;
+    const uint32_t snap = std::min(rows, r - lo <= A / 2 ? lo : lo + A);
+    bounds[p] = std::max(snap, bounds[p - 1]);
+  }
+  bounds[parts] = rows;
+}
+
 // In parallel over entry-balanced row ranges (thread t: rows [rb[t], rb[t+1])):
 // a window's segments are numbered by rows ascending, so thread t's first
 // segment of window w follows every earlier thread's segments of w.

@@ -69,6 +69,12 @@ struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane
 // 256 / 512 / 1024 / 2048 / 4096: the entries of row blocks b >= nblocks/2,
 // 5/8, 3/8, 1/4, 1/8 loaded
 // non-temporally (Infinity-Cache residency experiment).
+// 8192 (with 64; diagnostic, tools/step_trace.hip): step trace -- lane 0 of every
+// wave stores {ready, arrive, release, applied} (s_memtime low words: its data
+// landed, it reached the step barrier, the barrier let it go, its LDS apply
+// retired -- compute waves) of every step, as uint4
+// at partial + 16 * ((blockIdx.x * 16 + wave) * 256 + step); step slot 255: {kernel
+// entry, 0, release of the prologue barrier}.
 template <typename T, int SPLIT, int WL = VcCfg<SPLIT>::WL, int DE = VcCfg<SPLIT>::DE, int EPT = VcCfg<SPLIT>::EPT,
           int AB = 0, int MAP = 0, bool NT = false, int LD = 0, int CX = 0>
 __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restrict__ seg,
@@ -333,6 +339,22 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       barrier();
     }
   };
+  // step trace (AB & 8192): stamps, and the store after each step barrier
+  auto tr_now = [] {
+    asm volatile("" ::: "memory");
+    const uint32_t v = (uint32_t)__builtin_amdgcn_s_memtime();
+    asm volatile("" ::: "memory");
+    return v;
+  };
+  const uint32_t t_entry = (AB & 8192) ? tr_now() : 0;
+  auto tr_rel = [&](uint32_t s, uint32_t a, uint32_t b, uint32_t c = 0) {
+    if (!(AB & 8192)) return;
+    const uint32_t r = tr_now();
+    if ((t & 63) == 0)
+      reinterpret_cast<uint4*>(partial)[((size_t)blockIdx.x * 16 + (uint32_t)(t >> 6)) * 256 + min(s, 255u)] =
+          make_uint4(a, b, r, c);
+  };
+  static_assert(!(AB & 8192) || (AB & 64), "the step trace lives in the partials: no combine");
   // CX >= 2: both roles run a step count padded to the unroll (extra steps do
   // no work but keep their loads and barrier), so no loop exits mid-group.
   // An early exit inside the unrolled group is what makes hipcc's waitcnt
@@ -350,6 +372,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     patch_x(0);
     barrier();
+    tr_rel(255, t_entry, 0);
     if (AB & 128) {
       stamp(1, now());
       pf_mark = __builtin_amdgcn_s_memtime();
@@ -357,8 +380,10 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     for (uint32_t s = 0; s < nsteps; ++s) {
       if (s + 1 < npu) dma_x(s + 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t t_ready = (AB & 8192) ? tr_now() : 0;
       if (s + 1 < npu) patch_x(s + 1);
       pbarrier();
+      tr_rel(s, t_ready, t_ready);
     }
   } else if (loader && LD == 2) {
     // same ring, asm loads: storing x(s+1) waits for it with x(s+2)'s NJ
@@ -415,6 +440,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
 #pragma unroll
       for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i], ntc);
       barrier();
+      tr_rel(255, t_entry, 0);
       if (AB & 128) pf_mark = __builtin_amdgcn_s_memtime();
       for (uint32_t base = 0; base < nsteps; base += DE) {
 #pragma unroll
@@ -422,13 +448,24 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
           const uint32_t s = base + i;
           if (!PAD && s >= npu) break;
           if (CX == 2) vm_wait<(AB & 4) ? 0 : (DE - 1) * 2 * EPT>();  // slot i landed, DE-1 steps still in flight
+          uint32_t t_ready = 0, t_arr = 0, t_app = 0;
+          if (AB & 8192) {  // this step's entries landed: each later step issued 2 * EPT loads + 1 trace store
+            vm_wait<1 + (2 * EPT + 1) * (DE - 1)>();
+            t_ready = tr_now();
+          }
           if (CX) {
             if (!PAD || s < npu) apply_cx(s, EC[i], EV[i]);
           } else {
             apply(s, EC[i], EV[i]);
           }
+          if (AB & 8192) {  // the apply's LDS work retired, then the next loads issued
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            t_app = tr_now();
+          }
           load_e(s + DE, EC[i], EV[i], ntc);
+          if (AB & 8192) t_arr = tr_now();
           pbarrier();
+          tr_rel(s, t_ready, t_arr, t_app);
         }
       }
       if (CX == 2) vm_wait<0>();  // the clamped prefetches past the last panel

@@ -41,6 +41,7 @@
 #include "device_common.h"
 #include "hipspmv_internal.h"
 #include "kernels.h"
+#include "vc_map.h"
 
 namespace hipspmv {
 
@@ -82,6 +83,19 @@ __device__ __forceinline__ T bld_64_nt(u32x4d d, uint32_t off) {
   asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt" : "=v"(r) : "v"(off), "s"(d) : "memory");
   return __builtin_bit_cast(T, r);
 }
+// the same loads with the default policy: the lines allocate in the Infinity
+// Cache and stay there across launches
+__device__ __forceinline__ uint32_t bld_u32(u32x4d d, uint32_t off) {
+  uint32_t r;
+  asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(r) : "v"(off), "s"(d) : "memory");
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ T bld_64(u32x4d d, uint32_t off) {
+  uint64_t r;
+  asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(r) : "v"(off), "s"(d) : "memory");
+  return __builtin_bit_cast(T, r);
+}
 
 constexpr uint32_t gcd_u(uint32_t a, uint32_t b) { return b ? gcd_u(b, a % b) : a; }
 constexpr uint32_t lcm_u(uint32_t a, uint32_t b) { return a / gcd_u(a, b) * b; }
@@ -92,8 +106,15 @@ constexpr uint32_t lcm_u(uint32_t a, uint32_t b) { return a / gcd_u(a, b) * b; }
 // 2 no x stores into LDS, 4 no combine (each part writes its own rows), 8 no
 // step barrier, 16 x loads by LDS-DMA into the slots (timing only: DX > 1
 // panels in flight overwrite each other), 32 no x loads, 64 no entry loads;
-// 128 (results exact: the test of the combine's fallback) owners never wait
-template <typename T, int WL, int DX, int DE, int EPT, int AB = 0>
+// 128 (results exact: the test of the combine's fallback) owners never wait.
+// MAP 1: XCD-aware placement (csrc/vc_map.h: part h on XCDs 2h, 2h+1, so each
+// XCD's L2 serves one quarter of x).  NTR: row blocks b < nt_from load their
+// entries with the default policy (Infinity-Cache resident across launches),
+// the others non-temporally (NTR 0: all non-temporal).  YADD: an owner adds
+// its products to its y row with one LDS atomic (ds_add_f64 / ds_add_u64)
+// instead of a read and a write -- the same one update per row and step, so
+// the result is still deterministic.
+template <typename T, int WL, int DX, int DE, int EPT, int AB = 0, int MAP = 0, bool NTR = false, bool YADD = false>
 __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict__ seg,
                                                        const uint32_t* __restrict__ ecode,
                                                        const T* __restrict__ evals, const T* __restrict__ x,
@@ -101,7 +122,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
                                                        T* __restrict__ partial, uint32_t* __restrict__ tickets,
                                                        uint32_t* __restrict__ status, uint32_t rows, uint32_t cols,
                                                        uint32_t rows_per_block, uint32_t nblocks, uint32_t npanels,
-                                                       uint32_t npad, uint32_t last, int beta) {
+                                                       uint32_t npad, uint32_t last, int beta, uint32_t nt_from) {
 #pragma clang fp contract(off)
   constexpr int VT = kVcThreads, NW = VT / 64, WC = NW - WL;
   constexpr int LT = WL * 64, CT = WC * 64;
@@ -118,9 +139,15 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
   const uint32_t wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const bool loader = wv < (uint32_t)WL;  // wave-uniform role
   // unit i -> (b, h): the parts of a block are 8 dispatch slots apart
-  const uint32_t g8 = blockIdx.x / (8 * SPLIT), rem = blockIdx.x % (8 * SPLIT);
-  const uint32_t nbg = min(8u, nblocks - g8 * 8);
-  const uint32_t h = rem / nbg, b = g8 * 8 + rem % nbg;
+  uint32_t h, b;
+  if (MAP == 1 && vc_map1_applies<SPLIT>(nblocks)) {
+    vc_unit_map1<SPLIT>(blockIdx.x, b, h);
+  } else {
+    const uint32_t g8 = blockIdx.x / (8 * SPLIT), rem = blockIdx.x % (8 * SPLIT);
+    const uint32_t nbg = min(8u, nblocks - g8 * 8);
+    h = rem / nbg;
+    b = g8 * 8 + rem % nbg;
+  }
   const uint32_t r0 = b * rows_per_block;
   if (r0 >= rows) return;  // never with a vcache_grid_ok geometry (workgroup-uniform, before any barrier)
   const uint32_t nr = min(rows_per_block, rows - r0);
@@ -217,6 +244,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
                    ne = __builtin_amdgcn_readfirstlane(segl[npu]) - e0;  // wave-uniform: SGPR descriptors
     const u32x4d dcode = buf_desc(ecode + e0, 4 * ne), dvals = buf_desc(evals + e0, 8 * ne);
     uint32_t SB[DE], SE[DE];  // each ring slot's segment bounds (unit-relative), read once from LDS
+    auto entries = [&](auto ntc) {
     auto issue = [&](uint32_t s, uint32_t* c, T* v, uint32_t& sb, uint32_t& se) {
       const uint32_t beg = segl[min(s, npad)] - e0, end = segl[min(s + 1, npad)] - e0;
       sb = beg;
@@ -226,8 +254,13 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
       for (int j = 0; j < EPT; ++j) {
         const uint32_t q = beg + ct + j * CT;
         const bool in = q < end;
-        c[j] = bld_u32_nt(dcode, in ? 4 * q : 0x80000000u);
-        v[j] = bld_64_nt<T>(dvals, in ? 8 * q : 0x80000000u);
+        if constexpr (decltype(ntc)::value) {
+          c[j] = bld_u32_nt(dcode, in ? 4 * q : 0x80000000u);
+          v[j] = bld_64_nt<T>(dvals, in ? 8 * q : 0x80000000u);
+        } else {
+          c[j] = bld_u32(dcode, in ? 4 * q : 0x80000000u);
+          v[j] = bld_64<T>(dvals, in ? 8 * q : 0x80000000u);
+        }
       }
     };
     // step s over the build_vcache_lanes placement (lane ct holds positions ct
@@ -249,7 +282,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
         p[j] = valid ? v[j] * xs[c[j] & 0xFFF] : T(0);  // rounded product (contract off)
         own[j] = valid && !(c[j] & kVcCont);
         row[j] = (c[j] >> 12) & 0x3FFF;
-        acc[j] = own[j] ? ylds[row[j]] + p[j] : T(0);
+        acc[j] = own[j] ? (YADD ? p[j] : ylds[row[j]] + p[j]) : T(0);
       }
       if (own[0] && (c[0] & kVqLMore)) acc[0] = acc[0] + p[1];  // the lane's pair
 #pragma unroll
@@ -263,7 +296,12 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
             more = (ck & kVcMore) != 0;
           }
         }
-        if (own[j]) ylds[row[j]] = acc[j];
+        if (own[j]) {
+          if (YADD)
+            __hip_atomic_fetch_add(&ylds[row[j]], acc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          else
+            ylds[row[j]] = acc[j];
+        }
       }
     };
 #pragma unroll
@@ -295,6 +333,11 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
         tie(EC[d][j]);
         tie(EV[d][j]);
       }
+    };
+    if (!NTR || b >= nt_from)
+      entries(std::true_type{});
+    else
+      entries(std::false_type{});
   }
   if (AB & 4) {
     __syncthreads();
@@ -304,15 +347,15 @@ __global__ __launch_bounds__(kVcThreads) void k_vquad(const uint32_t* __restrict
   // ---- combine: unit h owns quarter h of the block's rows (csrc/combine.h)
   __syncthreads();  // the entry waves' last (clamped) issue read segl after the final step barrier
   owner_combine<T, SPLIT, VT, (VR + 1) & ~1u, (AB & 128) != 0>(ylds, segl, partial, tickets + (size_t)SPLIT * b, b, h,
-                                                               nblocks, nr, y_out + r0, t);
-  (void)status;  // no hand-off can time out into unpublished reads: the word stays 0
+                                                               nblocks, nr, y_out + r0, t, status);
 }
 
-template <typename T, int WL, int DX, int DE, int AB = 0>
+template <typename T, int WL, int DX, int DE, int AB = 0, int MAP = 0, bool NTR = false, bool YADD = false>
 static void launch_cfg(const VcacheArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_vquad<T, WL, DX, DE, 2, AB>), dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s, a.seg, a.code,
-                     (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets,
-                     a.status, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.npad, a.last, a.beta);
+  hipLaunchKernelGGL((k_vquad<T, WL, DX, DE, 2, AB, MAP, NTR, YADD>), dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s,
+                     a.seg, a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial,
+                     a.tickets, a.status, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.npad, a.last,
+                     a.beta, a.nt_from);
 }
 
 // the register window (entries one step holds) of configuration v
@@ -334,6 +377,13 @@ static hipError_t launch_vquad_t(const VcacheArgs& a, hipStream_t s) {
     case 18: launch_cfg<T, 3, 2, 4>(a, s); break;
     case 19: launch_cfg<T, 3, 4, 5>(a, s); break;
     case 20: launch_cfg<T, 3, 3, 6, 128>(a, s); break;  // exact: every owner gives up waiting
+    // round 5: XCD map (21), Infinity-Cache resident entries below nt_from (22, 23), LDS atomic y updates (24-26)
+    case 21: launch_cfg<T, 3, 3, 6, 0, 1>(a, s); break;
+    case 22: launch_cfg<T, 3, 3, 6, 0, 1, true>(a, s); break;
+    case 23: launch_cfg<T, 3, 3, 6, 0, 0, true>(a, s); break;
+    case 24: launch_cfg<T, 3, 3, 6, 0, 1, false, true>(a, s); break;
+    case 25: launch_cfg<T, 3, 3, 6, 0, 1, true, true>(a, s); break;
+    case 26: launch_cfg<T, 3, 3, 6, 0, 0, false, true>(a, s); break;
     // ablations (timing probes, wrong y): 6 no apply, 7 no x stores, 8 no combine,
     // 9 no apply and no x stores, 10 no step barriers (races), 11 skeleton (1|2|4),
     // 12 skeleton entries only, 13 skeleton x only, 14 skeleton x by LDS-DMA,

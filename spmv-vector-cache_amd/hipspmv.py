@@ -114,12 +114,15 @@ def load_hipspmv() -> C.CDLL:
     ip = C.POINTER(C.c_int)
     lib.hipspmv_multi_create.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, ip, C.c_int,
                                          C.POINTER(vp)]
+    lib.hipspmv_multi_create_csr.argtypes = lib.hipspmv_multi_create.argtypes
+    lib.hipspmv_multi_shard.argtypes = [vp, C.c_int, C.POINTER(vp)]
+    lib.hipspmv_partition_rows.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp]
     lib.hipspmv_multi_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
     lib.hipspmv_multi_exec.argtypes = [vp, vp, vp, C.c_int, C.c_int]
     lib.hipspmv_multi_stat.argtypes = [vp, C.c_char_p, C.POINTER(C.c_uint64)]
     lib.hipspmv_multi_destroy.argtypes = [vp]
-    for name in ("hipspmv_multi_create", "hipspmv_multi_set_option", "hipspmv_multi_exec", "hipspmv_multi_stat",
-                 "hipspmv_multi_destroy"):
+    for name in ("hipspmv_multi_create", "hipspmv_multi_create_csr", "hipspmv_multi_shard", "hipspmv_partition_rows",
+                 "hipspmv_multi_set_option", "hipspmv_multi_exec", "hipspmv_multi_stat", "hipspmv_multi_destroy"):
         getattr(lib, name).restype = C.c_int
     for name in ("hipspmv_create", "hipspmv_create_csr", "hipspmv_set_option", "hipspmv_exec",
                  "hipspmv_exec_device", "hipspmv_stat", "hipspmv_destroy", "hipspmv_abi_version",
@@ -268,9 +271,18 @@ class Handle:
         hazard_stalls / capacity_stalls (include/hipspmv.h); None detaches."""
         _check(self._lib.hipspmv_attach_pmc(self._h, (csv_path or "").encode()), "attach_pmc")
 
+    @classmethod
+    def _borrowed(cls, h, rows: int, cols: int, nnz: int, dtype: int, device: int):
+        """A view of a handle owned elsewhere (a MultiHandle block): never destroyed here."""
+        self = cls.__new__(cls)
+        self.rows, self.cols, self.nnz, self.dtype, self.device = rows, cols, nnz, dtype, device
+        self._h, self._lib, self._owner = h, load_hipspmv(), False
+        return self
+
     def close(self) -> None:
         if getattr(self, "_h", None):
-            self._lib.hipspmv_destroy(self._h)
+            if getattr(self, "_owner", True):
+                self._lib.hipspmv_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -302,25 +314,38 @@ def mark_row_starts(rowind: np.ndarray, rows: int, reverse: bool = False, shift:
 
 
 class MultiHandle:
-    """One CSC matrix row-partitioned over several devices of this process
-    (`hipspmv_multi_t`): x broadcast device to device, one block per device."""
+    """One matrix row-partitioned over several devices of this process
+    (`hipspmv_multi_t`): x broadcast device to device, one block per device.
+    CSC input (SparseMatrix) by default, CSR with csr=True."""
 
-    def __init__(self, colptr, rowind, vals, rows: int, cols: int, devices):
+    def __init__(self, ptr, ind, vals, rows: int, cols: int, devices, *, csr: bool = False):
         lib = load_hipspmv()
-        self._keep = [np.ascontiguousarray(colptr, dtype=np.uint32), np.ascontiguousarray(rowind, dtype=np.uint32),
+        self._keep = [np.ascontiguousarray(ptr, dtype=np.uint32), np.ascontiguousarray(ind, dtype=np.uint32),
                       np.ascontiguousarray(vals)]
-        if self._keep[0].size != cols + 1 or self._keep[2].size != self._keep[1].size:
-            raise ValueError("colptr needs cols + 1 entries and one value per row index")
+        if self._keep[0].size != (rows if csr else cols) + 1 or self._keep[2].size != self._keep[1].size:
+            raise ValueError(f"{'rowptr needs rows' if csr else 'colptr needs cols'} + 1 entries and one value "
+                             "per index")
         if self._keep[2].dtype not in (np.float64, np.uint64):
             raise TypeError("values must be float64 or uint64")
         self.dtype = self._keep[2].dtype
         self.rows, self.cols = rows, cols
+        self.devices = list(devices)
         devs = (C.c_int * len(devices))(*devices)
         self._h = C.c_void_p()
-        _check(lib.hipspmv_multi_create(_ptr(self._keep[0]), _ptr(self._keep[1]), _ptr(self._keep[2]), rows, cols,
-                                        self._keep[1].size, U64 if self.dtype == np.uint64 else F64, devs,
-                                        len(devices), C.byref(self._h)), "multi_create")
+        fn = lib.hipspmv_multi_create_csr if csr else lib.hipspmv_multi_create
+        _check(fn(_ptr(self._keep[0]), _ptr(self._keep[1]), _ptr(self._keep[2]), rows, cols,
+                  self._keep[1].size, U64 if self.dtype == np.uint64 else F64, devs,
+                  len(devices), C.byref(self._h)), "multi_create")
         self._keep = None
+
+    def shard(self, i: int):
+        """Block i's own Handle (owned by this MultiHandle; None for a block without rows)."""
+        h = C.c_void_p()
+        _check(load_hipspmv().hipspmv_multi_shard(self._h, i, C.byref(h)), "multi_shard")
+        if not h.value:
+            return None
+        return Handle._borrowed(h, self.stat(f"shard{i}_rows"), self.cols, self.stat(f"shard{i}_nz"),
+                                U64 if self.dtype == np.uint64 else F64, self.devices[i])
 
     def set_option(self, key: str, value: int) -> None:
         _check(load_hipspmv().hipspmv_multi_set_option(self._h, key.encode(), value), f"multi_set_option({key})")
@@ -504,6 +529,18 @@ def csr2csc(rows: int, cols: int, rowptr, colind, vals):
     lib.spmvhost_csr2csc(rows, cols, nnz, v, np.ascontiguousarray(colind, dtype=np.uint32),
                          np.ascontiguousarray(rowptr, dtype=np.uint32), out, rowind, colptr)
     return colptr, rowind, out.view(vals.dtype)
+
+
+def partition_rows_cost(rowptr: np.ndarray, colind: np.ndarray, cols: int, parts: int) -> np.ndarray:
+    """The library's row partition (hipspmv_partition_rows, the one
+    hipspmv_multi_create uses): cost-balanced contiguous blocks, a row costing
+    entries + wcsr segments + 1; bounds[parts + 1] as uint32."""
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.uint32)
+    colind = np.ascontiguousarray(colind, dtype=np.uint32)
+    bounds = np.empty(parts + 1, dtype=np.uint32)
+    _check(load_hipspmv().hipspmv_partition_rows(_ptr(rowptr), _ptr(colind), rowptr.size - 1, cols, parts,
+                                                 _ptr(bounds)), "partition_rows")
+    return bounds
 
 
 def partition_rows(rowptr: np.ndarray, parts: int) -> np.ndarray:

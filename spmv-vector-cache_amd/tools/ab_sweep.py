@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""A/B timing of FAST kernel configurations on C3 in the chip's steady state
+(DESIGN.md §6.14).  Diagnostic only.
+
+The first ~150 launches after an idle GPU run slower (a DVFS transient,
+tools/warm_probe.py), so the sweep first runs 400 launches, then
+times every configuration in interleaved rounds: per round and configuration,
+10 untimed launches and N timed ones between one HIP event pair.  Each
+configuration's result is checked once against the ORDERED kernel (bit-exact
+to SoftwareSpMV, tests/test_gpu_parity.py) within the FAST bound, and for
+determinism (two launches, identical bits).
+
+usage: ab_sweep.py [--set NAME] [--reps N] [--rounds R]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import hipspmv as hs  # noqa: E402
+
+SETS = {
+    # round 5: k_vquad's XCD map, Infinity-Cache resident entries, LDS atomic y updates
+    "vquad": [("split (product)", "vcache_split", {}),
+              ("vquad v0", "vcache_split4", {"vquad_variant": 0}),
+              ("vquad map", "vcache_split4", {"vquad_variant": 21}),
+              ("vquad map res 1/4", "vcache_split4", {"vquad_variant": 22, "vcache_nt": 16}),
+              ("vquad map res 3/8", "vcache_split4", {"vquad_variant": 22, "vcache_nt": 24}),
+              ("vquad map res 1/2", "vcache_split4", {"vquad_variant": 22, "vcache_nt": 32}),
+              ("vquad res 1/4", "vcache_split4", {"vquad_variant": 23, "vcache_nt": 16}),
+              ("vquad res 1/2", "vcache_split4", {"vquad_variant": 23, "vcache_nt": 32}),
+              ("vquad map yadd", "vcache_split4", {"vquad_variant": 24}),
+              ("vquad map res 1/4 yadd", "vcache_split4", {"vquad_variant": 25, "vcache_nt": 16}),
+              ("vquad yadd", "vcache_split4", {"vquad_variant": 26})],
+}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--set", default="vquad")
+    p.add_argument("--reps", type=int, default=100)
+    p.add_argument("--rounds", type=int, default=3)
+    a = p.parse_args()
+    n = 1 << 20
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32, 1, 2)
+    x = hs.gen_vector(n, 3)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    alg = h.stat("alg_bytes")
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.empty(n, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream()
+    h.set_kernel("vcache")
+    h.exec_device(xd, yd, beta=0, mode=hs.MODE_ORDERED, stream=s)
+    y_ref = yd.cpu().numpy().copy()
+    lens = np.diff(rowptr.astype(np.int64))
+    absprod = np.bincount(np.repeat(np.arange(n), lens), weights=np.abs(vals * x[colind]), minlength=n)
+    bound = 2.0 * lens * 2.0 ** -53 * absprod + 1e-300
+
+    cfgs = SETS[a.set]
+
+    def select(kernel, opts):
+        h.set_kernel(kernel)
+        for k, v in opts.items():
+            h.set_option(k, v)
+
+    def reset(opts):
+        for k in opts:
+            h.set_option(k, {"vquad_variant": 0, "vcache_nt": -1}.get(k, -1))
+
+    def run(k):
+        for _ in range(k):
+            h.exec_device(xd, yd, beta=0, mode=hs.MODE_FAST, stream=s)
+
+    checks = {}
+    for label, kernel, opts in cfgs:
+        select(kernel, opts)
+        run(1)
+        y1 = yd.cpu().numpy().copy()
+        run(1)
+        y2 = yd.cpu().numpy().copy()
+        r = np.abs(y1 - y_ref) / bound
+        checks[label] = {"within_bound": bool(np.all(r <= 1.0)), "max_err_over_bound": round(float(r.max()), 3),
+                         "deterministic": y1.tobytes() == y2.tobytes()}
+        reset(opts)
+    h.set_kernel("vcache_split")
+    run(400)
+    torch.cuda.synchronize()
+    times = {c[0]: [] for c in cfgs}
+    for rnd in range(a.rounds):
+        for label, kernel, opts in cfgs:
+            select(kernel, opts)
+            run(10)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            run(a.reps)
+            e1.record(s)
+            torch.cuda.synchronize()
+            times[label].append(e0.elapsed_time(e1) * 1e3 / a.reps)
+            reset(opts)
+        print(f"round {rnd} done", file=sys.stderr, flush=True)
+    for label, _, _ in cfgs:
+        us = float(np.median(times[label]))
+        print(f"{label:28s} {us:8.2f} us  frac {alg / (us * 1e-6) / 8e12:.4f}  "
+              f"rounds {' '.join(f'{t:.1f}' for t in times[label])}  {json.dumps(checks[label])}", flush=True)
+    h.close()
+
+
+if __name__ == "__main__":
+    main()
