@@ -100,7 +100,8 @@ def parse():
     p.add_argument("--c5-scale", type=int, default=24, help="log2 of the C5 block's R-MAT dimension (C5: 24)")
     p.add_argument("--c5-parts", type=int, default=8)
     p.add_argument("--c5-partition", default="cost", choices=["cost", "nnz"],
-                   help="C5 row partition: wcsr cost model (entries + segments + rows) or nonzeros only")
+                   help="C5 row partition: the library's (hipspmv_partition_rows: entries + wcsr segments + rows, "
+                        "counted on the matrix) or nonzeros only")
     p.add_argument("--c5-steps", type=int, default=50)
     p.add_argument("--parity-rows", type=int, default=2000,
                    help="rows of each rank's shard recomputed by the oracle after timing (per-rank parity)")
@@ -149,15 +150,20 @@ def traffic_from_csv(paths, kernel_substr):
 COPY_BYTES = 1 << 30  # 1 GiB each way: far beyond the 256 MiB Infinity Cache
 
 
-def hbm_copy_gbs(dev, reps: int = 10) -> float:
-    """Measured HBM ceiling on this GPU: a device-to-device copy of `nbytes`
-    (read + write counted), the second denominator SURVEY §8(d) asks for."""
+def hbm_copy_gbs(dev, reps: int = 10):
+    """Measured HBM ceiling on this GPU, the second denominator SURVEY §8(d)
+    asks for: the in-tree streaming kernels (hipspmv_stream_bandwidth, csrc/
+    stream.hip: 16-byte non-temporal grid-stride copy and read of 1 GiB
+    buffers, far beyond the 256 MiB Infinity Cache).  Returns (copy GB/s,
+    read + write counted; read GB/s; source).  Without a GPU (the CPU tests'
+    stand-ins) a torch copy is timed instead and the source says so."""
+    if dev.type == "cuda":
+        cp, rd = hs.stream_bandwidth(dev.index or 0, COPY_BYTES, reps)
+        return cp, rd, "hipspmv_stream_bandwidth (csrc/stream.hip), 1 GiB buffers"
     nbytes = COPY_BYTES
     src = torch.empty(nbytes // 8, dtype=torch.float64, device=dev)
     dst = torch.empty_like(src)
     src.fill_(1.0)
-    for _ in range(2):
-        dst.copy_(src)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
@@ -165,9 +171,7 @@ def hbm_copy_gbs(dev, reps: int = 10) -> float:
     e1.record()
     torch.cuda.synchronize()
     gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del src, dst
-    torch.cuda.empty_cache()
-    return gbs
+    return gbs, None, "torch copy_ (no GPU)"
 
 
 ROCPROF_DIR = os.path.join("gpurun_out", "rocprof_bench")
@@ -536,17 +540,36 @@ def run_strong(a, dist, dev, local: int, rank: int, world: int, stream) -> dict:
             "setup_ns_lib": setup_ns, "setup_phases_ns": phases}
 
 
+def c5_matrix(scale: int, parts: int, model: str):
+    """The whole C5 matrix (R-MAT scale `scale`, edge factor 16, hs.gen_rmat_csr) and its row partition:
+    "cost" is the library's own (hipspmv_partition_rows -- the partition hipspmv_multi_create uses: a row
+    costs its entries + its wcsr segments + 1, counted on this matrix's layout), "nnz" balances entries.
+    Returns (rowptr, colind, vals, bounds, gen_s, partition_s)."""
+    t = time.perf_counter()
+    rowptr, colind, vals = hs.gen_rmat_csr(scale, 16, 4)
+    gen_s = time.perf_counter() - t
+    t = time.perf_counter()
+    bounds = (hs.partition_rows_cost(rowptr, colind, 1 << scale, parts) if model == "cost"
+              else hs.partition_rows(rowptr, parts))
+    return rowptr, colind, vals, bounds, gen_s, time.perf_counter() - t
+
+
+def csr_slice(rowptr, colind, vals, row0: int, row1: int):
+    """Rows [row0, row1) of a CSR, rowptr rebased to 0 (colind / vals are views)."""
+    e0, e1 = int(rowptr[row0]), int(rowptr[row1])
+    rp = (rowptr[row0:row1 + 1].astype(np.int64) - e0).astype(np.uint32)
+    return rp, colind[e0:e1], vals[e0:e1]
+
+
 def run_c5_shards(a, dev, stream) -> dict:
     """SURVEY §8(d)'s C5 row on one GPU: R-MAT scale s (24: C5), edge factor 16, cut into --c5-parts row
-    shards by the wcsr cost model (hipspmv.c5_partition), and every shard run on this GPU in turn: AUTO's
+    shards by the library's partition (hipspmv_partition_rows, c5_matrix), and every shard run on this GPU in turn: AUTO's
     FAST kernel, its per-launch time (HIP events over --c5-steps back-to-back launches after a warmup),
     alg bytes and roofline fraction, and sampled rows against the oracle.  max/min of the shard times is
     the load balance an 8-GPU C5 step would see (the slowest rank sets it); value = all shards' flops /
     the slowest shard's time (the N-GPU strong-scaling estimate from one GPU, x replicated)."""
     parts, scale = a.c5_parts, a.c5_scale
-    t0 = time.perf_counter()
-    bounds, counts = hs.c5_partition(scale, parts, model=a.c5_partition)
-    part_s = time.perf_counter() - t0
+    full_rowptr, full_colind, full_vals, bounds, full_gen_s, part_s = c5_matrix(scale, parts, a.c5_partition)
     n = 1 << scale
     x = torch.from_numpy(hs.gen_vector(n, 3)).to(dev)
     shards = []
@@ -556,9 +579,7 @@ def run_c5_shards(a, dev, stream) -> dict:
         if row1 == row0:  # a tiny matrix snapped to SHARD_ALIGN rows can leave a shard empty
             shards.append({"shard": r, "rows": [row0, row1], "nnz": 0, "kernel": None})
             continue
-        tg = time.perf_counter()
-        rowptr, colind, vals = hs.gen_rmat_rows(scale, row0, row1, 16, 4)
-        gen_s = time.perf_counter() - tg
+        rowptr, colind, vals = csr_slice(full_rowptr, full_colind, full_vals, row0, row1)
         ts = time.perf_counter()
         h = hs.Handle.from_csr(rowptr, colind, vals, row1 - row0, n, device=dev.index or 0)
         setup_s = time.perf_counter() - ts
@@ -580,14 +601,16 @@ def run_c5_shards(a, dev, stream) -> dict:
         shards.append({"shard": r, "rows": [row0, row1], "nnz": int(colind.size), "kernel": kname,
                        "kernel_us": round(us, 3), "roofline_frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                        "segments": h.stat("wcsr_segments") if kname == "wcsr" else None,
-                       "parity": parity, "gen_s": round(gen_s, 2), "setup_s": round(setup_s, 2)})
+                       "parity": parity, "setup_s": round(setup_s, 2)})
         total_nnz += int(colind.size)
         h.close()
         del y
         torch.cuda.empty_cache()
+    del full_rowptr, full_colind, full_vals
     times = [s["kernel_us"] for s in shards if s["kernel"]]
     return {"workload": f"C5 R-MAT scale {scale} (a,b,c=0.57,0.19,0.19), edge factor 16, {parts} row shards "
-                        f"({a.c5_partition} partition), each run alone on this GPU", "mode": "fast",
+                        f"({'library hipspmv_partition_rows' if a.c5_partition == 'cost' else 'nnz'} partition), "
+                        f"each run alone on this GPU", "mode": "fast", "gen_s": round(full_gen_s, 2),
             "nnz_total": total_nnz, "max_over_min": round(max(times) / min(times), 4),
             "slowest_us": max(times), "min_roofline_frac": min(s["roofline_frac"] for s in shards if s["kernel"]),
             "value": round(2.0 * total_nnz / (max(times) * 1e-6) / 1e9, 2), "unit": "GFLOP/s",
@@ -660,13 +683,19 @@ def main():
         scaling = "strong"
     else:
         n = 1 << a.scale
-        # the cost partition of the c5_shards block (wcsr's measured cost model), or --c5-partition nnz
-        bounds, _ = hs.c5_partition(a.scale, pworld, model=a.c5_partition)
+        # the library's partition (hipspmv_partition_rows, as hipspmv_multi_create cuts), or --c5-partition
+        # nnz; every rank builds the whole matrix and keeps its rows
+        full = c5_matrix(a.scale, pworld, a.c5_partition)
+        bounds = full[3]
         row0, row1 = int(bounds[prank]), int(bounds[prank + 1])
         rows, cols = row1 - row0, n
-        rowptr, colind, vals = hs.gen_rmat_rows(a.scale, row0, row1, 16, 4)
+        rowptr, colind, vals = (np.ascontiguousarray(v) for v in csr_slice(*full[:3], row0, row1))
+        del full
+        if rows == 0:
+            raise SystemExit(f"C5 scale {a.scale} over {pworld} ranks leaves rank {prank} no rows "
+                             f"(blocks start at multiples of {hs.SHARD_ALIGN}): use a larger --scale")
         workload = (f"C5 R-MAT scale {a.scale} (a,b,c=0.57,0.19,0.19), edge factor 16, "
-                    f"{pworld} row blocks ({a.c5_partition} partition)")
+                    f"{pworld} row blocks ({'library' if a.c5_partition == 'cost' else 'nnz'} partition)")
         scaling = "strong"
     if a.shard:
         workload += f" -- shard {prank} of {pworld} alone on one GPU (rows [{row0},{row1}))"
@@ -738,9 +767,9 @@ def main():
     y_main = yd.cpu().numpy().copy()
     launch_us = per_launch_us(mode)
     if a.rocprof_child:  # only the SpMV kernel in the profiler's table
-        copy_gbs, h2d_us, d2h_us = 0.0, 0.0, 0.0
+        copy_gbs, read_gbs, copy_src, h2d_us, d2h_us = 0.0, None, None, 0.0, 0.0
     else:
-        copy_gbs = hbm_copy_gbs(dev)
+        copy_gbs, read_gbs, copy_src = hbm_copy_gbs(dev)
         h2d_us, d2h_us = host_transfer_us(xd, yd)
     ms_per_step = wall_max / a.steps * 1e3
     alg_bytes = h.stat("alg_bytes")  # 12*nnz + 4*(rows+1) + 8*cols + 8*rows per launch
@@ -879,11 +908,17 @@ def main():
                          "kernel": "k_" + kname, "alg_bytes_per_launch": alg_bytes,
                          "kernel_us": round(kern_ms * 1e3, 3), "kernel_us_per_launch": launch_us,
                          "measured_copy_gbs": round(copy_gbs, 1),
-                         "frac_of_measured_copy": round(achieved / copy_gbs, 4) if copy_gbs > 0 else None},
+                         "frac_of_measured_copy": round(achieved / copy_gbs, 4) if copy_gbs > 0 else None,
+                         "measured_read_gbs": None if not read_gbs else round(read_gbs, 1),
+                         "frac_of_measured_read": round(achieved / read_gbs, 4) if read_gbs else None,
+                         "measured_source": copy_src},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,
             "parity": parity,
             "secondary": secondary,
+            # which block the north star's ">= 6x at 8 GPUs" is read from
+            "scaling_note": ("value is weak-scaled (a C3 shard per GPU, no data-path collective); the strong-scaling "
+                             "criterion (>= 6x at 8 GPUs) is read from the `strong` block (C4, fixed total work)"),
             "x_bcast_us": None if bcast_us is None else round(bcast_us, 2),
             # scaling both ways -- `value` is compute-only (x resident);
             # this rate charges one x broadcast to every step (x changing per step)

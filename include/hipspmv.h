@@ -284,6 +284,13 @@ int hipspmv_multi_exec(hipspmv_multi_t *m, const void *x, void *y, int beta, int
 int hipspmv_multi_stat(hipspmv_multi_t *m, const char *key, uint64_t *out);
 int hipspmv_multi_destroy(hipspmv_multi_t *m);
 
+/* The measured HBM ceiling (not on the SpMV path; bench.py's second
+ * denominator): a streaming copy (read + write counted) and a
+ * streaming read of `bytes`-sized buffers on `device`, 16-byte non-temporal
+ * accesses, `reps` timed launches each after two untimed ones.  Either output
+ * may be NULL (that stream is then not run). */
+int hipspmv_stream_bandwidth(int device, uint64_t bytes, int reps, double *copy_gbs, double *read_gbs);
+
 const char *hipspmv_strerror(int status);
 /* Text of the last HIP error seen by this thread (static per-thread buffer). */
 const char *hipspmv_last_error(void);

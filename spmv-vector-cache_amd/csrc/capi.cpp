@@ -225,6 +225,11 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
     if (!build_vcache_lanes(a, g, lanes, L)) return HIPSPMV_ERR_UNSUPPORTED;
   } else {
     build_vcache(a, g, L, k == 3 && h->wgather_sort);  // k_wgather: gathers of one x line side by side
+    // the product FAST geometry: rows of each segment placed for LDS banks
+    // (plan.cpp place_segments_banked; bit-identical sums); HIPSPMV_VCACHE_BANK=0
+    // keeps the (row, column) order (A/B probe)
+    const char* bank = std::getenv("HIPSPMV_VCACHE_BANK");
+    if (k == 1 && !(bank && std::strcmp(bank, "0") == 0)) place_segments_banked(L, kVcSplitCT);
   }
   v.split = g.split;
   v.rows_per_block = L.rows_per_block;

@@ -72,7 +72,9 @@ constexpr uint32_t kVqLMore = 1u << 28;
 // the k_vquad geometry: 16384 rows, 1984-column panels, 4 parts, 12 column
 // bits (the code holds row_local << 12 and the flags in bits 28-31)
 constexpr VcGeom kVcQuad{16384, 1984, 4, 12};
-constexpr uint32_t kVqLanes = 13 * 64;  // k_vquad's compute lanes (13 of 16 waves): the layout's CT
+constexpr uint32_t kVqLanes = 13 * 64;
+// k_vcache's split geometry: compute lanes (16 - 3 loader waves) * 64 (VcCfg<3>)
+constexpr uint32_t kVcSplitCT = 13 * 64;  // k_vquad's compute lanes (13 of 16 waves): the layout's CT
 
 // ---- wcsr: csr_vector over the column-windowed segment matrix
 // Every row is cut at column windows of 2^kWcLog2Window columns (8 MiB of
@@ -327,6 +329,9 @@ uint32_t vcache_max_run(const HostCSR& a, uint32_t panel);
 void build_vcache(const HostCSR& a, const VcGeom& g, VcacheLayout& out, bool by_line = false);
 // k_wgather's segment order: row runs by the x line of their first column (plan.cpp)
 void sort_segments_by_line(VcacheLayout& L);
+// k_vcache split: entries of each segment re-placed for LDS banks (plan.cpp;
+// the same sums, bit-identical results)
+void place_segments_banked(VcacheLayout& L, uint32_t CT);
 // k_vquad's placement of the same entries for CT compute lanes (plan.cpp)
 bool build_vcache_lanes(const HostCSR& a, const VcGeom& g, uint32_t CT, VcacheLayout& out);
 void build_sell(const HostCSR& a, SellLayout& out);

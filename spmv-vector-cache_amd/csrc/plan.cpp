@@ -1,6 +1,7 @@
 // Host-side planning for libhipspmv: CSC -> CSR transpose, validation, and the
 // device layouts each kernel reads.
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -373,6 +374,284 @@ void sort_segments_by_line(VcacheLayout& L) {
       for (uint32_t u = (uint32_t)t; u < units; u += nt) {
         const uint32_t* sg = &L.seg[(size_t)u * (npad + 1)];
         for (uint32_t i = 0; i < npad; ++i) sort(L.code.data(), L.vals.data(), sg[i], sg[i + 1]);
+      }
+  });
+}
+
+// LDS-bank-aware placement of the split layout's segments.
+// k_vcache's compute lane ct of step s takes positions ct and CT + ct of the
+// segment; every wave-instruction of the apply reads x[col] and y[row] with
+// ds_read_b64 (bank pair (addr / 8) mod 32 per 32-lane half) and writes y[row]
+// with ds_write_b64 (row mod 16 per 16-lane quarter), so a half whose 32
+// entries repeat a column class (col mod 32) or a row class (row mod 32) is
+// served in as many LDS cycles as the largest repeat.  In (row, column) order
+// random columns cost ~3.5 cycles per half (3.64 conflict cycles
+// per LDS instruction).  Here every 32-position group of a segment is filled
+// with a maximum matching between column classes and row classes of the
+// entries still unplaced (Kuhn's augmenting paths over 32 x 32 bitmasks), the
+// rest of the group with the entries that add the fewest repeats, and each
+// half of a group gets distinct row mod 16 where it can.  A segment's
+// multi-entry row runs keep their consecutive positions (CONT / MORE) at its
+// start, inside one wave.  Only the order of rows inside a segment changes --
+// every row still has one run per segment in column order -- so every row's
+// sum, and the result, is bit-identical to the (row, column) layout.
+namespace {
+struct BankPlacer {
+  uint32_t CT;
+  std::vector<uint32_t> code, out;  // scratch: the segment, slot -> source entry
+  std::vector<uint64_t> vals;
+  std::vector<uint32_t> pair_head, pair_next;  // per (cc, rc) pair: a list of single entries
+  uint32_t cnt[32][32], adjbit[32], adjrank[32], cleft[32], rleft[32];
+  int rorder[32], rank[32];  // row classes by singles at the segment's start (most first), and back
+  std::vector<std::vector<uint32_t>> members;  // per group of 32 positions: its singles
+  std::vector<std::array<uint8_t, 32>> gc, gr;  // per group: column / row class counts (runs included)
+  explicit BankPlacer(uint32_t ct) : CT(ct), pair_head(1024) {}
+
+  static int dfs(int c, const uint32_t* adj, int* match, uint32_t& visited) {
+    for (uint32_t m = adj[c] & ~visited; m; m &= m - 1) {
+      const int k = __builtin_ctz(m);
+      visited |= 1u << k;
+      if (match[k] < 0 || dfs(match[k], adj, match, visited)) {
+        match[k] = c;
+        return 1;
+      }
+    }
+    return 0;
+  }
+  static int dfs64(int c, const uint64_t* adj, int* match, uint64_t& visited) {
+    for (uint64_t m = adj[c] & ~visited; m; m &= m - 1) {
+      const int k = __builtin_ctzll(m);
+      visited |= 1ull << k;
+      if (match[k] < 0 || dfs64(match[k], adj, match, visited)) {
+        match[k] = c;
+        return 1;
+      }
+    }
+    return 0;
+  }
+  uint32_t take(uint32_t c, uint32_t r) {  // one single of pair (c, r)
+    const uint32_t k = c * 32 + r, e = pair_head[k];
+    pair_head[k] = pair_next[e];
+    if (--cnt[c][r] == 0) {
+      adjbit[c] &= ~(1u << r);
+      adjrank[c] &= ~(1u << rank[r]);
+    }
+    cleft[c]--;
+    rleft[r]--;
+    return e;
+  }
+
+  // entries [s0, s1) of C / V (global arrays), rewritten in place
+  void operator()(uint32_t* C, uint64_t* V, uint32_t s0, uint32_t s1) {
+    const uint32_t n = s1 - s0;
+    if (n < 2 || n > 2 * CT) return;
+    code.assign(C + s0, C + s1);
+    vals.assign(V + s0, V + s1);
+    out.assign(n, UINT32_MAX);
+    auto cc = [&](uint32_t e) { return code[e] & 31u; };
+    auto rc = [&](uint32_t e) { return (code[e] >> 16) & 31u; };
+    // 1. multi-entry runs at the front, packed, none across a 64-position wave
+    uint32_t p = 0;
+    std::fill(pair_head.begin(), pair_head.end(), UINT32_MAX);
+    pair_next.assign(n, UINT32_MAX);
+    std::memset(cnt, 0, sizeof cnt);
+    std::memset(adjbit, 0, sizeof adjbit);
+    std::memset(cleft, 0, sizeof cleft);
+    std::memset(rleft, 0, sizeof rleft);
+    for (uint32_t e = 0; e < n;) {
+      uint32_t f = e + 1;
+      while (f < n && (code[f] & kVcCont)) ++f;
+      const uint32_t len = f - e;
+      if (len >= 2) {
+        if ((p % 64) + len > 64) p = (p + 63) / 64 * 64;
+        if (p + len > n) return;  // cannot pack (tiny segment): keep the (row, column) order
+        for (uint32_t q = 0; q < len; ++q) out[p + q] = e + q;
+        p += len;
+      } else {  // a single: into its (column class, row class) list
+        const uint32_t c = cc(e), r = rc(e), k = c * 32 + r;
+        pair_next[e] = pair_head[k];
+        pair_head[k] = e;
+        cnt[c][r]++;
+        adjbit[c] |= 1u << r;
+        cleft[c]++;
+        rleft[r]++;
+      }
+      e = f;
+    }
+    for (int i = 0; i < 32; ++i) rorder[i] = i;
+    std::sort(rorder, rorder + 32, [&](int x, int y) { return rleft[x] > rleft[y]; });
+    for (int i = 0; i < 32; ++i) rank[rorder[i]] = i;
+    for (int c = 0; c < 32; ++c) {
+      adjrank[c] = 0;
+      for (uint32_t bb = adjbit[c]; bb; bb &= bb - 1) adjrank[c] |= 1u << rank[__builtin_ctz(bb)];
+    }
+    // 2. groups of 32 positions: a maximum matching of column classes to row
+    // classes, the classes with the most singles preferred on both sides,
+    // then the entries adding the fewest repeats
+    const uint32_t ng = (n + 31) / 32;
+    members.assign(ng, {});
+    gc.assign(ng, {});
+    gr.assign(ng, {});
+    for (uint32_t g = 0; g < ng; ++g) {
+      const uint32_t g0 = g * 32, g1 = std::min(n, g0 + 32);
+      uint32_t used_c = 0, used_r = 0, nfree = 0;
+      for (uint32_t q = g0; q < g1; ++q) {
+        if (out[q] == UINT32_MAX) {
+          ++nfree;
+          continue;
+        }
+        const uint32_t e = out[q];
+        used_c |= 1u << cc(e);
+        gc[g][cc(e)]++;
+        if (!(code[e] & kVcCont)) {
+          used_r |= 1u << rc(e);
+          gr[g][rc(e)]++;
+        }
+      }
+      if (!nfree) continue;
+      // each class may appear cap = ceil(singles left / groups left) times (1 or
+      // 2 copies in the matching), so the classes with more singles than
+      // groups spread their repeats over every group instead of crowding the last
+      const uint32_t gl = ng - g;
+      int corder[32];
+      for (int i = 0; i < 32; ++i) corder[i] = i;
+      std::sort(corder, corder + 32, [&](int x, int y) { return cleft[x] > cleft[y]; });
+      auto cap = [&](uint32_t left, uint32_t used) {
+        const uint32_t c = std::min<uint32_t>(2, (left + gl - 1) / gl);
+        return c > used ? c - used : 0u;
+      };
+      // row copy k of rank i is bit i + 32 k; column copies are nodes c + 32 k
+      uint64_t rmask = 0;
+      for (int i = 0; i < 32; ++i) {
+        const uint32_t r = (uint32_t)rorder[i], cr = cap(rleft[r], gr[g][r]);
+        if (cr >= 1) rmask |= 1ull << i;
+        if (cr >= 2) rmask |= 1ull << (i + 32);
+      }
+      uint64_t adj[64];
+      int cnodes[64], ncn = 0;
+      for (int k = 0; k < 2; ++k)
+        for (int i = 0; i < 32; ++i) {
+          const int c = corder[i];
+          adj[c + 32 * k] = 0;
+          if (cap(cleft[c], gc[g][c]) <= (uint32_t)k) continue;
+          adj[c + 32 * k] = ((uint64_t)adjrank[c] | (uint64_t)adjrank[c] << 32) & rmask;
+          cnodes[ncn++] = c + 32 * k;
+        }
+      // augment in three phases: no repeat, then the column repeats the
+      // schedule asks for, then the row repeats
+      int match[64];
+      std::fill(match, match + 64, -1);
+      uint32_t size = 0;
+      bool matched[64] = {false};
+      for (int phase = 0; phase < 3 && size < nfree; ++phase) {
+        const uint64_t allow = phase < 2 ? 0xFFFFFFFFull : ~0ull;
+        uint64_t adjp[64];
+        for (int i = 0; i < ncn; ++i) adjp[cnodes[i]] = adj[cnodes[i]] & allow;
+        uint64_t taken_rows = 0;
+        for (int k = 0; k < 64; ++k)
+          if (match[k] >= 0) taken_rows |= 1ull << k;
+        for (int i = 0; i < ncn && size < nfree; ++i) {  // greedy first: most nodes match directly
+          const int cn = cnodes[i];
+          if (matched[cn] || (phase == 0 && cn >= 32)) continue;
+          const uint64_t m = adjp[cn] & ~taken_rows;
+          if (!m) continue;
+          const int k = __builtin_ctzll(m);
+          match[k] = cn;
+          taken_rows |= 1ull << k;
+          matched[cn] = true;
+          ++size;
+        }
+        for (int i = 0; i < ncn && size < nfree; ++i) {  // then augmenting paths
+          const int cn = cnodes[i];
+          if (matched[cn] || (phase == 0 && cn >= 32)) continue;
+          uint64_t vis = 0;
+          if (dfs64(cn, adjp, match, vis)) {
+            matched[cn] = true;
+            ++size;
+          }
+        }
+      }
+      auto add = [&](uint32_t c, uint32_t r) {
+        members[g].push_back(take(c, r));
+        gc[g][c]++;
+        gr[g][r]++;
+        used_c |= 1u << c;
+        used_r |= 1u << r;
+      };
+      for (int k = 0; k < 64; ++k)
+        if (match[k] >= 0) {
+          const uint32_t c = (uint32_t)(match[k] & 31), r = (uint32_t)rorder[k & 31];
+          if (cnt[c][r]) add(c, r);  // (a pair matched twice with one single left: the fill below)
+        }
+      while (members[g].size() < nfree) {
+        int bc = -1, br = -1, best = 3;
+        for (int i = 0; i < 32 && best; ++i) {
+          const int c = corder[i];
+          for (uint32_t bb = adjbit[c]; bb && best; bb &= bb - 1) {
+            const int r = __builtin_ctz(bb);
+            const int sc = (int)(used_c >> c & 1) + (int)(used_r >> r & 1);
+            if (sc < best) {
+              best = sc;
+              bc = c;
+              br = r;
+            }
+          }
+        }
+        if (bc < 0) return;  // (the free slots equal the singles left: not reached) keep the old order
+        add((uint32_t)bc, (uint32_t)br);
+      }
+    }
+    // 3. inside each group: distinct row mod 16 per half where possible
+    for (uint32_t g = 0; g < ng; ++g) {
+      const uint32_t g0 = g * 32, g1 = std::min(n, g0 + 32);
+      uint32_t used_h[2] = {0, 0}, hfree[2] = {0, 0}, placed[2] = {0, 0};
+      for (uint32_t q = g0; q < g1; ++q) {
+        if (out[q] == UINT32_MAX) {
+          hfree[(q - g0) / 16]++;
+        } else if (!(code[out[q]] & kVcCont)) {
+          used_h[(q - g0) / 16] |= 1u << (rc(out[q]) & 15);
+        }
+      }
+      uint32_t half[2][32], rest[32], nh[2] = {0, 0}, nrest = 0;
+      for (uint32_t e : members[g]) {
+        const uint32_t bit = 1u << (rc(e) & 15);
+        int hh = -1;
+        for (int x = 0; x < 2 && hh < 0; ++x)
+          if (placed[x] < hfree[x] && !(used_h[x] & bit)) hh = x;
+        if (hh < 0) {
+          rest[nrest++] = e;
+          continue;
+        }
+        used_h[hh] |= bit;
+        half[hh][nh[hh]++] = e;
+        placed[hh]++;
+      }
+      for (uint32_t i = 0; i < nrest; ++i) {
+        const int hh = placed[0] < hfree[0] ? 0 : 1;
+        half[hh][nh[hh]++] = rest[i];
+        placed[hh]++;
+      }
+      size_t i0 = 0, i1 = 0;
+      for (uint32_t q = g0; q < g1; ++q)
+        if (out[q] == UINT32_MAX) out[q] = (q - g0) < 16 ? half[0][i0++] : half[1][i1++];
+    }
+    for (uint32_t q = 0; q < n; ++q) {
+      C[s0 + q] = code[out[q]];
+      V[s0 + q] = vals[out[q]];
+    }
+  }
+};
+}  // namespace
+
+void place_segments_banked(VcacheLayout& L, uint32_t CT) {
+  const uint32_t units = L.nblocks * (uint32_t)L.geom.split, npad = L.npad;
+  const unsigned nt = std::max(1u, std::min(plan_threads(), units));
+  par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
+    BankPlacer place(CT);
+    for (uint64_t t = t0; t < t1; ++t)
+      for (uint32_t u = (uint32_t)t; u < units; u += nt) {
+        const uint32_t* sg = &L.seg[(size_t)u * (npad + 1)];
+        for (uint32_t i = 0; i < npad; ++i) place(L.code.data(), L.vals.data(), sg[i], sg[i + 1]);
       }
   });
 }

@@ -117,11 +117,13 @@ def load_hipspmv() -> C.CDLL:
     lib.hipspmv_multi_create_csr.argtypes = lib.hipspmv_multi_create.argtypes
     lib.hipspmv_multi_shard.argtypes = [vp, C.c_int, C.POINTER(vp)]
     lib.hipspmv_partition_rows.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp]
+    lib.hipspmv_stream_bandwidth.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double),
+                                             C.POINTER(C.c_double)]
     lib.hipspmv_multi_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
     lib.hipspmv_multi_exec.argtypes = [vp, vp, vp, C.c_int, C.c_int]
     lib.hipspmv_multi_stat.argtypes = [vp, C.c_char_p, C.POINTER(C.c_uint64)]
     lib.hipspmv_multi_destroy.argtypes = [vp]
-    for name in ("hipspmv_multi_create", "hipspmv_multi_create_csr", "hipspmv_multi_shard", "hipspmv_partition_rows",
+    for name in ("hipspmv_stream_bandwidth", "hipspmv_multi_create", "hipspmv_multi_create_csr", "hipspmv_multi_shard", "hipspmv_partition_rows",
                  "hipspmv_multi_set_option", "hipspmv_multi_exec", "hipspmv_multi_stat", "hipspmv_multi_destroy"):
         getattr(lib, name).restype = C.c_int
     for name in ("hipspmv_create", "hipspmv_create_csr", "hipspmv_set_option", "hipspmv_exec",
@@ -376,6 +378,15 @@ class MultiHandle:
             self.close()
         except Exception:
             pass
+
+
+def stream_bandwidth(device: int = 0, nbytes: int = 1 << 30, reps: int = 10) -> tuple:
+    """(copy GB/s counting read + write, read GB/s) of the in-tree streaming
+    kernels on buffers of nbytes (hipspmv_stream_bandwidth): the measured HBM
+    ceiling bench.py reports beside the 8 TB/s roofline."""
+    cp, rd = C.c_double(), C.c_double()
+    _check(load_hipspmv().hipspmv_stream_bandwidth(device, nbytes, reps, C.byref(cp), C.byref(rd)), "stream_bandwidth")
+    return float(cp.value), float(rd.value)
 
 
 def device_count() -> int:

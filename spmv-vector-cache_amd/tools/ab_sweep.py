@@ -25,6 +25,10 @@ sys.path.insert(0, os.path.dirname(HERE))
 import hipspmv as hs  # noqa: E402
 
 SETS = {
+    # round 5: the split layout's LDS-bank-aware placement against the (row, column) order
+    # ("bank0": a second handle created with HIPSPMV_VCACHE_BANK=0)
+    "bank": [("split banked", "vcache_split", {}), ("split row order", "bank0:vcache_split", {}),
+             ("vquad v0", "vcache_split4", {"vquad_variant": 0})],
     # round 5: k_vquad's XCD map, Infinity-Cache resident entries, LDS atomic y updates
     "vquad": [("split (product)", "vcache_split", {}),
               ("vquad v0", "vcache_split4", {"vquad_variant": 0}),
@@ -50,6 +54,11 @@ def main():
     rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32, 1, 2)
     x = hs.gen_vector(n, 3)
     h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    hb = None
+    if any(k.startswith("bank0:") for _, k, _ in SETS[a.set]):
+        os.environ["HIPSPMV_VCACHE_BANK"] = "0"
+        hb = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+        del os.environ["HIPSPMV_VCACHE_BANK"]
     alg = h.stat("alg_bytes")
     xd = torch.from_numpy(x).cuda()
     yd = torch.empty(n, dtype=torch.float64, device="cuda")
@@ -63,20 +72,24 @@ def main():
 
     cfgs = SETS[a.set]
 
+    cur = [h]
+
     def select(kernel, opts):
-        h.set_kernel(kernel)
+        cur[0] = hb if kernel.startswith("bank0:") else h
+        cur[0].set_kernel(kernel.split(":")[-1])
         for k, v in opts.items():
-            h.set_option(k, v)
+            cur[0].set_option(k, v)
 
     def reset(opts):
         for k in opts:
-            h.set_option(k, {"vquad_variant": 0, "vcache_nt": -1}.get(k, -1))
+            cur[0].set_option(k, {"vquad_variant": 0, "vcache_nt": -1}.get(k, -1))
 
     def run(k):
         for _ in range(k):
-            h.exec_device(xd, yd, beta=0, mode=hs.MODE_FAST, stream=s)
+            cur[0].exec_device(xd, yd, beta=0, mode=hs.MODE_FAST, stream=s)
 
     checks = {}
+    y_first = None
     for label, kernel, opts in cfgs:
         select(kernel, opts)
         run(1)
@@ -86,8 +99,12 @@ def main():
         r = np.abs(y1 - y_ref) / bound
         checks[label] = {"within_bound": bool(np.all(r <= 1.0)), "max_err_over_bound": round(float(r.max()), 3),
                          "deterministic": y1.tobytes() == y2.tobytes()}
+        if y_first is None:
+            y_first = y1
+        else:
+            checks[label]["bits_equal_first_config"] = y1.tobytes() == y_first.tobytes()
         reset(opts)
-    h.set_kernel("vcache_split")
+    select("vcache_split", {})
     run(400)
     torch.cuda.synchronize()
     times = {c[0]: [] for c in cfgs}

@@ -3,6 +3,7 @@
 // create time of full C4 goes.
 //
 //   setup_probe c4|c3|c5 [threads]
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -87,6 +88,57 @@ int main(int argc, char** argv) {
     VcacheLayout W2;
     build_vcache(a, kWgWindow, W2, true);
     phase("build_vcache wgather by line", t);
+  }
+  if (which == "c3") {  // the split layout and its LDS-bank placement (plan.cpp place_segments_banked)
+    t = now_s();
+    VcacheLayout V;
+    build_vcache(a, kVcSplit, V);
+    phase("build_vcache split", t);
+    // LDS cycles per 32-lane half of the apply's ds_read_b64 (x: distinct columns by
+    // column mod 32, y: rows by row mod 32) and per 16-lane quarter of its
+    // ds_write_b64 (row mod 16), positions as k_vcache's compute lanes take them
+    auto cost = [&](const VcacheLayout& L, double* out) {
+      double cx = 0, cy = 0, cw = 0, groups = 0, quarters = 0;
+      const uint32_t units = L.nblocks * 3, CT = kVcSplitCT;
+      for (uint32_t u = 0; u < units; ++u)
+        for (uint32_t i = 0; i < L.npad; ++i) {
+          const uint32_t s0 = L.seg[(size_t)u * (L.npad + 1) + i], s1 = L.seg[(size_t)u * (L.npad + 1) + i + 1];
+          if (s1 - s0 > 2 * CT) continue;
+          for (uint32_t g0 = s0; g0 < s1; g0 += 32) {
+            int mc[32] = {0}, my[32] = {0}, mw[2][16] = {{0}};
+            std::vector<uint32_t> cols;
+            for (uint32_t e = g0; e < std::min(s1, g0 + 32); ++e) {
+              const uint32_t c = L.code[e] & 0xFFFF, r = (L.code[e] >> 16) & 0x3FFF;
+              if (std::find(cols.begin(), cols.end(), c) == cols.end()) {
+                cols.push_back(c);
+                mc[c & 31]++;
+              }
+              if (!(L.code[e] & kVcCont)) {
+                my[r & 31]++;
+                mw[(e - g0) / 16][r & 15]++;
+              }
+            }
+            cx += *std::max_element(mc, mc + 32);
+            cy += std::max(1, *std::max_element(my, my + 32));
+            for (int q = 0; q < 2; ++q) {
+              cw += std::max(1, *std::max_element(mw[q], mw[q] + 16));
+              quarters += 1;
+            }
+            groups += 1;
+          }
+        }
+      out[0] = cx / groups;
+      out[1] = cy / groups;
+      out[2] = cw / quarters;
+    };
+    double c0[3], c1[3];
+    cost(V, c0);
+    t = now_s();
+    place_segments_banked(V, kVcSplitCT);
+    phase("place_segments_banked", t);
+    cost(V, c1);
+    std::printf("  LDS cycles per group (x read / y read / y write quarter): row order %.2f / %.2f / %.2f, "
+                "banked %.2f / %.2f / %.2f\n", c0[0], c0[1], c0[2], c1[0], c1[1], c1[2]);
   }
   if (which == "c5") {
     t = now_s();

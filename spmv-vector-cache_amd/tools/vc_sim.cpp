@@ -655,9 +655,46 @@ int main(int argc, char** argv) {
         std::printf("%-28s split=%d cx=%d: segments exceed the window, CX 0 runs\n", cs.name.c_str(), c.SPLIT, c.CX);
         continue;
       }
+      // the product's bank-aware placement (plan.cpp place_segments_banked):
+      // a permutation inside every segment, runs consecutive inside one wave,
+      // and the same result bits as the (row, column) layout
+      VcacheLayout B;
+      const bool banked = c.SPLIT == 3 && c.LD == 1 && c.CX >= 2;  // the product: xlane 3 (modelled as CX 2)
+      if (banked) {
+        B = L;
+        const uint32_t CT = (uint32_t)(16 - c.WL) * 64;
+        place_segments_banked(B, CT);
+        bool perm = B.seg == L.seg;
+        const uint32_t units = L.nblocks * (uint32_t)c.SPLIT;
+        for (uint32_t u = 0; u < units && perm; ++u)
+          for (uint32_t i = 0; i < L.npad && perm; ++i) {
+            const uint32_t s0 = L.seg[(size_t)u * (L.npad + 1) + i], s1 = L.seg[(size_t)u * (L.npad + 1) + i + 1];
+            std::vector<std::pair<uint32_t, uint64_t>> a0, a1;
+            for (uint32_t e = s0; e < s1; ++e) {
+              a0.emplace_back(L.code[e], L.vals[e]);
+              a1.emplace_back(B.code[e], B.vals[e]);
+              if ((B.code[e] & kVcCont) && (e == s0 || !(B.code[e - 1] & kVcMore) || (e - s0) % 64 == 0))
+                perm = false;  // a continuation right after its run's previous entry, same wave
+            }
+            std::sort(a0.begin(), a0.end());
+            std::sort(a1.begin(), a1.end());
+            perm = perm && a0 == a1;
+          }
+        if (!perm) {
+          std::printf("%-28s place_segments_banked: not a run-preserving permutation\n", cs.name.c_str());
+          ++failures;
+        }
+      }
       for (int beta = 0; beta < 2; ++beta) {
         g_errors = 0;
         const auto y = simulate(cs.A, L, c, x, yin, beta);
+        if (banked) {
+          const auto yb = simulate(cs.A, B, c, x, yin, beta);
+          if (std::memcmp(y.data(), yb.data(), 8ull * cs.A.rows) != 0) {
+            std::printf("%-28s banked placement changes result bits\n", cs.name.c_str());
+            ++failures;
+          }
+        }
         const auto r = reference(cs.A, x, yin, beta);
         size_t bad = 0;
         if (c.SPLIT > 1) {  // deterministic: the other arrival order gives the same bits

@@ -370,3 +370,30 @@ def test_bench_four_ranks_gloo():
     assert out["n_gpus"] == 4 and len(out["rank_kernel_us"]) == 4
     _check_rank_parity_and_strong(out, 4)
     assert out["config"]["nnz_total"] == 4 * out["config"]["nnz_per_gpu"]
+
+
+@pytest.mark.parametrize("workload,scale", [("c4", 12), ("c5", 12)])
+def test_bench_eight_ranks_gloo(workload, scale):
+    # the driver's N=8 case rehearsed on CPU: the C4 / C5
+    # strong-scaled workloads cut into eight row blocks, the x broadcast and the
+    # y allgather timed, per-rank parity on every rank
+    res = _multi_rank(["--workload", workload, "--scale", str(scale)], world=8)
+    out = res[0]
+    assert all(res[r] is None for r in range(1, 8))
+    assert out["n_gpus"] == 8 and out["scaling"] == "strong" and len(out["rank_kernel_us"]) == 8
+    assert out["x_bcast_us"] is not None and out["x_bcast_us"] > 0
+    assert out["y_allgather_us"] is not None and out["y_allgather_us"] > 0
+    assert out["end_to_end"] is not None and out["end_to_end"]["value"] <= out["value"]
+    assert out["iterative"] is not None and out["iterative"]["value"] <= out["value"]
+    rp = out["rank_parity"]
+    assert [p["rank"] for p in rp] == list(range(8))
+    assert all(p["fast"].startswith("within FAST bound") and p["ordered"].startswith("bit-exact") for p in rp), rp
+    rows = [p["rows"] for p in rp]  # the blocks tile the matrix
+    assert rows[0][0] == 0 and rows[-1][1] == 1 << scale and all(rows[i][1] == rows[i + 1][0] for i in range(7))
+    assert "strong" in out["scaling_note"]
+    if workload == "c5":
+        import hipspmv as hs_
+        rp_, ci_, _ = hs_.gen_rmat_csr(scale)
+        assert out["config"]["nnz_total"] == ci_.size
+        # the blocks are the library's partition (hipspmv_partition_rows), not the bench's
+        assert [r[0] for r in rows] == [int(b) for b in hs_.partition_rows_cost(rp_, ci_, 1 << scale, 8)[:8]]

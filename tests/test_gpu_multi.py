@@ -170,3 +170,52 @@ def test_multi_wcsr_wide_skewed(gpu, dtype):
         absprod = np.bincount(np.repeat(np.arange(rows), lens), weights=np.abs(vals * x[colind]), minlength=rows)
         bound = 2.0 * np.maximum(lens, 1) * 2.0 ** -53 * absprod + 1e-300
         assert np.all(np.abs(y3 - y_ref) <= bound) and np.all(np.abs(y1 - y_ref) <= bound)
+
+
+def test_c5_multi_create_balanced_shards(gpu):
+    """Full C5 (R-MAT scale 24, 263 M nonzeros) through hipspmv_multi_create_csr
+    with eight repeated device ids: the library's own
+    partition (hipspmv_partition_rows) cuts the rows; every block, timed alone
+    on this GPU through its own handle, runs AUTO's FAST kernel (wcsr) within
+    1.15x of the others, and sampled rows of every block are within the FAST
+    bound (recomputed sequentially in numpy)."""
+    import torch
+    scale, parts = 24, 8
+    n = 1 << scale
+    rowptr, colind, vals = hs.gen_rmat_csr(scale)
+    bounds = hs.partition_rows_cost(rowptr, colind, n, parts)
+    m = hs.MultiHandle(rowptr, colind, vals, n, n, [0] * parts, csr=True)
+    assert [m.stat(f"shard{i}_row0") for i in range(parts)] == [int(b) for b in bounds[:parts]]
+    x = hs.gen_vector(n, 3)
+    xd = torch.from_numpy(x).cuda()
+    s = torch.cuda.current_stream()
+    hs_ = [m.shard(i) for i in range(parts)]
+    ys = [torch.empty(h.rows, dtype=torch.float64, device="cuda") for h in hs_]
+    for _ in range(25):  # past the clock transient of an idle GPU (DESIGN.md §7)
+        for h, y in zip(hs_, ys):
+            h.exec_device(xd, y, beta=0, mode=hs.MODE_FAST, stream=s)
+    torch.cuda.synchronize()
+    times = []
+    for h, y in zip(hs_, ys):
+        assert h.kernel_name(hs.MODE_FAST) == "wcsr"
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(20):
+            h.exec_device(xd, y, beta=0, mode=hs.MODE_FAST, stream=s)
+        e1.record(s)
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1) * 1e3 / 20)
+    rng = np.random.default_rng(0)
+    for i, y in enumerate(ys):
+        r0, r1 = int(bounds[i]), int(bounds[i + 1])
+        yy = y.cpu().numpy()
+        for r in rng.choice(np.arange(r0, r1), size=min(300, r1 - r0), replace=False):
+            e0, e1 = int(rowptr[r]), int(rowptr[r + 1])
+            prod = vals[e0:e1] * x[colind[e0:e1]]
+            acc = 0.0
+            for p in prod:
+                acc += p
+            bound = 2.0 * (e1 - e0 + 1) * 2.0 ** -53 * np.abs(prod).sum() + 1e-300
+            assert abs(yy[r - r0] - acc) <= bound, (i, r)
+    assert max(times) / min(times) <= 1.15, times
+    m.close()

@@ -978,3 +978,9 @@ def test_wgather_runs_and_line_order(gpu, dtype):
         y = h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_ORDERED)
         assert y.tobytes() == y_ref.tobytes(), (dtype, beta)
     h.close()
+
+
+def test_stream_bandwidth(gpu):
+    # the bench's second denominator (hipspmv_stream_bandwidth, csrc/stream.hip): plausible GB/s on an MI355X
+    cp, rd = hs.stream_bandwidth(0, 1 << 28, 5)
+    assert 1000 < cp < 8000 and 1000 < rd < 8000, (cp, rd)
