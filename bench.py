@@ -215,7 +215,7 @@ def kernel_provenance(kname: str, dtype: str = "double", exact: bool = False, is
     sys.path.insert(0, os.path.join(REPO, "spmv-vector-cache_amd", "tools"))
     import kernel_isa
     want = {"vcache": f"void hipspmv::k_vcache<{dtype}, 1, 8, 4, 3, 0, 0, false, 0, 0>",
-            "vcache_split": f"void hipspmv::k_vcache<{dtype}, 3, 3, 4, 2, 0, 0, false, 1, 3>",
+            "vcache_split": f"void hipspmv::k_vcache<{dtype}, 3, 3, 4, 2, 0, 0, false, 1, 5>",
             "csr_lane": f"void hipspmv::k_csr_lane<{dtype}>", "csr_vector": f"void hipspmv::k_csr_vector<{dtype}, false>",
             "wgather": f"void hipspmv::k_wgather<{dtype}, 17, 4, 2, true>",
             "sell": f"void hipspmv::(anonymous namespace)::k_sell<{dtype}, {'true' if exact else 'false'}>",

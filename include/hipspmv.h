@@ -106,12 +106,14 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
 /* Options: "kernel" (HIPSPMV_KERNEL_*), "mode" (default mode for exec with
  * HIPSPMV_MODE_AUTO), "timing" (1 = record per-exec kernel events),
  * "vcache_dma" (-1 default; 1 = vcache kernels stage x by LDS-DMA; the
- * VCACHE_SPLIT geometry always does), "vcache_xlane" (-1 default: 3 for
+ * VCACHE_SPLIT geometry always does), "vcache_xlane" (-1 default: 5 (else 3) for
  * VCACHE_SPLIT, 0 otherwise; 1 = vcache run continuations across lanes
  * instead of reloads; 2 = that plus step loops padded to the unroll and
  * register rings loaded by inline asm with explicit vmcnt waits; 3 =
  * cross-lane and padded loops with the compiler's own waits -- 2 and 3 keep
- * the DE-deep entry prefetch in flight across the loop header), "vcache_map"
+ * the DE-deep entry prefetch in flight across the loop header; 5 = 3 with the
+ * first continuation step by DPP, for VCACHE_SPLIT layouts whose runs stay in
+ * 16-lane rows -- the default there), "vcache_map"
  * (1 = VCACHE_SPLIT4 places column part h on XCDs 2h and 2h+1, so each XCD's
  * L2 serves a quarter of x; experimental), "profile" (1 = VCACHE and
  * VCACHE_SPLIT launches run in their default configuration with in-kernel

@@ -81,6 +81,7 @@ struct hipspmv_handle {
     uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, part_panels = 0, npad = 0, max_seg = 0, max_run = 0;
     uint64_t n_cont = 0;
     int split = 1;
+    bool row_runs = false;  // place_segments_banked: runs inside 16-lane rows (xlane 5 applies)
   } vc[4];  // [0] ordered (kVcOrdered), [1] split (kVcSplit); experimental: [2] split4; [3] wgather windows
   // The ordered vcache layout is only ever selected by name: its eligibility
   // and geometry are known at create, its entries built on first selection.
@@ -225,11 +226,13 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
     if (!build_vcache_lanes(a, g, lanes, L)) return HIPSPMV_ERR_UNSUPPORTED;
   } else {
     build_vcache(a, g, L, k == 3 && h->wgather_sort);  // k_wgather: gathers of one x line side by side
-    // the product FAST geometry: rows of each segment placed for LDS banks
-    // (plan.cpp place_segments_banked; bit-identical sums); HIPSPMV_VCACHE_BANK=0
-    // keeps the (row, column) order (A/B probe)
+    // the vector-cache geometries (ordered and split): rows of each segment
+    // placed for LDS banks (plan.cpp place_segments_banked; every row keeps its
+    // run and its column order, so the sums are bit-identical);
+    // HIPSPMV_VCACHE_BANK=0 keeps the (row, column) order (A/B probe)
     const char* bank = std::getenv("HIPSPMV_VCACHE_BANK");
-    if (k == 1 && !(bank && std::strcmp(bank, "0") == 0)) place_segments_banked(L, kVcSplitCT);
+    if ((k == 0 || k == 1) && !(bank && std::strcmp(bank, "0") == 0))
+      place_segments_banked(L, k == 1 ? kVcSplitCT : kVcOrderedCT);
   }
   v.split = g.split;
   v.rows_per_block = L.rows_per_block;
@@ -240,6 +243,7 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
   v.max_seg = L.max_seg;
   v.max_run = L.max_run;
   v.n_cont = L.n_cont;
+  v.row_runs = L.row_runs;
   auto fail = [&](int st) {
     free_vc(h, k);
     h->device_bytes = bytes0;
@@ -746,6 +750,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                  h->vcache_xlane, v.max_seg, h->vcache_map};
     a.nt_from = h->vcache_nt >= 0 ? (uint32_t)std::min<int64_t>(h->vcache_nt, UINT32_MAX)
                 : k == 1 ? 0u : k == 0 ? v.nblocks / 2 : ~0u;
+    a.row_runs = v.row_runs;
     // an unprofiled launch leaves an unread profile of an earlier launch readable
     // (it writes no stamps); d_prof is allocated when the option is set, never
     // here, so a profiled launch is legal only outside a capture (checked below)
@@ -971,7 +976,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
     if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_nt = value;
   } else if (k == "vcache_xlane") {
-    if (value < -1 || value > 4) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < -1 || value > 5) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_xlane = (int)value;
   } else if (k == "mode") {
     if (value != HIPSPMV_MODE_ORDERED && value != HIPSPMV_MODE_FAST) return HIPSPMV_ERR_INVALID_ARG;

@@ -74,7 +74,9 @@ constexpr uint32_t kVqLMore = 1u << 28;
 constexpr VcGeom kVcQuad{16384, 1984, 4, 12};
 constexpr uint32_t kVqLanes = 13 * 64;
 // k_vcache's split geometry: compute lanes (16 - 3 loader waves) * 64 (VcCfg<3>)
-constexpr uint32_t kVcSplitCT = 13 * 64;  // k_vquad's compute lanes (13 of 16 waves): the layout's CT
+constexpr uint32_t kVcSplitCT = 13 * 64;
+// ... and its ordered geometry's: (16 - 8 loader waves) * 64 (VcCfg<1>)
+constexpr uint32_t kVcOrderedCT = 8 * 64;  // k_vquad's compute lanes (13 of 16 waves): the layout's CT
 
 // ---- wcsr: csr_vector over the column-windowed segment matrix
 // Every row is cut at column windows of 2^kWcLog2Window columns (8 MiB of
@@ -287,6 +289,7 @@ struct VcacheLayout {
   uint32_t max_seg = 0;
   uint32_t max_run = 0;  // longest run of one row inside one segment
   uint64_t n_cont = 0;   // entries continuing a run (added after another entry of their row in one step)
+  bool row_runs = false;  // place_segments_banked: every run inside one 16-lane DPP row of one wave
 };
 
 struct WinLayout {

@@ -27,6 +27,8 @@ struct VcacheArgs {
   uint32_t nt_from = ~0u;  // k_vcache: row blocks b >= nt_from load their entries non-temporally
   uint32_t* status = nullptr;  // k_vquad: bit 0 set when a combine hand-off wait timed out
   int variant = 0;             // k_vquad: configuration (loader waves, x / entry ring depths)
+  bool row_runs = false;       // every run of the layout inside one 16-lane row (place_segments_banked):
+                               // the split kernel's first continuation step by DPP (xlane 5)
 };
 
 struct CsrArgs {

@@ -441,16 +441,19 @@ struct BankPlacer {
     return e;
   }
 
-  // entries [s0, s1) of C / V (global arrays), rewritten in place
-  void operator()(uint32_t* C, uint64_t* V, uint32_t s0, uint32_t s1) {
+  // entries [s0, s1) of C / V (global arrays), rewritten in place; false: the
+  // segment keeps its (row, column) order (its runs may then cross DPP rows)
+  bool operator()(uint32_t* C, uint64_t* V, uint32_t s0, uint32_t s1) {
     const uint32_t n = s1 - s0;
-    if (n < 2 || n > 2 * CT) return;
+    if (n < 2) return true;
+    if (n > 2 * CT) return false;
     code.assign(C + s0, C + s1);
     vals.assign(V + s0, V + s1);
     out.assign(n, UINT32_MAX);
     auto cc = [&](uint32_t e) { return code[e] & 31u; };
     auto rc = [&](uint32_t e) { return (code[e] >> 16) & 31u; };
-    // 1. multi-entry runs at the front, packed, none across a 64-position wave
+    // 1. multi-entry runs at the front, packed, none across a 16-position DPP
+    // row (so none across a wave either)
     uint32_t p = 0;
     std::fill(pair_head.begin(), pair_head.end(), UINT32_MAX);
     pair_next.assign(n, UINT32_MAX);
@@ -463,8 +466,9 @@ struct BankPlacer {
       while (f < n && (code[f] & kVcCont)) ++f;
       const uint32_t len = f - e;
       if (len >= 2) {
-        if ((p % 64) + len > 64) p = (p + 63) / 64 * 64;
-        if (p + len > n) return;  // cannot pack (tiny segment): keep the (row, column) order
+        if (len > 16) return false;  // no DPP row holds it: keep the (row, column) order
+        if ((p % 16) + len > 16) p = (p + 15) / 16 * 16;
+        if (p + len > n) return false;  // cannot pack (tiny segment): keep the (row, column) order
         for (uint32_t q = 0; q < len; ++q) out[p + q] = e + q;
         p += len;
       } else {  // a single: into its (column class, row class) list
@@ -597,7 +601,7 @@ struct BankPlacer {
             }
           }
         }
-        if (bc < 0) return;  // (the free slots equal the singles left: not reached) keep the old order
+        if (bc < 0) return false;  // (the free slots equal the singles left: not reached) keep the old order
         add((uint32_t)bc, (uint32_t)br);
       }
     }
@@ -639,6 +643,7 @@ struct BankPlacer {
       C[s0 + q] = code[out[q]];
       V[s0 + q] = vals[out[q]];
     }
+    return true;
   }
 };
 }  // namespace
@@ -646,14 +651,19 @@ struct BankPlacer {
 void place_segments_banked(VcacheLayout& L, uint32_t CT) {
   const uint32_t units = L.nblocks * (uint32_t)L.geom.split, npad = L.npad;
   const unsigned nt = std::max(1u, std::min(plan_threads(), units));
+  std::atomic<bool> all{true};
   par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
     BankPlacer place(CT);
+    bool ok = true;
     for (uint64_t t = t0; t < t1; ++t)
       for (uint32_t u = (uint32_t)t; u < units; u += nt) {
         const uint32_t* sg = &L.seg[(size_t)u * (npad + 1)];
-        for (uint32_t i = 0; i < npad; ++i) place(L.code.data(), L.vals.data(), sg[i], sg[i + 1]);
+        for (uint32_t i = 0; i < npad; ++i) ok = place(L.code.data(), L.vals.data(), sg[i], sg[i + 1]) && ok;
       }
+    if (!ok) all = false;
   });
+  // a segment left in (row, column) order may hold a run across a DPP row
+  L.row_runs = all;
 }
 
 // The k_vquad form of the vcache layout: the same blocks,

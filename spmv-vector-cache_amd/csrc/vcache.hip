@@ -35,6 +35,18 @@
 
 namespace hipspmv {
 
+// lane l gets lane l + 1's value inside its 16-lane row (DPP row_shl:1; lane
+// 15 of a row gets 0): the first step of a run continuation when the layout
+// keeps every run inside one row (CX == 5)
+__device__ __forceinline__ uint32_t dpp_next32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xF, 0xF, false);
+}
+template <typename T>
+__device__ __forceinline__ T dpp_next(T v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  return __builtin_bit_cast(T, (uint64_t)dpp_next32((uint32_t)u) | (uint64_t)dpp_next32((uint32_t)(u >> 32)) << 32);
+}
+
 // Per-geometry configuration.  LDS: VR*8 + 2*VP*8 + kVcSegMax*4 = 163840 B.
 template <int SPLIT>
 struct VcCfg;
@@ -69,6 +81,8 @@ struct VcCfg<4> {  // 16384 rows; x panel 15.5 KiB; 2 loader waves (8 pairs/lane
 // 256 / 512 / 1024 / 2048 / 4096: the entries of row blocks b >= nblocks/2,
 // 5/8, 3/8, 1/4, 1/8 loaded
 // non-temporally (Infinity-Cache residency experiment).
+// 16384 (xlane 3 path): y updated by one LDS atomic add per owner (the same
+// one update per row and step; deterministic).
 // 8192 (with 64; diagnostic, tools/step_trace.hip): step trace -- lane 0 of every
 // wave stores {ready, arrive, release, applied} (s_memtime low words: its data
 // landed, it reached the step barrier, the barrier let it go, its LDS apply
@@ -182,13 +196,14 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   // continuation entries (MORE) are read back from memory (rare: several
   // entries of one row inside one panel).
   const int ct = t - LT;
-  auto load_e = [&](uint32_t s, uint32_t* c, T* v, auto ntc) {
+  // beg_in: the step's first entry when the caller has it (CX 5), else read here
+  auto load_e = [&](uint32_t s, uint32_t* c, T* v, auto ntc, uint32_t beg_in = ~0u) {
     if (AB & 4) {
 #pragma unroll
       for (int j = 0; j < EPT; ++j) c[j] = kVcCont;
       return;
     }
-    const uint32_t beg = segl[min(s, npad)];
+    const uint32_t beg = beg_in != ~0u ? beg_in : segl[min(s, npad)];
     if constexpr (CX == 4) {
       // masked: a lane past the step's segment gets an out-of-range offset in
       // a descriptor of the unit's entries -- zero, and no memory request
@@ -280,11 +295,21 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       const T p = valid ? v[j] * xs[code & 0xFFFF] : T(0);  // rounded product (contract off)
       const bool own = valid && !(code & kVcCont);
       const uint32_t row = (code >> 16) & 0x3FFF;
-      T acc = own ? ylds[row] + p : T(0);
+      T acc = own ? ((AB & 16384) ? p : ylds[row] + p) : T(0);
       bool more = own && (code & kVcMore);
       bool fb = false;
       uint32_t fbi = 0;
-      for (uint32_t k = 1; __builtin_amdgcn_ballot_w64(more) != 0; ++k) {  // wave-uniform trip count
+      uint32_t k0 = 1;
+      if constexpr (CX == 5) {  // the layout keeps each run inside its 16-lane row: step 1 by DPP, no LDS
+        const T p1 = dpp_next(p);
+        const uint32_t c1 = dpp_next32(code);
+        if (more) {
+          acc = acc + p1;
+          more = (c1 & kVcMore) != 0;
+        }
+        k0 = 2;
+      }
+      for (uint32_t k = k0; __builtin_amdgcn_ballot_w64(more) != 0; ++k) {  // wave-uniform trip count
         const T pk = __shfl_down(p, k);
         const uint32_t ck = __shfl_down(code, k);
         if (more) {
@@ -313,7 +338,59 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
         } while (cd & kVcMore);
         if (lw == l) acc = a;
       }
-      if (own) ylds[row] = acc;
+      if (own) {
+        if (AB & 16384)  // one LDS atomic (ds_add_f64 / ds_add_u64) instead of the read and the write
+          __hip_atomic_fetch_add(&ylds[row], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+          ylds[row] = acc;
+      }
+    }
+  };
+
+  // CX == 5 (a layout whose runs stay inside 16-lane rows, place_segments_banked):
+  // the same arithmetic as CX 1-3 without branches around the LDS accesses --
+  // both slots' x and y reads issue together, then one wait (CX 3 waited for
+  // the x read, then the y read, per slot: four round trips per step) -- and
+  // the step's segment bounds come from registers (beg, end) instead of LDS.
+  // A run head takes its first continuation from the next lane by DPP, longer
+  // runs by shuffles as in CX 1-3; no run leaves its row, so none leaves the wave.
+  auto apply5 = [&](uint32_t s, const uint32_t* c, const T* v, uint32_t beg, uint32_t end) {
+    if (AB & 8) return;
+    const T* xs = xb[s & 1];
+    T xv[EPT], yv[EPT], p[EPT], acc[EPT];
+    uint32_t row[EPT];
+    bool own[EPT], more[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      row[j] = (c[j] >> 16) & 0x3FFF;
+      xv[j] = xs[c[j] & 0xFFFF];  // unconditional: every lane's code is a clamped entry, in range
+      yv[j] = ylds[row[j]];
+    }
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const bool valid = beg + ct + j * CT < end;
+      p[j] = valid ? v[j] * xv[j] : T(0);  // rounded product (contract off)
+      own[j] = valid && !(c[j] & kVcCont);
+      acc[j] = own[j] ? yv[j] + p[j] : T(0);
+      more[j] = own[j] && (c[j] & kVcMore);
+      const T p1 = dpp_next(p[j]);
+      const uint32_t c1 = dpp_next32(c[j]);
+      if (more[j]) {
+        acc[j] = acc[j] + p1;
+        more[j] = (c1 & kVcMore) != 0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      for (uint32_t k = 2; __builtin_amdgcn_ballot_w64(more[j]) != 0; ++k) {  // runs of 3+ (rare)
+        const T pk = __shfl_down(p[j], k);
+        const uint32_t ck = __shfl_down(c[j], k);
+        if (more[j]) {
+          acc[j] = acc[j] + pk;
+          more[j] = (ck & kVcMore) != 0;
+        }
+      }
+      if (own[j]) ylds[row[j]] = acc[j];
     }
   };
 
@@ -437,6 +514,43 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     auto entries = [&](auto ntc) {
       uint32_t EC[DE][EPT];
       T EV[DE][EPT];
+      if constexpr (CX == 5) {
+        // segment bounds ride with the ring: SB/SE[i] of the step slot i holds
+        uint32_t SB[DE], SE[DE];
+#pragma unroll
+        for (int i = 0; i < DE; ++i) {
+          SB[i] = segl[min((uint32_t)i, npad)];
+          SE[i] = segl[min((uint32_t)i + 1, npad)];
+          load_e(i, EC[i], EV[i], ntc, SB[i]);
+        }
+        barrier();
+        tr_rel(255, t_entry, 0);
+        for (uint32_t base = 0; base < nsteps; base += DE) {
+#pragma unroll
+          for (int i = 0; i < DE; ++i) {
+            const uint32_t s = base + i;
+            // the bounds of step s + DE, read before the apply so their LDS latency hides behind it
+            const uint32_t nb = segl[min(s + DE, npad)], ne = segl[min(s + DE + 1, npad)];
+            uint32_t t_ready = 0, t_arr = 0, t_app = 0;
+            if (AB & 8192) {
+              vm_wait<1 + (2 * EPT + 1) * (DE - 1)>();
+              t_ready = tr_now();
+            }
+            if (s < npu) apply5(s, EC[i], EV[i], SB[i], SE[i]);
+            if (AB & 8192) {
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              t_app = tr_now();
+            }
+            SB[i] = nb;
+            SE[i] = ne;
+            load_e(s + DE, EC[i], EV[i], ntc, nb);
+            if (AB & 8192) t_arr = tr_now();
+            pbarrier();
+            tr_rel(s, t_ready, t_arr, t_app);
+          }
+        }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i], ntc);
       barrier();
@@ -526,10 +640,14 @@ static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
       launch_one<T, SPLIT, 1, 2, MAP>(a, s);
     else if (cx == 3)
       launch_one<T, SPLIT, 1, 3, MAP>(a, s);
+    else if (cx == 5)
+      launch_one<T, SPLIT, 1, 5, MAP>(a, s);
     else
       launch_one<T, SPLIT, 1, 4, MAP>(a, s);
   } else if (cx == 4) {  // (split 3 only)
     launch_one<T, SPLIT, 0, 3, MAP>(a, s);
+  } else if (cx == 5) {  // (a banked layout: runs inside 16-lane rows)
+    launch_one<T, SPLIT, 0, 5, MAP>(a, s);
   } else if (cx == 0) {
     ld == 1 ? launch_one<T, SPLIT, 1, 0, MAP>(a, s) : launch_one<T, SPLIT, 0, 0, MAP>(a, s);
   } else if (cx == 1) {
@@ -557,10 +675,14 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   // xlane 1: cross-lane continuation; 2: also padded loops and asm rings
   // (entries, and x unless LDS-DMA stages it) with explicit vmcnt waits;
   // 3: cross-lane continuation and padded loops, the compiler's own waits;
-  // 4 (split 3): 3 with the entry loads masked past each step's segment.
-  // -1 (default): 3 for the split geometry (C3: 131.7 us against 135.7 with
-  // the run continuation re-read from memory), 0 for the others.
-  const int xl = a.xlane < 0 ? (a.split == 3 ? 3 : 0) : a.xlane;
+  // 4 (split 3): 3 with the entry loads masked past each step's segment;
+  // 5 (split 3, a layout whose runs stay inside 16-lane rows --
+  // place_segments_banked): 3 with the first continuation step by DPP.
+  // -1 (default): 5 for the split geometry where the layout allows it, else 3
+  // (C3: 131.7 us against 135.7 with the run continuation re-read from
+  // memory), 0 for the others.
+  int xl = a.xlane < 0 ? (a.split == 3 ? (a.row_runs ? 5 : 3) : 0) : a.xlane;
+  if (xl == 5 && !a.row_runs) xl = 3;
   const int cx = xl && a.max_seg <= window(a.split) ? xl : 0;
   // dma -1 (default): register-staged x loaders; the split geometry's two
   // loader waves always stage by LDS-DMA (dispatch)

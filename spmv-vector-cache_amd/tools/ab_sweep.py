@@ -25,6 +25,16 @@ sys.path.insert(0, os.path.dirname(HERE))
 import hipspmv as hs  # noqa: E402
 
 SETS = {
+    # round 5: the ORDERED vcache (bit-exact) on the banked layout, run continuation by memory re-reads
+    # (xlane 0, the default), cross-lane (3) or DPP (5); checked bit-exact against the row-order layout
+    "ordered": [("ordered banked xl0", "vcache", {}), ("ordered row order xl0", "bank0:vcache", {}),
+                ("ordered banked xl3", "vcache", {"vcache_xlane": 3}),
+                ("ordered banked xl5", "vcache", {"vcache_xlane": 5}),
+                ("ordered banked xl5 nt none", "vcache", {"vcache_xlane": 5, "vcache_nt": 1 << 30}),
+                ("ordered banked xl5 nt all", "vcache", {"vcache_xlane": 5, "vcache_nt": 0})],
+    # round 5: the split kernel's first run-continuation step by DPP (xlane 5, the default on banked layouts)
+    "dpp": [("split dpp (default)", "vcache_split", {}), ("split xlane 3", "vcache_split", {"vcache_xlane": 3}),
+            ("split row order", "bank0:vcache_split", {})],
     # round 5: the split layout's LDS-bank-aware placement against the (row, column) order
     # ("bank0": a second handle created with HIPSPMV_VCACHE_BANK=0)
     "bank": [("split banked", "vcache_split", {}), ("split row order", "bank0:vcache_split", {}),
@@ -63,8 +73,11 @@ def main():
     xd = torch.from_numpy(x).cuda()
     yd = torch.empty(n, dtype=torch.float64, device="cuda")
     s = torch.cuda.current_stream()
-    h.set_kernel("vcache")
-    h.exec_device(xd, yd, beta=0, mode=hs.MODE_ORDERED, stream=s)
+    # the reference: the ORDERED kernel (bit-exact to SoftwareSpMV by the GPU tests), on the row-order
+    # layout when the set has that handle
+    href = hb if hb is not None else h
+    href.set_kernel("vcache")
+    href.exec_device(xd, yd, beta=0, mode=hs.MODE_ORDERED, stream=s)
     y_ref = yd.cpu().numpy().copy()
     lens = np.diff(rowptr.astype(np.int64))
     absprod = np.bincount(np.repeat(np.arange(n), lens), weights=np.abs(vals * x[colind]), minlength=n)
@@ -84,9 +97,11 @@ def main():
         for k in opts:
             cur[0].set_option(k, {"vquad_variant": 0, "vcache_nt": -1}.get(k, -1))
 
+    mode = hs.MODE_ORDERED if a.set == "ordered" else hs.MODE_FAST
+
     def run(k):
         for _ in range(k):
-            cur[0].exec_device(xd, yd, beta=0, mode=hs.MODE_FAST, stream=s)
+            cur[0].exec_device(xd, yd, beta=0, mode=mode, stream=s)
 
     checks = {}
     y_first = None
@@ -99,13 +114,16 @@ def main():
         r = np.abs(y1 - y_ref) / bound
         checks[label] = {"within_bound": bool(np.all(r <= 1.0)), "max_err_over_bound": round(float(r.max()), 3),
                          "deterministic": y1.tobytes() == y2.tobytes()}
+        if mode == hs.MODE_ORDERED:  # y_ref came from the ordered kernel on the row-order layout? (below)
+            checks[label]["bit_exact_vs_ordered_ref"] = y1.tobytes() == y_ref.tobytes()
         if y_first is None:
             y_first = y1
         else:
             checks[label]["bits_equal_first_config"] = y1.tobytes() == y_first.tobytes()
         reset(opts)
-    select("vcache_split", {})
+    select(cfgs[0][1], cfgs[0][2])
     run(400)
+    reset(cfgs[0][2])
     torch.cuda.synchronize()
     times = {c[0]: [] for c in cfgs}
     for rnd in range(a.rounds):

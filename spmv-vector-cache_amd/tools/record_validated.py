@@ -21,6 +21,7 @@ import kernel_isa  # noqa: E402
 # the instantiations choose_kernel (csrc/capi.cpp) can launch without options
 PRODUCT = [f"void hipspmv::k_{k}<{t}{a}>" for t in ("double", "unsigned long")
            for k, a in (("vcache", ", 1, 8, 4, 3, 0, 0, false, 0, 0"), ("vcache", ", 3, 3, 4, 2, 0, 0, false, 1, 3"),
+                        ("vcache", ", 3, 3, 4, 2, 0, 0, false, 1, 5"),
                         ("csr_lane", ""), ("csr_vector", ", false"), ("wgather", ", 16, 4, 2, true, true"), ("wgather", ", 16, 4, 3, true, true"),
                         ("wgather", ", 16, 2, 6, true, true"), ("wgather", ", 16, 2, 9, true, true"),
                         ("wgather", ", 16, 4, 2, true, false"))] + \

@@ -16,6 +16,7 @@
 #include "../csrc/vcache.hip"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -70,6 +71,8 @@ int main(int argc, char** argv) {
   const VcGeom g = kVcSplit;
   VcacheLayout L;
   build_vcache(a, g, L);
+  const bool row_order = argc > 1 && std::string(argv[1]) == "roworder";
+  if (!row_order) place_segments_banked(L, kVcSplitCT);  // the product layout (capi.cpp upload_vc)
   const uint32_t units = L.nblocks * g.split;
   if (!vcache_grid_ok(a.rows, a.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels, L.npad,
                       (uint32_t)g.panel, g.split, g) ||
@@ -94,9 +97,30 @@ int main(int argc, char** argv) {
                        dy, dpart, dtick, a.rows, a.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels,
                        L.npad, a.nnz - 1, 0, 0u);
   };
-  auto product = k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 3>;
-  auto traced = k_vcache<double, 3, 3, 4, 2, 8192 | 64, 0, false, 1, 3>;
-  auto nocomb = k_vcache<double, 3, 3, 4, 2, 64, 0, false, 1, 3>;
+  // the product: xlane 5 on the banked layout (runs inside 16-lane rows), xlane 3 on the row-order one
+  const bool x5 = !row_order && L.row_runs;
+  auto product = x5 ? k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 5> : k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 3>;
+  auto traced = x5 ? k_vcache<double, 3, 3, 4, 2, 8192 | 64, 0, false, 1, 5>
+                   : k_vcache<double, 3, 3, 4, 2, 8192 | 64, 0, false, 1, 3>;
+  auto nocomb = x5 ? k_vcache<double, 3, 3, 4, 2, 64, 0, false, 1, 5> : k_vcache<double, 3, 3, 4, 2, 64, 0, false, 1, 3>;
+  // configurations on the same layout (the register window must hold every segment)
+  struct V {
+    const char* name;
+    void (*k)(const uint32_t*, const uint32_t*, const double*, const double*, const double*, double*, double*,
+              uint32_t*, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, int,
+              uint32_t);
+    uint32_t window;
+  };
+  const V vars[] = {{"product", product, 13 * 64 * 2},
+                    {"xlane 3 (WL3 DE4 EPT2)", k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 3>, 13 * 64 * 2},
+                    {"xlane 5 WL3 DE6", k_vcache<double, 3, 3, 6, 2, 0, 0, false, 1, 5>, 13 * 64 * 2},
+                    {"xlane 5 WL2 DE4", k_vcache<double, 3, 2, 4, 2, 0, 0, false, 1, 5>, 14 * 64 * 2},
+                    {"y by LDS atomic", k_vcache<double, 3, 3, 4, 2, 16384, 0, false, 1, 3>, 13 * 64 * 2},
+                    {"WL2 DE4 EPT2", k_vcache<double, 3, 2, 4, 2, 0, 0, false, 1, 3>, 14 * 64 * 2},
+                    {"WL2 DE4 EPT2 y atomic", k_vcache<double, 3, 2, 4, 2, 16384, 0, false, 1, 3>, 14 * 64 * 2},
+                    {"WL3 DE6 EPT2", k_vcache<double, 3, 3, 6, 2, 0, 0, false, 1, 3>, 13 * 64 * 2},
+                    {"WL3 DE3 EPT2", k_vcache<double, 3, 3, 3, 2, 0, 0, false, 1, 3>, 13 * 64 * 2},
+                    {"WL4 DE4 EPT2", k_vcache<double, 3, 4, 4, 2, 0, 0, false, 1, 3>, 12 * 64 * 2}};
   auto timeit = [&](auto kern, int reps) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -111,6 +135,19 @@ int main(int argc, char** argv) {
   };
   for (int i = 0; i < 400; ++i) launch(product);
   CK(hipDeviceSynchronize());
+  std::vector<double> y0(n), y1(n);
+  launch(product);
+  CK(hipMemcpy(y0.data(), dy, 8ull * n, hipMemcpyDeviceToHost));
+  for (int round = 0; round < 3; ++round)
+    for (const V& v : vars) {
+      if (L.max_seg > v.window) continue;
+      const double us = timeit(v.k, 100);
+      launch(v.k);
+      CK(hipMemcpy(y1.data(), dy, 8ull * n, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (uint32_t i = 0; i < n; ++i) md = std::max(md, std::fabs(y1[i] - y0[i]) / (std::fabs(y0[i]) + 1e-300));
+      std::printf("round %d  %-26s %8.2f us  max rel diff vs product %.1e\n", round, v.name, us, md);
+    }
   std::printf("C3 FAST, %u units, %u steps per unit: product %.2f us, without combine %.2f us, traced %.2f us\n",
               units, L.part_panels, timeit(product, 100), timeit(nocomb, 100), timeit(traced, 100));
   CK(hipMemset(dpart, 0, 16ull * units * 16 * 256));

@@ -659,7 +659,8 @@ int main(int argc, char** argv) {
       // a permutation inside every segment, runs consecutive inside one wave,
       // and the same result bits as the (row, column) layout
       VcacheLayout B;
-      const bool banked = c.SPLIT == 3 && c.LD == 1 && c.CX >= 2;  // the product: xlane 3 (modelled as CX 2)
+      // the product layouts: split (xlane 3, modelled as CX 2) and the ordered geometry
+      const bool banked = (c.SPLIT == 3 && c.LD == 1 && c.CX >= 2) || (c.SPLIT == 1 && c.LD != 2);
       if (banked) {
         B = L;
         const uint32_t CT = (uint32_t)(16 - c.WL) * 64;
@@ -673,8 +674,9 @@ int main(int argc, char** argv) {
             for (uint32_t e = s0; e < s1; ++e) {
               a0.emplace_back(L.code[e], L.vals[e]);
               a1.emplace_back(B.code[e], B.vals[e]);
-              if ((B.code[e] & kVcCont) && (e == s0 || !(B.code[e - 1] & kVcMore) || (e - s0) % 64 == 0))
-                perm = false;  // a continuation right after its run's previous entry, same wave
+              if ((B.code[e] & kVcCont) && (e == s0 || !(B.code[e - 1] & kVcMore) ||
+                                             (B.row_runs && (e - s0) % 16 == 0)))
+                perm = false;  // a continuation right after its run's previous entry (row_runs: same DPP row)
             }
             std::sort(a0.begin(), a0.end());
             std::sort(a1.begin(), a1.end());
