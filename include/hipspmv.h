@@ -119,8 +119,9 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
  * VCACHE_SPLIT launches run in their default configuration with in-kernel
  * stamps, and the NewCache state statistics below are measured; results are
  * bit-identical to the unprofiled kernel), "vcache_nt" (row blocks b >=
- * vcache_nt of VCACHE / VCACHE_SPLIT load their entries non-temporally; -1
- * default: every block for VCACHE_SPLIT, the second half for VCACHE; WGATHER:
+ * vcache_nt of VCACHE / VCACHE_SPLIT load their entries non-temporally, the
+ * blocks before them stay in the Infinity Cache across launches; -1 default:
+ * about 192 MiB of entries resident -- C3: half the blocks of either; WGATHER:
  * 0 or -1 non-temporal, > 0 the default policy), "sell_nt" (SELL slices s >=
  * sell_nt likewise; -1 default: the second half).  The cache policy never
  * changes a result bit.  "vquad_variant" (VCACHE_SPLIT4 configuration,

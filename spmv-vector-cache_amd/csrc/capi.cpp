@@ -133,9 +133,12 @@ struct hipspmv_handle {
   // measured 6 % slower)
   bool wcsr_line_order = false;
   // option "vcache_nt": row blocks b >= vcache_nt load their entries
-  // non-temporally; -1 default: every block for the split
-  // geometry, the second half of the blocks for the ordered one
+  // non-temporally; -1 default: about kVcResidentBytes of
+  // entries resident (resident_blocks; C3: half the blocks of either geometry)
   int64_t vcache_nt = -1;
+  // option "wcsr_res": wcsr segment-pass groups g < wcsr_res load their entries
+  // with the default policy (Infinity-Cache resident); 0 default: all non-temporal
+  int64_t wcsr_res = 0;
   // option "sell_nt": SELL slices s >= sell_nt load their entries
   // non-temporally (-1 default: the second half of the slices)
   int64_t sell_nt = -1;
@@ -705,6 +708,19 @@ static int ensure_layout(hipspmv_t* h, int kernel) {
   return st;
 }
 
+// Row blocks of a vcache layout whose entries load with the default cache
+// policy, so they stay in the 256 MiB Infinity Cache from one launch to the
+// next; the rest load non-temporally (nt lines do not displace resident ones,
+// DESIGN.md §6.10).  About kVcResidentBytes of entries stay resident: C3 (384
+// MiB of entries) keeps half its blocks -- split 101.9 -> 98.0 us, ordered
+// 179 -> 168 us with the banked layouts; more starves x of L2
+// and MALL (5/8: 102.6 us).
+static uint32_t resident_blocks(uint32_t nblocks, uint64_t nnz) {
+  const double entry_bytes = 12.0 * (double)nnz;
+  if (entry_bytes <= (double)kVcResidentBytes) return nblocks;
+  return (uint32_t)((double)nblocks * (double)kVcResidentBytes / entry_bytes);
+}
+
 static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in, void* d_y_out, int beta,
                   hipStream_t s, int mode) {
   hipError_t e = hipSuccess;
@@ -749,7 +765,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                  v.npad,      h->nnz - 1, v.split,   beta, h->vcache_dma, (uint32_t)geoms[k].panel,
                  h->vcache_xlane, v.max_seg, h->vcache_map};
     a.nt_from = h->vcache_nt >= 0 ? (uint32_t)std::min<int64_t>(h->vcache_nt, UINT32_MAX)
-                : k == 1 ? 0u : k == 0 ? v.nblocks / 2 : ~0u;
+                : k < 2 ? resident_blocks(v.nblocks, h->nnz) : ~0u;
     a.row_runs = v.row_runs;
     // an unprofiled launch leaves an unread profile of an earlier launch readable
     // (it writes no stamps); d_prof is allocated when the option is set, never
@@ -794,6 +810,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                w.d_rgroups, w.rgroups,   w.d_ypart, d_x,      d_y_in,     d_y_out,  h->rows, beta};
     a.chunks = w.d_chunks;
     a.nchunks = w.nchunks;
+    a.res_groups = (uint32_t)std::min<int64_t>(h->wcsr_res, w.ngroups);
     a.cols = h->cols;
     e = launch_wcsr(h->dtype, a, s);
   } else {
@@ -947,8 +964,9 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "vcache_dma") {
     if (value < -1 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_dma = (int)value;
-  } else if (k == "vcache_map") {
-    h->vcache_map = value ? 1 : 0;
+  } else if (k == "vcache_map") {  // 1: split4 XCD pairs; 2: split, one column part per XCD where it can
+    if (value < 0 || value > 2) return HIPSPMV_ERR_INVALID_ARG;
+    h->vcache_map = (int)value;
   } else if (k == "vquad_variant") {  // k_vquad configuration (csrc/vquad.hip)
     if (value < 0 || value > 26) return HIPSPMV_ERR_INVALID_ARG;
     // 6-16 are timing ablations that give wrong y (or race): experimental builds only
@@ -972,6 +990,9 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "sell_nt") {  // first SELL slice whose entries load non-temporally (-1: half)
     if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->sell_nt = value;
+  } else if (k == "wcsr_res") {  // wcsr segment-pass groups below it keep their entries resident
+    if (value < 0 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
+    h->wcsr_res = value;
   } else if (k == "vcache_nt") {  // first row block whose entries load non-temporally (-1: per geometry)
     if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_nt = value;
@@ -1117,6 +1138,7 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "wcsr_max_segment") *out = h->wc.max_seg;
   else if (k == "wcsr_window_log2") *out = h->wc.built ? h->wc.log2w : kWcLog2Window;
   else if (k == "wcsr_chunks") *out = h->wc.nchunks;
+  else if (k == "wcsr_groups") *out = h->wc.ngroups;
   else if (k == "sell_slices") *out = h->sell.nslices;
   else if (k == "sell_hubs") *out = h->sell.nhubs;
   else if (k == "sell_iso_hubs") *out = h->sell.niso;

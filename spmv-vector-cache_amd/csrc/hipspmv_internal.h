@@ -55,6 +55,9 @@ constexpr VcGeom kWgWindow{16384, 1 << 16, 1, 16, 512};
 // (profiles/r03/logs/sweep_c4_s7.log): one launch 6468 us, chunks of 1024
 // 5287, 512 (two per CU) 4078, 256 (one per CU) 3620.
 constexpr uint32_t kWgChunk = 256;
+// Entry bytes of a vcache layout kept resident in the Infinity Cache across
+// launches (capi.cpp resident_blocks): half of the 384 MiB of C3's entries
+constexpr uint64_t kVcResidentBytes = 192ull << 20;
 constexpr int kVcThreads = 1024;
 constexpr int kVcSegMax = 256;        // npad + 1 <= kVcSegMax per unit
 constexpr int kVcEpt = 2;             // entries per thread held in registers per panel

@@ -60,6 +60,8 @@ struct WcsrArgs {  // csr_vector over the column-windowed segment matrix, then k
   uint32_t rows;
   int beta;
   const uint32_t* chunks = nullptr;  // LDS form (k_wseg): (window, first group, end group) per workgroup
+  uint32_t res_groups = 0;  // segment-pass groups g < res_groups load entries with the default policy
+                            // (Infinity-Cache resident across launches; k_wpass), the rest non-temporal
   uint32_t nchunks = 0;
   uint32_t cols = 0;
 };

@@ -237,6 +237,28 @@ __global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__
   csr_vector_group<T, NTE ? 1 : 0>(rowptr, colind, vals, x, y_in, y_out, groups, ngroups, beta);
 }
 
+// k_wpass (wcsr segment pass with resident entries): the groups g <
+// res_groups load their entries with the default cache policy, so those lines
+// stay in the Infinity Cache across launches, the others non-temporally (the
+// split vcache's residency); the arithmetic is k_csr_vector's
+template <typename T>
+__global__ __launch_bounds__(256) void k_wpass(const uint32_t* __restrict__ rowptr,
+                                                const uint32_t* __restrict__ colind, const T* __restrict__ vals,
+                                                const T* __restrict__ x, T* __restrict__ ypart,
+                                                const uint32_t* __restrict__ groups, uint32_t ngroups,
+                                                uint32_t res_groups) {
+  __shared__ uint32_t heads[4][kCvGroupNnz / 32];
+  const int w = threadIdx.x >> 6;
+  const uint32_t g = blockIdx.x * 4 + w;
+  if (g >= ngroups) return;  // wave-uniform
+  auto xv = [&](uint32_t c) { return x[c]; };
+  const RowOut<T> out{(const T*)nullptr, ypart, 0};
+  if (g >= res_groups)
+    csr_vector_rows<T, 1>(rowptr, colind, vals, xv, out, groups[g], groups[g + 1], heads[w]);
+  else
+    csr_vector_rows<T, 0>(rowptr, colind, vals, xv, out, groups[g], groups[g + 1], heads[w]);
+}
+
 // k_wreduce (wcsr): y[r] = (y_in[r] +) the sum of row r's segment partials
 // ypart[segidx[k]], k in [rowseg[r], rowseg[r+1]) (window order), over the
 // reduce's own balanced row groups -- a fixed order, so wcsr is
@@ -272,6 +294,9 @@ hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
   if (a.nchunks)
     hipLaunchKernelGGL(k_wseg<T>, dim3(a.nchunks), dim3(1024), 0, s, a.chunks, a.groups, a.seg_rowptr, a.seg_colind,
                        (const T*)a.seg_vals, (const T*)a.x, a.cols, (T*)a.ypart);
+  else if (a.ngroups && a.res_groups)
+    hipLaunchKernelGGL(k_wpass<T>, dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,
+                       (const T*)a.seg_vals, (const T*)a.x, (T*)a.ypart, a.groups, a.ngroups, a.res_groups);
   else if (a.ngroups)
     hipLaunchKernelGGL((k_csr_vector<T, true>), dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr,
                        a.seg_colind, (const T*)a.seg_vals, (const T*)a.x, (const T*)nullptr, (T*)a.ypart,

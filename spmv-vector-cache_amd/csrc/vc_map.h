@@ -29,6 +29,22 @@ constexpr void vc_unit_map1(uint32_t slot, uint32_t& b, uint32_t& h) {
   b = (slot / 8) * (8 / SPLIT) + grp % (8 / SPLIT);
 }
 
+// MAP 2 (any SPLIT > 1, any grid G = nblocks * SPLIT <= 256): the units in
+// part-major order (u = h * nblocks + b) are dealt to the XCDs in contiguous
+// runs -- XCD k (the slots s with s mod 8 == k) takes units [off_k, off_k +
+// c_k), c_k = its slot count -- so each XCD's L2 serves one column part of x
+// (C3, 3 parts of 85 blocks: six XCDs hold one part, two hold two) instead of
+// all of x.  The parts of a block then sit on different XCDs (the combine
+// hand-off is placement-independent, csrc/combine.h).
+constexpr void vc_unit_map2(uint32_t slot, uint32_t G, uint32_t nblocks, uint32_t& b, uint32_t& h) {
+  const uint32_t k = slot % 8, j = slot / 8;
+  uint32_t off = 0;
+  for (uint32_t q = 0; q < k; ++q) off += (G - q + 7) / 8;  // slots on XCD q: ceil((G - q) / 8)
+  const uint32_t u = off + j;
+  h = u / nblocks;
+  b = u % nblocks;
+}
+
 template <int SPLIT>
 constexpr void vc_unit_map0(uint32_t slot, uint32_t nblocks, uint32_t& b, uint32_t& h) {
   if (SPLIT == 1) {

@@ -118,6 +118,8 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   uint32_t b = blockIdx.x, h = 0;
   if (MAP == 1 && SPLIT > 1 && vc_map1_applies<SPLIT>(nblocks)) {
     vc_unit_map1<SPLIT>(blockIdx.x, b, h);  // XCD-aware placement (csrc/vc_map.h)
+  } else if (MAP == 2 && SPLIT > 1) {
+    vc_unit_map2(blockIdx.x, nblocks * SPLIT, nblocks, b, h);  // one column part per XCD where it can
   } else if (SPLIT > 1) {  // unit i -> (b, h): the parts of a block are 8 dispatch slots apart (vc_unit_map0)
     const uint32_t g = blockIdx.x / (8 * SPLIT), rem = blockIdx.x % (8 * SPLIT);
     const uint32_t nbg = min(8u, nblocks - g * 8);
@@ -690,6 +692,8 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   const int ld = dma ? 1 : cx == 2 ? 2 : 0;
   if (a.split == 1)
     dispatch<T, 1>(a, s, ld, cx);
+  else if (a.split == 3 && a.map == 2 && cx == 5)  // (option "vcache_map" 2)
+    launch_one<T, 3, 1, 5, 2>(a, s);
   else if (a.split == 3)
     dispatch<T, 3>(a, s, ld, cx);
   else  // four parts: k_vquad (csrc/vquad.hip) runs that layout

@@ -25,6 +25,23 @@ sys.path.insert(0, os.path.dirname(HERE))
 import hipspmv as hs  # noqa: E402
 
 SETS = {
+    "resid2": [("split resident 1/2", "vcache_split", {"vcache_nt": 42}),
+               ("split resident 7/16", "vcache_split", {"vcache_nt": 37}),
+               ("split resident 17/32", "vcache_split", {"vcache_nt": 45}),
+               ("split resident 9/16", "vcache_split", {"vcache_nt": 48}),
+               ("split resident 1/2 map 2", "vcache_split", {"vcache_nt": 42, "vcache_map": 2}),
+               ("split resident 9/16 map 2", "vcache_split", {"vcache_nt": 48, "vcache_map": 2}),
+               ("split resident 5/8 map 2", "vcache_split", {"vcache_nt": 53, "vcache_map": 2})],
+    # round 5: Infinity-Cache residency of the split kernel's entries on the banked layout (blocks < vcache_nt
+    # load with the default policy; C3 has 85 row blocks)
+    "resid": [("split all nt (product)", "vcache_split", {}),
+              ("split resident 1/8", "vcache_split", {"vcache_nt": 11}),
+              ("split resident 1/4", "vcache_split", {"vcache_nt": 21}),
+              ("split resident 3/8", "vcache_split", {"vcache_nt": 32}),
+              ("split resident 1/2", "vcache_split", {"vcache_nt": 42}),
+              ("split resident 5/8", "vcache_split", {"vcache_nt": 53})],
+    # round 5: the split kernel with one column part per XCD where it can (vcache_map 2)
+    "map": [("split (product)", "vcache_split", {}), ("split map 2", "vcache_split", {"vcache_map": 2})],
     # round 5: the ORDERED vcache (bit-exact) on the banked layout, run continuation by memory re-reads
     # (xlane 0, the default), cross-lane (3) or DPP (5); checked bit-exact against the row-order layout
     "ordered": [("ordered banked xl0", "vcache", {}), ("ordered row order xl0", "bank0:vcache", {}),
@@ -95,7 +112,7 @@ def main():
 
     def reset(opts):
         for k in opts:
-            cur[0].set_option(k, {"vquad_variant": 0, "vcache_nt": -1}.get(k, -1))
+            cur[0].set_option(k, {"vquad_variant": 0, "vcache_nt": -1, "vcache_map": 0}.get(k, -1))
 
     mode = hs.MODE_ORDERED if a.set == "ordered" else hs.MODE_FAST
 

@@ -386,12 +386,14 @@ template <int SPLIT>
 static int check_maps() {
   int bad = 0;
   for (uint32_t nb = 1; nb <= 300; ++nb) {
-    for (int map = 0; map < 2; ++map) {
+    for (int map = 0; map < 3; ++map) {
       if (map == 1 && !vc_map1_applies<SPLIT>(nb)) continue;
       std::vector<int> seen((size_t)nb * SPLIT, 0);
       for (uint32_t slot = 0; slot < nb * SPLIT; ++slot) {
         uint32_t b = 0, h = 0;
-        if (map)
+        if (map == 2)
+          vc_unit_map2(slot, nb * SPLIT, nb, b, h);
+        else if (map)
           vc_unit_map1<SPLIT>(slot, b, h);
         else
           vc_unit_map0<SPLIT>(slot, nb, b, h);
@@ -400,7 +402,7 @@ static int check_maps() {
           continue;
         }
         seen[(size_t)b * SPLIT + h]++;
-        if (map && h != (slot % 8) / (8 / SPLIT)) ++bad;  // part h on XCDs of group h
+        if (map == 1 && h != (slot % 8) / (8 / SPLIT)) ++bad;  // part h on XCDs of group h
       }
       for (int c : seen) bad += c != 1;
     }

@@ -213,6 +213,11 @@ def test_wcsr_wide_windows(gpu, dtype):
             np.add.at(absprod, row_of, np.abs(vals * x[colind]))
             bound = _fast_bound(lens, absprod, y0 if beta else np.zeros(rows))
             assert np.all(np.abs(ys[0] - y_ref) <= bound)
+    # the segment pass with half its groups' entries resident (option wcsr_res, k_wpass): the same bits
+    y_nt = h.exec(x, y0.copy(), beta=1, mode=hs.MODE_FAST)
+    h.set_option("wcsr_res", h.stat("wcsr_groups") // 2)
+    assert h.exec(x, y0.copy(), beta=1, mode=hs.MODE_FAST).tobytes() == y_nt.tobytes()
+    h.set_option("wcsr_res", 0)
     if dtype == np.float64:
         with pytest.raises(hs.HipSpMVError):  # FAST only
             h.exec(x, beta=0, mode=hs.MODE_ORDERED)
