@@ -989,3 +989,45 @@ def test_stream_bandwidth(gpu):
     # the bench's second denominator (hipspmv_stream_bandwidth, csrc/stream.hip): plausible GB/s on an MI355X
     cp, rd = hs.stream_bandwidth(0, 1 << 28, 5)
     assert 1000 < cp < 8000 and 1000 < rd < 8000, (cp, rd)
+
+
+def test_live_cache_statistics_from_rocprofv3(gpu, tmp_path):
+    """The reference reads its cache counters from the accelerator after every
+    run (HardwareSpMVNewCache.cpp:161-173).  Here: spmvbench runs once as a
+    fresh child under `rocprofv3 --pmc TCC_MISS SQ_LDS_BANK_CONFLICT` (the
+    program right after --), then again with that run's counter CSV (--pmc):
+    the row's readMisses / hazardStalls equal the profiled run's counters of
+    the kernel that ran, matched by its name."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    bench = [f"{hs.LIB_DIR}/spmvbench", "--dir", fx.MATRICES, "--confs", "hip", "--cms", "0", "--mode", "fast",
+             "--reps", "5", "circuit204"]
+    out_dir = tmp_path / "pmc"
+    prof = subprocess.run([exe, "--pmc", "TCC_MISS", "SQ_LDS_BANK_CONFLICT", "-d", str(out_dir), "-o", "run",
+                           "--output-format", "csv", "--"] + bench, capture_output=True, text=True, timeout=120,
+                          env=dict(os.environ, TMPDIR="/tmp"))
+    assert prof.returncode == 0, prof.stdout[-2000:] + prof.stderr[-2000:]
+    csvs = glob.glob(str(out_dir / "**" / "*counter_collection.csv"), recursive=True)
+    assert csvs, prof.stdout[-2000:]
+    run = subprocess.run(bench[:-1] + ["--pmc", csvs[0], "circuit204"], capture_output=True, text=True, timeout=120)
+    assert run.returncode == 0, run.stdout + run.stderr
+    lines = run.stdout.splitlines()
+    keys = next(l for l in lines if l.startswith("diffFromGolden,")).rstrip(",").split(",")
+    rec = dict(zip(keys, [l for l in lines if l[:1].isdigit()][-1].rstrip(",").split(",")))
+    # the kernel that ran: the hipspmv kernel of the profiled run (one SpMV per spmvbench row)
+    per = {}
+    with open(csvs[0]) as f:
+        for row in csv.DictReader(f):
+            if "hipspmv::" in row["Kernel_Name"]:
+                per.setdefault((row["Kernel_Name"], row["Counter_Name"]), {})[row["Dispatch_Id"]] = \
+                    float(row["Counter_Value"])
+    names = {k for k, _ in per}
+    main = max(names, key=lambda n: len(per.get((n, "TCC_MISS"), {})))  # the SpMV kernel (most dispatches)
+    miss = per[(main, "TCC_MISS")]
+    conf = per[(main, "SQ_LDS_BANK_CONFLICT")]
+    assert int(rec["readMisses"]) == round(sum(miss.values()) / len(miss)), (main, rec["readMisses"])
+    assert int(rec["hazardStalls"]) == round(sum(conf.values()) / len(conf)), (main, rec["hazardStalls"])
+    assert "readMissesModel" in rec and "hazardStallsModel" in rec

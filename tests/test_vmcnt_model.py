@@ -159,3 +159,28 @@ def test_compiled_rings_pass_the_dataflow_check(tmp_path):
                              capture_output=True, text=True)
         assert out.returncode == 0, out.stdout
         assert out.stdout.count(": 0 violations") >= {"vcache.hip": 24, "wgather.hip": 6, "sell.hip": 6, "vquad.hip": 10}[src], out.stdout
+
+
+def test_overlap_probe_rings_pass_the_dataflow_check(tmp_path):
+    """The round-4 overlap probe's GPU fault (DESIGN.md
+    §9.4): its k_gather (the G skeletons) read and overwrote VGPRs that asm
+    loads were still writing -- 35 violations in the D=0 instantiation of the
+    faulting revision (13a60ea), among them an address register rewritten under
+    an in-flight load -- and the fault surfaced at the synchronisation after
+    G's warm-up launches (overlap_probe.hip:306 there).  The fixed probe ties
+    every asm-loaded register to its wait (vm_wait_tie): every kernel in it
+    passes tools/vmcnt_check.py."""
+    import os
+    import subprocess
+    import sys
+    import hipspmv as hs
+    src = os.path.join(hs.PKG_DIR, "tools", "overlap_probe.hip")
+    asm = tmp_path / "overlap_probe.s"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                    "--cuda-device-only", "-S", src, "-o", str(asm)], check=True, capture_output=True)
+    out = subprocess.run([sys.executable, os.path.join(hs.PKG_DIR, "tools", "vmcnt_check.py"), str(asm)],
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    lines = [l for l in out.stdout.splitlines() if "violations" in l]
+    assert len(lines) >= 20 and all(l.endswith(": 0 violations") for l in lines), out.stdout
+    assert any("k_gather" in l for l in lines)
