@@ -82,6 +82,7 @@ struct hipspmv_handle {
     uint64_t n_cont = 0;
     int split = 1;
     bool row_runs = false;  // place_segments_banked: runs inside 16-lane rows (xlane 5 applies)
+    bool vc4 = false;       // [2] built for k_vcache's four-part geometry (HIPSPMV_SPLIT4_VCACHE=1), not k_vquad
   } vc[4];  // [0] ordered (kVcOrdered), [1] split (kVcSplit); experimental: [2] split4; [3] wgather windows
   // The ordered vcache layout is only ever selected by name: its eligibility
   // and geometry are known at create, its entries built on first selection.
@@ -234,8 +235,8 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
     // run and its column order, so the sums are bit-identical);
     // HIPSPMV_VCACHE_BANK=0 keeps the (row, column) order (A/B probe)
     const char* bank = std::getenv("HIPSPMV_VCACHE_BANK");
-    if ((k == 0 || k == 1) && !(bank && std::strcmp(bank, "0") == 0))
-      place_segments_banked(L, k == 1 ? kVcSplitCT : kVcOrderedCT);
+    if ((k == 0 || k == 1 || (k == 2 && g.split == 4 && g.colbits == 16)) && !(bank && std::strcmp(bank, "0") == 0))
+      place_segments_banked(L, k == 1 ? kVcSplitCT : k == 0 ? kVcOrderedCT : kVcSplit4CT);
   }
   v.split = g.split;
   v.rows_per_block = L.rows_per_block;
@@ -692,7 +693,13 @@ static int ensure_layout(hipspmv_t* h, int kernel) {
       else if (kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
         // every segment inside the kernel's register window, runs placeable
         // (build_vcache_lanes); otherwise not eligible from now on
-        st = h->vq_eligible ? upload_vc(h, 2, a, kVcQuad, kVqLanes) : HIPSPMV_ERR_UNSUPPORTED;
+        // HIPSPMV_SPLIT4_VCACHE=1 (probe): the k_vcache four-part geometry with banked segments instead
+        const char* v4 = std::getenv("HIPSPMV_SPLIT4_VCACHE");
+        const bool vc4 = v4 && std::strcmp(v4, "1") == 0;
+        st = !h->vq_eligible ? HIPSPMV_ERR_UNSUPPORTED
+             : vc4 ? (vcache_eligible(a, kVcSplit4) ? upload_vc(h, 2, a, kVcSplit4) : HIPSPMV_ERR_UNSUPPORTED)
+                   : upload_vc(h, 2, a, kVcQuad, kVqLanes);
+        if (!st) h->vc[2].vc4 = vc4;
         if (st == HIPSPMV_ERR_UNSUPPORTED) h->vq_eligible = false;
       } else st = build_vc_layout(h, kernel == HIPSPMV_KERNEL_WGATHER ? 3 : 0, a);
     }
@@ -759,13 +766,13 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
       kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
     const int k = kernel == HIPSPMV_KERNEL_VCACHE ? 0 : kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1 : 2;
     const auto& v = h->vc[k];
-    const VcGeom geoms[3] = {kVcOrdered, kVcSplit, kVcQuad};
+    const VcGeom geoms[3] = {kVcOrdered, kVcSplit, v.vc4 ? kVcSplit4 : kVcQuad};
     VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    v.d_partial,
                  v.d_tickets, h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
                  v.npad,      h->nnz - 1, v.split,   beta, h->vcache_dma, (uint32_t)geoms[k].panel,
                  h->vcache_xlane, v.max_seg, h->vcache_map};
     a.nt_from = h->vcache_nt >= 0 ? (uint32_t)std::min<int64_t>(h->vcache_nt, UINT32_MAX)
-                : k < 2 ? resident_blocks(v.nblocks, h->nnz) : ~0u;
+                : k < 2 || v.vc4 ? resident_blocks(v.nblocks, h->nnz) : ~0u;
     a.row_runs = v.row_runs;
     // an unprofiled launch leaves an unread profile of an earlier launch readable
     // (it writes no stamps); d_prof is allocated when the option is set, never
@@ -787,6 +794,8 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
       h->prof_valid = false;
       h->prof_stream = s;
       h->prof_layout = k;
+    } else if (k == 2 && v.vc4) {  // k_vcache's four-part geometry (probe)
+      e = launch_vcache(h->dtype, a, s);
     } else if (k == 2) {
       a.status = h->d_status;
       a.variant = h->vquad_variant;

@@ -79,7 +79,9 @@ constexpr uint32_t kVqLanes = 13 * 64;
 // k_vcache's split geometry: compute lanes (16 - 3 loader waves) * 64 (VcCfg<3>)
 constexpr uint32_t kVcSplitCT = 13 * 64;
 // ... and its ordered geometry's: (16 - 8 loader waves) * 64 (VcCfg<1>)
-constexpr uint32_t kVcOrderedCT = 8 * 64;  // k_vquad's compute lanes (13 of 16 waves): the layout's CT
+constexpr uint32_t kVcOrderedCT = 8 * 64;
+// ... and its four-part geometry's: (16 - 2 loader waves) * 64 (VcCfg<4>)
+constexpr uint32_t kVcSplit4CT = 14 * 64;  // k_vquad's compute lanes (13 of 16 waves): the layout's CT
 
 // ---- wcsr: csr_vector over the column-windowed segment matrix
 // Every row is cut at column windows of 2^kWcLog2Window columns (8 MiB of

@@ -747,9 +747,14 @@ bool build_vcache_lanes(const HostCSR& a, const VcGeom& g, uint32_t CT, VcacheLa
             if (runs[k].second >= 2) multi.push_back(k);
           std::stable_sort(multi.begin(), multi.end(),
                            [&](size_t v, size_t w) { return runs[v].second > runs[w].second; });
+          // a cursor at the first free position: every placement fills positions, so it
+          // never moves back, and a run's search starts there (the scan from 0
+          // made segments with many short runs quadratic)
+          uint32_t cursor = 0;
           for (size_t k : multi) {
             auto& r = runs[k];
-            uint32_t p = 0;
+            while (cursor < n && used[cursor]) ++cursor;
+            uint32_t p = cursor;
             while (p < n && !fits(p, r.second)) ++p;
             if (p >= n) {
               ok = false;

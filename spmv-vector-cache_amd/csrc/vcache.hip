@@ -683,7 +683,7 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   // -1 (default): 5 for the split geometry where the layout allows it, else 3
   // (C3: 131.7 us against 135.7 with the run continuation re-read from
   // memory), 0 for the others.
-  int xl = a.xlane < 0 ? (a.split == 3 ? (a.row_runs ? 5 : 3) : 0) : a.xlane;
+  int xl = a.xlane < 0 ? (a.split >= 3 ? (a.row_runs ? 5 : 3) : 0) : a.xlane;
   if (xl == 5 && !a.row_runs) xl = 3;
   const int cx = xl && a.max_seg <= window(a.split) ? xl : 0;
   // dma -1 (default): register-staged x loaders; the split geometry's two
@@ -696,7 +696,11 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
     launch_one<T, 3, 1, 5, 2>(a, s);
   else if (a.split == 3)
     dispatch<T, 3>(a, s, ld, cx);
-  else  // four parts: k_vquad (csrc/vquad.hip) runs that layout
+  else if (cx == 5 && a.map == 1)  // four parts (probe, HIPSPMV_SPLIT4_VCACHE=1): LDS-DMA loaders, xlane 5
+    launch_one<T, 4, 1, 5, 1>(a, s);
+  else if (cx == 5)
+    launch_one<T, 4, 1, 5, 0>(a, s);
+  else  // four parts otherwise: k_vquad (csrc/vquad.hip) runs that layout
     return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -25,6 +25,11 @@ sys.path.insert(0, os.path.dirname(HERE))
 import hipspmv as hs  # noqa: E402
 
 SETS = {
+    # round 5: k_vcache's four-part geometry (banked, LDS-DMA loaders, xlane 5, resident entries) against the
+    # product; "v4:" a handle created with HIPSPMV_SPLIT4_VCACHE=1
+    "split4": [("split (product)", "vcache_split", {}), ("vcache 4 parts", "v4:vcache_split4", {}),
+               ("vcache 4 parts map 1", "v4:vcache_split4", {"vcache_map": 1}),
+               ("vquad v0", "vcache_split4", {"vquad_variant": 0})],
     "resid2": [("split resident 1/2", "vcache_split", {"vcache_nt": 42}),
                ("split resident 7/16", "vcache_split", {"vcache_nt": 37}),
                ("split resident 17/32", "vcache_split", {"vcache_nt": 45}),
@@ -81,11 +86,16 @@ def main():
     rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32, 1, 2)
     x = hs.gen_vector(n, 3)
     h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
-    hb = None
+    hb = h4 = None
     if any(k.startswith("bank0:") for _, k, _ in SETS[a.set]):
         os.environ["HIPSPMV_VCACHE_BANK"] = "0"
         hb = hs.Handle.from_csr(rowptr, colind, vals, n, n)
         del os.environ["HIPSPMV_VCACHE_BANK"]
+    if any(k.startswith("v4:") for _, k, _ in SETS[a.set]):
+        os.environ["HIPSPMV_SPLIT4_VCACHE"] = "1"
+        h4 = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+        h4.set_kernel("vcache_split4")  # the layout is built on first selection, while the variable is set
+        del os.environ["HIPSPMV_SPLIT4_VCACHE"]
     alg = h.stat("alg_bytes")
     xd = torch.from_numpy(x).cuda()
     yd = torch.empty(n, dtype=torch.float64, device="cuda")
@@ -105,7 +115,7 @@ def main():
     cur = [h]
 
     def select(kernel, opts):
-        cur[0] = hb if kernel.startswith("bank0:") else h
+        cur[0] = hb if kernel.startswith("bank0:") else h4 if kernel.startswith("v4:") else h
         cur[0].set_kernel(kernel.split(":")[-1])
         for k, v in opts.items():
             cur[0].set_option(k, v)

@@ -500,6 +500,7 @@ int main(int argc, char** argv) {
                       {kVcSplit.rows, kVcSplit.panel, 6, 4, 3, 3, 0, 16, 2},
                       {kVcSplit.rows, kVcSplit.panel, 3, 4, 2, 3, 1, 16, 1},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0, 16, 2},
+                      {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 1, 16, 2},
                       {kWgWindow.rows, kWgWindow.panel, 0, 4, 4, 1, 2, kWgWindow.colbits, 2}};
   int failures = check_maps<1>() + check_maps<2>() + check_maps<3>() + check_maps<4>();
   {  // the round-1 incident geometry: the ordered (split 1) kernel launched with the split layout's
@@ -662,7 +663,7 @@ int main(int argc, char** argv) {
       // and the same result bits as the (row, column) layout
       VcacheLayout B;
       // the product layouts: split (xlane 3, modelled as CX 2) and the ordered geometry
-      const bool banked = (c.SPLIT == 3 && c.LD == 1 && c.CX >= 2) || (c.SPLIT == 1 && c.LD != 2);
+      const bool banked = (c.SPLIT >= 3 && c.LD == 1 && c.CX >= 2) || (c.SPLIT == 1 && c.LD != 2);
       if (banked) {
         B = L;
         const uint32_t CT = (uint32_t)(16 - c.WL) * 64;
