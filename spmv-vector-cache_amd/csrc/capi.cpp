@@ -115,6 +115,7 @@ struct hipspmv_handle {
   int vcache_dma = -1;   // option "vcache_dma": LDS-DMA x loader (-1 default: on for the split geometry)
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
   int vcache_map = 0;    // option "vcache_map": XCD-aware part placement (unused since k_vquad; kept as an option)
+  int vcache_spf = 0;    // option "vcache_spf": split kernel with the loaders' scalar L2 prefetch (1-3, diagnostic)
   int vquad_variant = 0;  // option "vquad_variant": k_vquad configuration (csrc/vquad.hip launch_vquad_t)
   // bit 0: reserved for a combine hand-off that timed out into unpublished
   // partials (csrc/combine.h has no such path since round 4; the word stays 0)
@@ -774,6 +775,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     a.nt_from = h->vcache_nt >= 0 ? (uint32_t)std::min<int64_t>(h->vcache_nt, UINT32_MAX)
                 : k < 2 || v.vc4 ? resident_blocks(v.nblocks, h->nnz) : ~0u;
     a.row_runs = v.row_runs;
+    a.spf = h->vcache_spf;
     // an unprofiled launch leaves an unread profile of an earlier launch readable
     // (it writes no stamps); d_prof is allocated when the option is set, never
     // here, so a profiled launch is legal only outside a capture (checked below)
@@ -976,6 +978,9 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "vcache_map") {  // 1: split4 XCD pairs; 2: split, one column part per XCD where it can
     if (value < 0 || value > 2) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_map = (int)value;
+  } else if (k == "vcache_spf") {  // 1: distance 1, all lines; 2: distance 2; 3: distance 1, 16 lines per wave
+    if (value < 0 || value > 3) return HIPSPMV_ERR_INVALID_ARG;
+    h->vcache_spf = (int)value;
   } else if (k == "vquad_variant") {  // k_vquad configuration (csrc/vquad.hip)
     if (value < 0 || value > 26) return HIPSPMV_ERR_INVALID_ARG;
     // 6-16 are timing ablations that give wrong y (or race): experimental builds only

@@ -29,6 +29,8 @@ struct VcacheArgs {
   int variant = 0;             // k_vquad: configuration (loader waves, x / entry ring depths)
   bool row_runs = false;       // every run of the layout inside one 16-lane row (place_segments_banked):
                                // the split kernel's first continuation step by DPP (xlane 5)
+  int spf = 0;                 // k_vcache split: loaders' scalar L2 prefetch of the entries (option
+                               // "vcache_spf" 1-3, diagnostic)
 };
 
 struct CsrArgs {
