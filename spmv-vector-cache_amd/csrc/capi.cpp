@@ -109,13 +109,14 @@ struct hipspmv_handle {
     bool built = false;
     uint32_t *d_rowptr = nullptr, *d_colind = nullptr, *d_groups = nullptr, *d_rowseg = nullptr,
              *d_segidx = nullptr, *d_rgroups = nullptr, *d_chunks = nullptr;
+    // the compact reduce (k_wreduce_c): rows with segments, their offsets, groups, the bitmap
+    uint32_t *d_rrow = nullptr, *d_rsegc = nullptr, *d_cgroups = nullptr, *d_nebits = nullptr;
     uint64_t *d_vals = nullptr, *d_ypart = nullptr;
-    uint32_t nseg = 0, ngroups = 0, rgroups = 0, max_seg = 0, log2w = 0, nchunks = 0;
+    uint32_t nseg = 0, ngroups = 0, rgroups = 0, ncgroups = 0, nrows_ne = 0, max_seg = 0, log2w = 0, nchunks = 0;
   } wc;
   int vcache_dma = -1;   // option "vcache_dma": LDS-DMA x loader (-1 default: on for the split geometry)
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
   int vcache_map = 0;    // option "vcache_map": XCD-aware part placement (unused since k_vquad; kept as an option)
-  int vcache_spf = 0;    // option "vcache_spf": split kernel with the loaders' scalar L2 prefetch (1-3, diagnostic)
   int vquad_variant = 0;  // option "vquad_variant": k_vquad configuration (csrc/vquad.hip launch_vquad_t)
   // bit 0: reserved for a combine hand-off that timed out into unpublished
   // partials (csrc/combine.h has no such path since round 4; the word stays 0)
@@ -141,6 +142,8 @@ struct hipspmv_handle {
   // option "wcsr_res": wcsr segment-pass groups g < wcsr_res load their entries
   // with the default policy (Infinity-Cache resident); 0 default: all non-temporal
   int64_t wcsr_res = 0;
+  int wcsr_reduce = 0;    // option "wcsr_reduce": 0 the compact reduce over rows with segments, 1 every row
+  int wcsr_preload = 0;   // option "wcsr_preload": 1 the segment pass loads a group's terms before its scans
   // option "sell_nt": SELL slices s >= sell_nt load their entries
   // non-temporally (-1 default: the second half of the slices)
   int64_t sell_nt = -1;
@@ -202,7 +205,8 @@ static void release(hipspmv_t* h) {
   }
   {
     auto& w = h->wc;
-    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart};
+    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart,
+                  w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits};
     for (void* p : wp)
       if (p) (void)hipFree(p);
   }
@@ -290,7 +294,8 @@ static void drop_partial_layouts(hipspmv_t* h) {
   }
   if (!h->wc.built) {
     auto& w = h->wc;
-    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart};
+    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart,
+                  w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits};
     for (void* p : wp)
       if (p) (void)hipFree(p);
     w = hipspmv_handle::Wc{};
@@ -419,8 +424,8 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   }
   const uint64_t bytes0 = h->device_bytes;
   auto fail = [&](int st) {
-    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx,
-                  w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart};
+    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks,
+                  w.d_vals, w.d_ypart, w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits};
     for (void* p : wp)
       if (p) (void)hipFree(p);
     w = hipspmv_handle::Wc{};
@@ -442,6 +447,23 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
     build_row_groups(L.rowseg.data(), a.rows, rg);
     if ((st = dev_upload(&w.d_rgroups, rg.data(), rg.size(), h->device_bytes))) return fail(st);
     w.rgroups = (uint32_t)rg.size() - 1;
+  }
+  {  // the compact reduce: the rows with segments, in order, and a bitmap of them for the fill
+    std::vector<uint32_t> rrow, rsegc, cg, bits(((size_t)a.rows + 31) / 32, 0u);
+    for (uint32_t r = 0; r < a.rows; ++r)
+      if (L.rowseg[r + 1] > L.rowseg[r]) {
+        rrow.push_back(r);
+        rsegc.push_back(L.rowseg[r]);
+        bits[r >> 5] |= 1u << (r & 31);
+      }
+    rsegc.push_back(L.rowseg[a.rows]);
+    build_row_groups(rsegc.data(), (uint32_t)rrow.size(), cg);
+    if (!rrow.empty() && (st = dev_upload(&w.d_rrow, rrow.data(), rrow.size(), h->device_bytes))) return fail(st);
+    if ((st = dev_upload(&w.d_rsegc, rsegc.data(), rsegc.size(), h->device_bytes))) return fail(st);
+    if ((st = dev_upload(&w.d_cgroups, cg.data(), cg.size(), h->device_bytes))) return fail(st);
+    if (!bits.empty() && (st = dev_upload(&w.d_nebits, bits.data(), bits.size(), h->device_bytes))) return fail(st);
+    w.ncgroups = (uint32_t)cg.size() - 1;
+    w.nrows_ne = (uint32_t)rrow.size();
   }
   {
     const uint64_t b = 8ull * std::max<uint32_t>(L.nseg, 1);
@@ -775,7 +797,6 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     a.nt_from = h->vcache_nt >= 0 ? (uint32_t)std::min<int64_t>(h->vcache_nt, UINT32_MAX)
                 : k < 2 || v.vc4 ? resident_blocks(v.nblocks, h->nnz) : ~0u;
     a.row_runs = v.row_runs;
-    a.spf = h->vcache_spf;
     // an unprofiled launch leaves an unread profile of an earlier launch readable
     // (it writes no stamps); d_prof is allocated when the option is set, never
     // here, so a profiled launch is legal only outside a capture (checked below)
@@ -823,6 +844,14 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     a.nchunks = w.nchunks;
     a.res_groups = (uint32_t)std::min<int64_t>(h->wcsr_res, w.ngroups);
     a.cols = h->cols;
+    a.preload = h->wcsr_preload;
+    if (h->wcsr_reduce == 0 && w.d_rrow) {  // the compact reduce (default; option wcsr_reduce 1: all rows)
+      a.rrow = w.d_rrow;
+      a.rsegc = w.d_rsegc;
+      a.nebits = w.d_nebits;
+      a.cgroups = w.d_cgroups;
+      a.ncgroups = w.ncgroups;
+    }
     e = launch_wcsr(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
@@ -978,9 +1007,6 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "vcache_map") {  // 1: split4 XCD pairs; 2: split, one column part per XCD where it can
     if (value < 0 || value > 2) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_map = (int)value;
-  } else if (k == "vcache_spf") {  // 1: distance 1, all lines; 2: distance 2; 3: distance 1, 16 lines per wave
-    if (value < 0 || value > 3) return HIPSPMV_ERR_INVALID_ARG;
-    h->vcache_spf = (int)value;
   } else if (k == "vquad_variant") {  // k_vquad configuration (csrc/vquad.hip)
     if (value < 0 || value > 26) return HIPSPMV_ERR_INVALID_ARG;
     // 6-16 are timing ablations that give wrong y (or race): experimental builds only
@@ -1004,6 +1030,12 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "sell_nt") {  // first SELL slice whose entries load non-temporally (-1: half)
     if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->sell_nt = value;
+  } else if (k == "wcsr_preload") {
+    if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
+    h->wcsr_preload = (int)value;
+  } else if (k == "wcsr_reduce") {  // 0: compact reduce over the rows with segments (default); 1: every row
+    if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
+    h->wcsr_reduce = (int)value;
   } else if (k == "wcsr_res") {  // wcsr segment-pass groups below it keep their entries resident
     if (value < 0 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->wcsr_res = value;
@@ -1153,6 +1185,8 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "wcsr_window_log2") *out = h->wc.built ? h->wc.log2w : kWcLog2Window;
   else if (k == "wcsr_chunks") *out = h->wc.nchunks;
   else if (k == "wcsr_groups") *out = h->wc.ngroups;
+  else if (k == "wcsr_reduce_groups") *out = h->wc.built ? (h->wcsr_reduce == 0 ? h->wc.ncgroups : h->wc.rgroups) : 0;
+  else if (k == "wcsr_rows_with_segments") *out = h->wc.nrows_ne;
   else if (k == "sell_slices") *out = h->sell.nslices;
   else if (k == "sell_hubs") *out = h->sell.nhubs;
   else if (k == "sell_iso_hubs") *out = h->sell.niso;

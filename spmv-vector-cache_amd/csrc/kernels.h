@@ -29,8 +29,6 @@ struct VcacheArgs {
   int variant = 0;             // k_vquad: configuration (loader waves, x / entry ring depths)
   bool row_runs = false;       // every run of the layout inside one 16-lane row (place_segments_banked):
                                // the split kernel's first continuation step by DPP (xlane 5)
-  int spf = 0;                 // k_vcache split: loaders' scalar L2 prefetch of the entries (option
-                               // "vcache_spf" 1-3, diagnostic)
 };
 
 struct CsrArgs {
@@ -66,6 +64,15 @@ struct WcsrArgs {  // csr_vector over the column-windowed segment matrix, then k
                             // (Infinity-Cache resident across launches; k_wpass), the rest non-temporal
   uint32_t nchunks = 0;
   uint32_t cols = 0;
+  int preload = 0;  // segment pass: a group's terms loaded before its scans (k_wpass_pre)
+  // the compact reduce (k_wreduce_c, used when rrow is set): groups over the rows that have segments
+  // only -- rrow[i] is the i-th such row, rsegc[i] = rowseg[rrow[i]] (nrows_ne + 1 entries) -- and
+  // the rows without any (bit r of nebits clear) written by the same launch's fill blocks
+  const uint32_t* rrow = nullptr;
+  const uint32_t* rsegc = nullptr;
+  const uint32_t* nebits = nullptr;
+  const uint32_t* cgroups = nullptr;
+  uint32_t ncgroups = 0;
 };
 
 struct SellArgs {

@@ -174,30 +174,6 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
             (__attribute__((address_space(3))) void*)(slot + 2 * c0), 16, 0, 0);
     }
   };
-  // AB bits 16-19 (d) and 20-27 (cap), LD == 1 (diagnostic, tools/ab_sweep.py set "spf"): during
-  // step s the loader waves touch the 128-B lines of step s + DE + d's entries with scalar loads --
-  // the scalar cache's own path to L2, outside the CU's vector L1 request slots -- so the compute
-  // waves' vector loads of those lines one or more steps later hit L2 instead of HBM.  At most cap
-  // lines per wave and step; the loaded words are never read.
-  constexpr uint32_t SPF_D = (AB >> 16) & 0xF, SPF_CAP = (AB >> 20) & 0xFF;
-  auto spf_range = [&](uint64_t lo, uint64_t hi, uint32_t& budget) {
-    for (uint64_t p = (lo & ~127ull) + 128ull * wl; p < hi && budget; p += 128ull * WL, --budget) {
-      const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
-      uint32_t dummy;
-      asm volatile("s_load_dword %0, %1, 0x0" : "=s"(dummy) : "s"(q));
-    }
-  };
-  auto spf = [&](uint32_t q) {
-    if constexpr (SPF_D != 0) {
-      if (q >= npu) return;
-      const uint32_t beg = __builtin_amdgcn_readfirstlane(segl[q]);
-      const uint32_t end = __builtin_amdgcn_readfirstlane(segl[q + 1]);
-      if (end <= beg) return;
-      uint32_t budget = SPF_CAP;
-      spf_range((uint64_t)(evals + beg), (uint64_t)(evals + end), budget);
-      spf_range((uint64_t)(ecode + beg), (uint64_t)(ecode + end), budget);
-    }
-  };
   auto patch_x = [&](uint32_t s) {  // odd cols: the last element, after this wave's DMA landed
     if ((cols & 1) && p0 + s == npanels - 1) {
       const uint32_t sl = cols - 1 - (p0 + s) * VP, c = sl >> 1;
@@ -480,19 +456,14 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       stamp(1, now());
       pf_mark = __builtin_amdgcn_s_memtime();
     }
-    if constexpr (SPF_D != 0) {
-      for (uint32_t q = DE; q < DE + SPF_D; ++q) spf(q);
-    }
     for (uint32_t s = 0; s < nsteps; ++s) {
       if (s + 1 < npu) dma_x(s + 1);
-      spf(s + DE + SPF_D);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t t_ready = (AB & 8192) ? tr_now() : 0;
       if (s + 1 < npu) patch_x(s + 1);
       pbarrier();
       tr_rel(s, t_ready, t_ready);
     }
-    if constexpr (SPF_D != 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   } else if (loader && LD == 2) {
     // same ring, asm loads: storing x(s+1) waits for it with x(s+2)'s NJ
     // loads (issued one step later) still in flight
@@ -652,9 +623,9 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   if (AB & 128) stamp(3, now());
 }
 
-template <typename T, int SPLIT, int LD, int CX = 0, int MAP = 0, int AB = 0>
+template <typename T, int SPLIT, int LD, int CX = 0, int MAP = 0>
 static void launch_one(const VcacheArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_vcache<T, SPLIT, VcCfg<SPLIT>::WL, VcCfg<SPLIT>::DE, VcCfg<SPLIT>::EPT, AB, MAP, false, LD, CX>),
+  hipLaunchKernelGGL((k_vcache<T, SPLIT, VcCfg<SPLIT>::WL, VcCfg<SPLIT>::DE, VcCfg<SPLIT>::EPT, 0, MAP, false, LD, CX>),
                      dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s, a.seg, a.code, (const T*)a.vals,
                      (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets, a.rows, a.cols,
                      a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta, a.nt_from);
@@ -719,18 +690,6 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   // loader waves always stage by LDS-DMA (dispatch)
   const int dma = a.dma < 0 ? 0 : a.dma;
   const int ld = dma ? 1 : cx == 2 ? 2 : 0;
-  // option "vcache_spf" (diagnostic): the split kernel with the loaders' scalar L2 prefetch of the
-  // entries (AB bits 16-27: distance d, cap lines per wave and step)
-  constexpr int SPF1 = (1 << 16) | (64 << 20), SPF2 = (2 << 16) | (64 << 20), SPF3 = (1 << 16) | (16 << 20);
-  if (a.split == 3 && cx == 5 && a.spf) {
-    if (a.spf == 1)
-      launch_one<T, 3, 1, 5, 0, SPF1>(a, s);
-    else if (a.spf == 2)
-      launch_one<T, 3, 1, 5, 0, SPF2>(a, s);
-    else
-      launch_one<T, 3, 1, 5, 0, SPF3>(a, s);
-    return hipGetLastError();
-  }
   if (a.split == 1)
     dispatch<T, 1>(a, s, ld, cx);
   else if (a.split == 3 && a.map == 2 && cx == 5)  // (option "vcache_map" 2)

@@ -213,8 +213,34 @@ def test_wcsr_wide_windows(gpu, dtype):
             np.add.at(absprod, row_of, np.abs(vals * x[colind]))
             bound = _fast_bound(lens, absprod, y0 if beta else np.zeros(rows))
             assert np.all(np.abs(ys[0] - y_ref) <= bound)
+    # the compact reduce (default) runs groups over the rows with segments only; the fill blocks give
+    # the empty rows y_in (beta 1) or +0.0 (beta 0) exactly
+    empty = lens == 0
+    assert empty.sum() > 0 and h.stat("wcsr_rows_with_segments") == int((~empty).sum())
+    ncg = h.stat("wcsr_reduce_groups")
+    h.set_option("wcsr_reduce", 1)
+    assert ncg <= h.stat("wcsr_reduce_groups")
+    h.set_option("wcsr_reduce", 0)
+    y1 = h.exec(x, y0.copy(), beta=1, mode=hs.MODE_FAST)
+    assert y1[empty].tobytes() == y0[empty].tobytes()
+    y_zero = h.exec(x, y0.copy(), beta=0, mode=hs.MODE_FAST)
+    assert np.all(y_zero[empty] == 0) and not np.signbit(y_zero[empty].astype(np.float64)).any()
+    # the all-rows reduce (option wcsr_reduce 1): also deterministic and within the bound
+    h.set_option("wcsr_reduce", 1)
+    for beta in (0, 1):
+        y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else np.zeros(rows, dtype)), rows=rows)
+        ys = [h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST) for _ in range(2)]
+        assert ys[0].tobytes() == ys[1].tobytes()
+        if dtype == np.uint64:
+            assert ys[0].tobytes() == y_ref.tobytes()
+        else:
+            absprod = np.zeros(rows)
+            np.add.at(absprod, row_of, np.abs(vals * x[colind]))
+            assert np.all(np.abs(ys[0] - y_ref) <= _fast_bound(lens, absprod, y0 if beta else np.zeros(rows)))
+    h.set_option("wcsr_reduce", 0)
     # the segment pass with half its groups' entries resident (option wcsr_res, k_wpass): the same bits
     y_nt = h.exec(x, y0.copy(), beta=1, mode=hs.MODE_FAST)
+    assert y_nt.tobytes() == y1.tobytes()
     h.set_option("wcsr_res", h.stat("wcsr_groups") // 2)
     assert h.exec(x, y0.copy(), beta=1, mode=hs.MODE_FAST).tobytes() == y_nt.tobytes()
     h.set_option("wcsr_res", 0)
