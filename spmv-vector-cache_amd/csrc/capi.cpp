@@ -143,7 +143,6 @@ struct hipspmv_handle {
   // with the default policy (Infinity-Cache resident); 0 default: all non-temporal
   int64_t wcsr_res = 0;
   int wcsr_reduce = 0;    // option "wcsr_reduce": 0 the compact reduce over rows with segments, 1 every row
-  int wcsr_preload = 0;   // option "wcsr_preload": 1 the segment pass loads a group's terms before its scans
   // option "sell_nt": SELL slices s >= sell_nt load their entries
   // non-temporally (-1 default: the second half of the slices)
   int64_t sell_nt = -1;
@@ -844,7 +843,6 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     a.nchunks = w.nchunks;
     a.res_groups = (uint32_t)std::min<int64_t>(h->wcsr_res, w.ngroups);
     a.cols = h->cols;
-    a.preload = h->wcsr_preload;
     if (h->wcsr_reduce == 0 && w.d_rrow) {  // the compact reduce (default; option wcsr_reduce 1: all rows)
       a.rrow = w.d_rrow;
       a.rsegc = w.d_rsegc;
@@ -1030,9 +1028,6 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "sell_nt") {  // first SELL slice whose entries load non-temporally (-1: half)
     if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->sell_nt = value;
-  } else if (k == "wcsr_preload") {
-    if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
-    h->wcsr_preload = (int)value;
   } else if (k == "wcsr_reduce") {  // 0: compact reduce over the rows with segments (default); 1: every row
     if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
     h->wcsr_reduce = (int)value;

@@ -64,7 +64,6 @@ struct WcsrArgs {  // csr_vector over the column-windowed segment matrix, then k
                             // (Infinity-Cache resident across launches; k_wpass), the rest non-temporal
   uint32_t nchunks = 0;
   uint32_t cols = 0;
-  int preload = 0;  // segment pass: a group's terms loaded before its scans (k_wpass_pre)
   // the compact reduce (k_wreduce_c, used when rrow is set): groups over the rows that have segments
   // only -- rrow[i] is the i-th such row, rsegc[i] = rowseg[rrow[i]] (nrows_ne + 1 entries) -- and
   // the rows without any (bit r of nebits clear) written by the same launch's fill blocks

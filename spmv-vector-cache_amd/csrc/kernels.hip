@@ -89,7 +89,7 @@ __device__ __forceinline__ void csr_vector_rows(const uint32_t* __restrict__ row
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   const uint32_t base = rowptr[r0], n = rowptr[r1] - base;
-  constexpr bool NTL = KIND == 1 || KIND == 3 || KIND == 4;  // entries non-temporal
+  constexpr bool NTL = KIND == 1 || KIND == 3;  // entries non-temporal
   auto ci = [&](uint32_t e) { return NTL ? __builtin_nontemporal_load(colind + e) : colind[e]; };
   // the e-th term of the group's sums: a rounded product, or a partial
   auto term = [&](uint32_t e) -> T {
@@ -128,7 +128,7 @@ __device__ __forceinline__ void csr_vector_rows(const uint32_t* __restrict__ row
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
   T carry = T(0);
-  if constexpr (KIND == 2 || KIND == 3 || KIND == 4) {
+  if constexpr (KIND == 2 || KIND == 3) {
     // the wcsr reduce and k_wseg: every term of the group (<= 256) is loaded
     // before the scans, so a wave keeps four loads in flight instead of one
     // per round trip (k_wseg on C5 shard 0: 359.7 -> 322.4 us; the same in
@@ -260,22 +260,6 @@ __global__ __launch_bounds__(256) void k_wpass(const uint32_t* __restrict__ rowp
     csr_vector_rows<T, 0>(rowptr, colind, vals, xv, out, groups[g], groups[g + 1], heads[w]);
 }
 
-// k_wpass_pre (wcsr segment pass, option wcsr_preload): KIND 4 -- the
-// segment pass's non-temporal entries with every term of a group loaded before
-// its scans (the reduce's form), for short-segment shards
-template <typename T>
-__global__ __launch_bounds__(256) void k_wpass_pre(const uint32_t* __restrict__ rowptr,
-                                                    const uint32_t* __restrict__ colind, const T* __restrict__ vals,
-                                                    const T* __restrict__ x, T* __restrict__ ypart,
-                                                    const uint32_t* __restrict__ groups, uint32_t ngroups) {
-  __shared__ uint32_t heads[4][kCvGroupNnz / 32];
-  const int w = threadIdx.x >> 6;
-  const uint32_t g = blockIdx.x * 4 + w;
-  if (g >= ngroups) return;  // wave-uniform
-  csr_vector_rows<T, 4>(rowptr, colind, vals, [&](uint32_t c) { return x[c]; }, RowOut<T>{(const T*)nullptr, ypart, 0},
-                        groups[g], groups[g + 1], heads[w]);
-}
-
 // k_wreduce (wcsr): y[r] = (y_in[r] +) the sum of row r's segment partials
 // ypart[segidx[k]], k in [rowseg[r], rowseg[r+1]) (window order), over the
 // reduce's own balanced row groups -- a fixed order, so wcsr is
@@ -293,7 +277,7 @@ __global__ __launch_bounds__(256) void k_wreduce(const uint32_t* __restrict__ ro
 // segment offsets), so a group no longer spends lanes and a round trip per
 // row on rows without entries -- C5's short-row shards are 50-70 % empty rows;
 // blocks past red_blocks write the rows without segments (y_in or +0.0), one
-// row per lane, from the bitmap nebits.  The order of every row's sum is the
+// row per lane and grid-stride step, from the bitmap nebits.  The order of every row's sum is the
 // group scan's, as in k_wreduce (deterministic; FAST bound).
 template <typename T>
 struct RowOutMapped {
@@ -322,8 +306,9 @@ __global__ __launch_bounds__(256) void k_wreduce_c(const uint32_t* __restrict__ 
                           RowOutMapped<T>{rrow, y_in, y_out, beta}, groups[g], groups[g + 1], heads[w]);
     return;
   }
-  const uint32_t r = (blockIdx.x - red_blocks) * 256 + threadIdx.x;
-  if (r < rows && !((nebits[r >> 5] >> (r & 31)) & 1u)) y_out[r] = beta ? y_in[r] : T(0);
+  const uint32_t stride = (gridDim.x - red_blocks) * 256;
+  for (uint32_t r = (blockIdx.x - red_blocks) * 256 + threadIdx.x; r < rows; r += stride)
+    if (!((nebits[r >> 5] >> (r & 31)) & 1u)) y_out[r] = beta ? y_in[r] : T(0);
 }
 
 // ---------------------------------------------------------------------------
@@ -349,9 +334,6 @@ hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
   if (a.nchunks)
     hipLaunchKernelGGL(k_wseg<T>, dim3(a.nchunks), dim3(1024), 0, s, a.chunks, a.groups, a.seg_rowptr, a.seg_colind,
                        (const T*)a.seg_vals, (const T*)a.x, a.cols, (T*)a.ypart);
-  else if (a.ngroups && a.preload)
-    hipLaunchKernelGGL(k_wpass_pre<T>, dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,
-                       (const T*)a.seg_vals, (const T*)a.x, (T*)a.ypart, a.groups, a.ngroups);
   else if (a.ngroups && a.res_groups)
     hipLaunchKernelGGL(k_wpass<T>, dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,
                        (const T*)a.seg_vals, (const T*)a.x, (T*)a.ypart, a.groups, a.ngroups, a.res_groups);
@@ -360,7 +342,8 @@ hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
                        a.seg_colind, (const T*)a.seg_vals, (const T*)a.x, (const T*)nullptr, (T*)a.ypart,
                        a.groups, a.ngroups, 0);
   if (a.rrow) {
-    const uint32_t red = (a.ncgroups + 3) / 4, fill = (a.rows + 255) / 256;
+    // the fill: at most 1024 blocks, grid-stride (one block per 256 rows measured as a dispatch tail)
+    const uint32_t red = (a.ncgroups + 3) / 4, fill = std::min((a.rows + 255) / 256, 1024u);
     hipLaunchKernelGGL(k_wreduce_c<T>, dim3(red + fill), dim3(256), 0, s, a.rsegc, a.segidx, (const T*)a.ypart,
                        a.rrow, a.nebits, (const T*)a.y_in, (T*)a.y_out, a.cgroups, a.ncgroups, red, a.rows, a.beta);
   } else {

@@ -19,7 +19,6 @@ import hipspmv as hs  # noqa: E402
 
 # settings: (label, {option: value or ("groups", fraction)})
 SETS = {
-    "preload": [("product", {}), ("preload", {"wcsr_preload": 1})],
     "reduce": [("compact reduce", {}), ("all-rows reduce", {"wcsr_reduce": 1})],
     "res": [("all nt (product)", {}), ("resident 1/8", {"wcsr_res": ("groups", 0.125)}),
             ("resident 1/4", {"wcsr_res": ("groups", 0.25)}), ("resident 3/8", {"wcsr_res": ("groups", 0.375)}),
