@@ -124,7 +124,11 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
  * about 192 MiB of entries resident -- C3: half the blocks of either; WGATHER:
  * 0 or -1 non-temporal, > 0 the default policy), "sell_nt" (SELL slices s >=
  * sell_nt likewise; -1 default: the second half).  The cache policy never
- * changes a result bit.  "vquad_variant" (VCACHE_SPLIT4 configuration,
+ * changes a result bit.  "vcache_xmask" (1 default: VCACHE's x loaders skip
+ * the 128-byte x lines no entry of a unit's panel uses; 0 = load every line;
+ * the same bits).  "wcsr_reduce" (0 default: WCSR's reduce runs over the rows
+ * that have segments and fills the others; 1 = over every row; both
+ * deterministic, their FAST bits may differ).  "vquad_variant" (VCACHE_SPLIT4 configuration,
  * csrc/vquad.hip: 0 default; 1-5, 17-19 other x / entry ring depths; 20 every
  * column-part owner gives up waiting, so the publish-and-count combine runs --
  * exact, counted by the stat "handoff_fallbacks"; 21 XCD placement; 22 / 23

@@ -78,6 +78,7 @@ struct hipspmv_handle {
     bool ok = false;
     uint32_t *d_seg = nullptr, *d_code = nullptr, *d_tickets = nullptr;
     uint64_t *d_vals = nullptr, *d_partial = nullptr;
+    uint64_t* d_xmask = nullptr;  // [0] ordered: the x lines each unit's panels use (build_xmask)
     uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, part_panels = 0, npad = 0, max_seg = 0, max_run = 0;
     uint64_t n_cont = 0;
     int split = 1;
@@ -117,6 +118,7 @@ struct hipspmv_handle {
   int vcache_dma = -1;   // option "vcache_dma": LDS-DMA x loader (-1 default: on for the split geometry)
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
   int vcache_map = 0;    // option "vcache_map": XCD-aware part placement (unused since k_vquad; kept as an option)
+  int vcache_xmask = 1;  // option "vcache_xmask": the ordered loaders skip unused x lines (0: load every line)
   int vquad_variant = 0;  // option "vquad_variant": k_vquad configuration (csrc/vquad.hip launch_vquad_t)
   // bit 0: reserved for a combine hand-off that timed out into unpublished
   // partials (csrc/combine.h has no such path since round 4; the word stays 0)
@@ -191,7 +193,7 @@ static void release(hipspmv_t* h) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& v : h->vc) {
-    void* vp[] = {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial};
+    void* vp[] = {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial, v.d_xmask};
     for (void* p : vp)
       if (p) (void)hipFree(p);
   }
@@ -218,7 +220,7 @@ static void release(hipspmv_t* h) {
 
 static void free_vc(hipspmv_t* h, int k) {
   auto& v = h->vc[k];
-  void* vp[] = {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial};
+  void* vp[] = {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial, v.d_xmask};
   for (void* p : vp)
     if (p) (void)hipFree(p);
   v = hipspmv_handle::Vc{};
@@ -261,6 +263,11 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
   if ((st = dev_upload(&v.d_seg, L.seg.data(), L.seg.size(), h->device_bytes))) return fail(st);
   if ((st = dev_upload(&v.d_code, L.code.data(), L.code.size(), h->device_bytes))) return fail(st);
   if ((st = dev_upload(&v.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return fail(st);
+  if (k == 0) {  // the ordered geometry's loaders skip the x lines no entry of a panel uses
+    std::vector<uint64_t> xm;
+    build_xmask(L, kVcOrderedLoaders, xm);
+    if ((st = dev_upload(&v.d_xmask, xm.data(), xm.size(), h->device_bytes))) return fail(st);
+  }
   if (v.split > 1) {
     // [4 b, 4 b + split): the published-share counters of block b (the owner
     // combine, csrc/combine.h; they return to 0 within each launch), then
@@ -796,6 +803,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     a.nt_from = h->vcache_nt >= 0 ? (uint32_t)std::min<int64_t>(h->vcache_nt, UINT32_MAX)
                 : k < 2 || v.vc4 ? resident_blocks(v.nblocks, h->nnz) : ~0u;
     a.row_runs = v.row_runs;
+    if (h->vcache_xmask) a.xmask = v.d_xmask;
     // an unprofiled launch leaves an unread profile of an earlier launch readable
     // (it writes no stamps); d_prof is allocated when the option is set, never
     // here, so a profiled launch is legal only outside a capture (checked below)
@@ -1005,6 +1013,9 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "vcache_map") {  // 1: split4 XCD pairs; 2: split, one column part per XCD where it can
     if (value < 0 || value > 2) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_map = (int)value;
+  } else if (k == "vcache_xmask") {
+    if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
+    h->vcache_xmask = (int)value;
   } else if (k == "vquad_variant") {  // k_vquad configuration (csrc/vquad.hip)
     if (value < 0 || value > 26) return HIPSPMV_ERR_INVALID_ARG;
     // 6-16 are timing ablations that give wrong y (or race): experimental builds only

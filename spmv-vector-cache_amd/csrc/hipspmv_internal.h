@@ -80,6 +80,8 @@ constexpr uint32_t kVqLanes = 13 * 64;
 constexpr uint32_t kVcSplitCT = 13 * 64;
 // ... and its ordered geometry's: (16 - 8 loader waves) * 64 (VcCfg<1>)
 constexpr uint32_t kVcOrderedCT = 8 * 64;
+// ... and its register-staged x loader waves (VcCfg<1>::WL; build_xmask's word per wave)
+constexpr uint32_t kVcOrderedLoaders = 8;
 // ... and its four-part geometry's: (16 - 2 loader waves) * 64 (VcCfg<4>)
 constexpr uint32_t kVcSplit4CT = 14 * 64;  // k_vquad's compute lanes (13 of 16 waves): the layout's CT
 
@@ -342,6 +344,10 @@ void sort_segments_by_line(VcacheLayout& L);
 void place_segments_banked(VcacheLayout& L, uint32_t CT);
 // k_vquad's placement of the same entries for CT compute lanes (plan.cpp)
 bool build_vcache_lanes(const HostCSR& a, const VcGeom& g, uint32_t CT, VcacheLayout& out);
+// The ordered geometry's x-line mask (k_vcache SPLIT 1, register-staged loaders): per unit, panel
+// and loader wave w (of WL), bit 8 j + k set when an entry of the unit's panel reads a column of x
+// line w * 8 + j * 8 * WL + k (16 columns of 8 bytes per line).  out: units * npanels * WL words.
+void build_xmask(const VcacheLayout& L, uint32_t WL, std::vector<uint64_t>& out);
 void build_sell(const HostCSR& a, SellLayout& out);
 // The column-windowed segment matrix of `a` (columns sorted within each row:
 // vcache_eligible's condition).  Throws std::bad_alloc on host OOM.

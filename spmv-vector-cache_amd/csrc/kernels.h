@@ -29,6 +29,7 @@ struct VcacheArgs {
   int variant = 0;             // k_vquad: configuration (loader waves, x / entry ring depths)
   bool row_runs = false;       // every run of the layout inside one 16-lane row (place_segments_banked):
                                // the split kernel's first continuation step by DPP (xlane 5)
+  const uint64_t* xmask = nullptr;  // ordered geometry: the x lines each unit's panels use (build_xmask)
 };
 
 struct CsrArgs {

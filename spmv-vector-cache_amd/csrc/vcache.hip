@@ -56,6 +56,7 @@ struct VcCfg<1> {  // 4096 rows; x panel 63.5 KiB; 8 loader waves (8 pairs/lane)
   // against 217 here -- each CU streams all 8 MB of x, so the loaders bound it; AUTO's ORDERED kernel is sell)
   static constexpr int VR = kVcOrdered.rows, VP = kVcOrdered.panel, WL = 8, DE = 4, EPT = 3;
 };
+static_assert(VcCfg<1>::WL == (int)kVcOrderedLoaders, "build_xmask's words are the ordered loader waves'");
 template <>
 struct VcCfg<3> {  // 12352 rows; x panel 31.25 KiB; 3 LDS-DMA loader waves, 13 compute waves (2 entries/lane)
   // round-2 sweep on C3 (WL, DE, EPT, loader): 3/4/2 DMA 124.6 us; 3/4/3 DMA 131.2; 2/4/2 DMA 125.8-126.3;
@@ -99,7 +100,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
                                                         uint32_t rows, uint32_t cols, uint32_t rows_per_block,
                                                         uint32_t nblocks, uint32_t npanels, uint32_t part_panels,
                                                         uint32_t npad, uint32_t last, int beta,
-                                                        uint32_t nt_from) {
+                                                        uint32_t nt_from, const uint64_t* __restrict__ xmask) {
 #pragma clang fp contract(off)
   constexpr int VR = VcCfg<SPLIT>::VR, VP = VcCfg<SPLIT>::VP;
   constexpr int VT = kVcThreads, NW = VT / 64, WC = NW - WL;
@@ -146,13 +147,25 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   // load by the lane owning its LDS slot.
   const uint32_t cmax = (cols - 2) & ~1u;
   const T xlast = x[cols - 1];
+  const uint32_t wl = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+  // xmask (SPLIT 1, register-staged loaders): bit 8 j + k of word [unit][panel][loader wave wl] says
+  // whether the unit's entries of that panel use x line wl * 8 + j * LT / 8 + k (build_xmask,
+  // csrc/plan.cpp) -- the 128-byte line that lanes 8 k .. 8 k + 7 of the wave's j-th load cover; the
+  // lanes of a line no entry uses load nothing (no L2 request), and their LDS slots are never read
+  constexpr bool XMASK = SPLIT == 1 && LD == 0 && NJ * 8 <= 64;  // one 64-bit word per loader wave and panel
   auto load_x = [&](uint32_t s, u64x2* r) {
     if (AB & 1) return;
-    const uint32_t base = (AB & 16) ? 0 : (p0 + min(s, npu - 1)) * VP;
+    const uint32_t p = p0 + min(s, npu - 1);
+    const uint32_t base = (AB & 16) ? 0 : p * VP;
+    // (LD 0 only: LD 2's counted vmcnt waits assume every load issued)
+    const uint64_t m = (XMASK && xmask) ? xmask[((size_t)b * npanels + p) * WL + wl] : ~0ull;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const T* src = x + min(base + 2 * (t + j * LT), cmax);
-      r[j] = LD == 2 ? ald_128(src) : *reinterpret_cast<const u64x2*>(src);
+      if (LD == 2)
+        r[j] = ald_128(src);
+      else if ((m >> (j * 8 + (lane >> 3))) & 1u)
+        r[j] = *reinterpret_cast<const u64x2*>(src);
     }
   };
   // LD == 1: the loader lanes' 16-byte chunks go straight into LDS.  A
@@ -160,7 +173,6 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   // 16 B); chunk c of a panel is issued by wave (c / 64) % WL in its
   // instruction c / (64 * WL), lanes past the panel's end masked off.
   constexpr int NDMA = (PAIRS + LT - 1) / LT;
-  const uint32_t wl = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
   auto dma_x = [&](uint32_t s) {
     if (AB & 1) return;
     const uint32_t base = (AB & 16) ? 0 : (p0 + min(s, npu - 1)) * VP;
@@ -628,7 +640,8 @@ static void launch_one(const VcacheArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((k_vcache<T, SPLIT, VcCfg<SPLIT>::WL, VcCfg<SPLIT>::DE, VcCfg<SPLIT>::EPT, 0, MAP, false, LD, CX>),
                      dim3(a.nblocks * SPLIT), dim3(kVcThreads), 0, s, a.seg, a.code, (const T*)a.vals,
                      (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial, a.tickets, a.rows, a.cols,
-                     a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta, a.nt_from);
+                     a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.last, a.beta, a.nt_from,
+                     a.xmask);
 }
 
 template <typename T, int SPLIT, int MAP = 0>
@@ -722,17 +735,17 @@ static hipError_t launch_vcache_profiled_t(const VcacheArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((k_vcache<T, 1, VcCfg<1>::WL, VcCfg<1>::DE, VcCfg<1>::EPT, P>), grid, block, 0, s, a.seg,
                        a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, (T*)a.partial,
                        a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad,
-                       a.last, a.beta, a.nt_from);
+                       a.last, a.beta, a.nt_from, a.xmask);
   } else if (a.max_seg <= (uint32_t)((kVcThreads / 64 - VcCfg<3>::WL) * 64 * VcCfg<3>::EPT)) {
     hipLaunchKernelGGL((k_vcache<T, 3, VcCfg<3>::WL, VcCfg<3>::DE, VcCfg<3>::EPT, P, 0, false, 1, 3>), grid, block, 0,
                        s, a.seg, a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out,
                        (T*)a.partial, a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels,
-                       a.part_panels, a.npad, a.last, a.beta, a.nt_from);
+                       a.part_panels, a.npad, a.last, a.beta, a.nt_from, a.xmask);
   } else {
     hipLaunchKernelGGL((k_vcache<T, 3, VcCfg<3>::WL, VcCfg<3>::DE, VcCfg<3>::EPT, P, 0, false, 1, 0>), grid, block, 0,
                        s, a.seg, a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out,
                        (T*)a.partial, a.tickets, a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels,
-                       a.part_panels, a.npad, a.last, a.beta, a.nt_from);
+                       a.part_panels, a.npad, a.last, a.beta, a.nt_from, a.xmask);
   }
   return hipGetLastError();
 }

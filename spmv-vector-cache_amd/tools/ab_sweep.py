@@ -25,6 +25,9 @@ sys.path.insert(0, os.path.dirname(HERE))
 import hipspmv as hs  # noqa: E402
 
 SETS = {
+    # round 5: the ORDERED loaders skipping the x lines no entry of a panel uses (option vcache_xmask)
+    "xmask": [("ordered (product: xmask)", "vcache", {}), ("ordered xmask off", "vcache", {"vcache_xmask": 0}),
+              ("ordered row order xmask", "bank0:vcache", {})],
     # round 5: k_vcache's four-part geometry (banked, LDS-DMA loaders, xlane 5, resident entries) against the
     # product; "v4:" a handle created with HIPSPMV_SPLIT4_VCACHE=1
     "split4": [("split (product)", "vcache_split", {}), ("vcache 4 parts", "v4:vcache_split4", {}),
@@ -122,9 +125,9 @@ def main():
 
     def reset(opts):
         for k in opts:
-            cur[0].set_option(k, {"vquad_variant": 0, "vcache_nt": -1, "vcache_map": 0}.get(k, -1))
+            cur[0].set_option(k, {"vquad_variant": 0, "vcache_nt": -1, "vcache_map": 0, "vcache_xmask": 1}.get(k, -1))
 
-    mode = hs.MODE_ORDERED if a.set == "ordered" else hs.MODE_FAST
+    mode = hs.MODE_ORDERED if a.set in ("ordered", "xmask") else hs.MODE_FAST
 
     def run(k):
         for _ in range(k):

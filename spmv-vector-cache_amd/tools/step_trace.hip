@@ -95,7 +95,7 @@ int main(int argc, char** argv) {
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(units), dim3(kVcThreads), 0, nullptr, dseg, dcode, dvals, dx, (const double*)dy,
                        dy, dpart, dtick, a.rows, a.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels,
-                       L.npad, a.nnz - 1, 0, 0u);
+                       L.npad, a.nnz - 1, 0, 0u, (const uint64_t*)nullptr);
   };
   // the product: xlane 5 on the banked layout (runs inside 16-lane rows), xlane 3 on the row-order one
   const bool x5 = !row_order && L.row_runs;
@@ -108,7 +108,7 @@ int main(int argc, char** argv) {
     const char* name;
     void (*k)(const uint32_t*, const uint32_t*, const double*, const double*, const double*, double*, double*,
               uint32_t*, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, int,
-              uint32_t);
+              uint32_t, const uint64_t*);
     uint32_t window;
   };
   const V vars[] = {{"product", product, 13 * 64 * 2},

@@ -97,7 +97,7 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(kern, dim3(A.nblocks * A.split), dim3(kVcThreads), 0, nullptr, A.seg, A.code,
                            (const double*)A.vals, (const double*)A.x, (const double*)A.y_in, (double*)A.y_out,
                            (double*)A.partial, A.tickets, A.rows, A.cols, A.rows_per_block, A.nblocks, A.npanels,
-                           A.part_panels, A.npad, A.last, A.beta, ~0u);
+                           A.part_panels, A.npad, A.last, A.beta, ~0u, (const uint64_t*)nullptr);
       });
       std::printf("  %-30s mask %2d %8.2f us  (alg %6.1f GB/s)", nm, mask, us, alg / us * 1e-3);
       if (mask == 0) {  // compare against the first (ordered) result
@@ -117,7 +117,7 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(kern, dim3(units), dim3(kVcThreads), 0, nullptr, A.seg, A.code, (const double*)A.vals,
                            (const double*)A.x, (const double*)A.y_in, (double*)A.y_out, (double*)A.partial,
                            A.tickets, A.rows, A.cols, A.rows_per_block, A.nblocks, A.npanels, A.part_panels, A.npad,
-                           A.last, A.beta, ~0u);
+                           A.last, A.beta, ~0u, (const uint64_t*)nullptr);
       CK(hipDeviceSynchronize());
       std::vector<uint32_t> st(8 * units);
       const uint32_t* src = A.split == 1 ? reinterpret_cast<const uint32_t*>(A.partial) : A.tickets + 2 * A.nblocks;

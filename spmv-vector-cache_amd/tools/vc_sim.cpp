@@ -103,7 +103,8 @@ static double madd(double acc, double a, double b) {
 // arrival_rev: the column parts of every block arrive in reverse unit order
 // (the combine's result must not depend on the order)
 static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, const Cfg& c, const std::vector<double>& x,
-                                    const std::vector<double>& yin, int beta, bool arrival_rev = false) {
+                                    const std::vector<double>& yin, int beta, bool arrival_rev = false,
+                                    const std::vector<uint64_t>* xmask = nullptr) {
   const bool gather = c.LD == 2;  // k_wgather: every wave computes, no loader role
   const int VT = 1024, NW = VT / 64, WC = gather ? NW : NW - c.WL, LT = c.WL * 64, CT = WC * 64;
   const uint32_t CMASK = (1u << c.CB) - 1, RMASK = (1u << (30 - c.CB)) - 1;
@@ -181,6 +182,12 @@ static std::vector<double> simulate(const HostCSR& A, const VcacheLayout& L, con
       }
       for (int t = 0; t < LT; ++t)
         for (int j = 0; j < NJ; ++j) {
+          // the ordered loaders' x-line mask (build_xmask): a lane of an unused line loads nothing and
+          // its LDS slot keeps what it held (NaN here: any read of it shows in y)
+          if (xmask) {
+            const uint64_t m = (*xmask)[((size_t)b * npanels + p0 + std::min(s, npu - 1)) * c.WL + t / 64];
+            if (!((m >> (j * 8 + (t % 64) / 8)) & 1u)) continue;
+          }
           const uint32_t a = std::min(base + 2 * (t + j * LT), cmax);
           const double v0 = X.get(a), v1 = X.get(a + 1);
           if ((j + 1) * LT <= (int)PAIRS || (uint32_t)(t + j * LT) < PAIRS) {
@@ -698,6 +705,21 @@ int main(int argc, char** argv) {
           if (std::memcmp(y.data(), yb.data(), 8ull * cs.A.rows) != 0) {
             std::printf("%-28s banked placement changes result bits\n", cs.name.c_str());
             ++failures;
+          }
+          if (c.SPLIT == 1 && c.LD == 0 && c.WL == (int)kVcOrderedLoaders) {
+            // the ordered loaders skipping the x lines no entry of a panel uses: the same bits
+            std::vector<uint64_t> xm;
+            build_xmask(B, kVcOrderedLoaders, xm);
+            const auto ym = simulate(cs.A, B, c, x, yin, beta, false, &xm);
+            size_t skipped = 0, total = 0;
+            for (uint64_t w : xm) skipped += 64 - __builtin_popcountll(w), total += 64;
+            if (std::memcmp(y.data(), ym.data(), 8ull * cs.A.rows) != 0) {
+              std::printf("%-28s x-line mask changes result bits\n", cs.name.c_str());
+              ++failures;
+            } else if (beta == 0) {
+              std::printf("%-28s x-line mask: same bits, %.1f %% of line slots skipped\n", cs.name.c_str(),
+                          100.0 * skipped / std::max<size_t>(total, 1));
+            }
           }
         }
         const auto r = reference(cs.A, x, yin, beta);
