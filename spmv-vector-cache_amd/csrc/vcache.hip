@@ -153,19 +153,29 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   // csrc/plan.cpp) -- the 128-byte line that lanes 8 k .. 8 k + 7 of the wave's j-th load cover; the
   // lanes of a line no entry uses load nothing (no L2 request), and their LDS slots are never read
   constexpr bool XMASK = SPLIT == 1 && LD == 0 && NJ * 8 <= 64;  // one 64-bit word per loader wave and panel
-  auto load_x = [&](uint32_t s, u64x2* r) {
+  // the mask word of panel s (all ones without a mask); the LD 0 loader loads it a step before its
+  // x loads need it (LD 2's counted vmcnt waits assume every load issued: no mask there)
+  auto mask_of = [&](uint32_t s) -> uint64_t {
+    return (XMASK && xmask) ? xmask[((size_t)b * npanels + p0 + min(s, npu - 1)) * WL + wl] : ~0ull;
+  };
+  const __amdgpu_buffer_rsrc_t xrs = buf_rsrc(x, XMASK ? cols * (uint32_t)sizeof(T) : 0u);
+  auto load_x = [&](uint32_t s, u64x2* r, uint64_t m = ~0ull) {
     if (AB & 1) return;
-    const uint32_t p = p0 + min(s, npu - 1);
-    const uint32_t base = (AB & 16) ? 0 : p * VP;
-    // (LD 0 only: LD 2's counted vmcnt waits assume every load issued)
-    const uint64_t m = (XMASK && xmask) ? xmask[((size_t)b * npanels + p) * WL + wl] : ~0ull;
+    const uint32_t base = (AB & 16) ? 0 : (p0 + min(s, npu - 1)) * VP;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const T* src = x + min(base + 2 * (t + j * LT), cmax);
-      if (LD == 2)
-        r[j] = ald_128(src);
-      else if ((m >> (j * 8 + (lane >> 3))) & 1u)
-        r[j] = *reinterpret_cast<const u64x2*>(src);
+      const uint32_t ci = min(base + 2 * (t + j * LT), cmax);
+      if constexpr (XMASK) {
+        // branch-free: a lane of an unused line gets an out-of-range offset in the descriptor of x --
+        // zero, and no memory request (a divergent `if` around a plain load made hipcc wait vmcnt(0)
+        // before every load of the ring)
+        const bool need = (m >> (j * 8 + (lane >> 3))) & 1u;
+        r[j] = __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(
+                                             xrs, need ? (int)(ci * (uint32_t)sizeof(T)) : (int)0x80000000, 0, 0));
+      } else {
+        const T* src = x + ci;
+        r[j] = LD == 2 ? ald_128(src) : *reinterpret_cast<const u64x2*>(src);
+      }
     }
   };
   // LD == 1: the loader lanes' 16-byte chunks go straight into LDS.  A
@@ -452,6 +462,10 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   // pass merge a path with fewer loads in flight into the loop header and
   // emit vmcnt(0) there (tools/vmcnt_check.py finds the same infeasible
   // path); without it the compiler's own waits are exact (CX == 3).
+  // (The ordered geometry, SPLIT 1 / CX 0, does not pad: its unpadded loader
+  // loop drains the two-panel x ring before every odd step's stores, and
+  // padding fixed that but cost its three extra steps and measured 2 % slower:
+  // 171.9 against 168-170 us, profiles/r05/logs/ab_xmask_b_pad.log.)
   constexpr bool PAD = CX >= 2;
   constexpr uint32_t ALIGN = (DE % 2 == 0) ? DE : 2 * DE;
   const uint32_t nsteps = PAD ? (npu + ALIGN - 1) / ALIGN * ALIGN : npu;
@@ -500,11 +514,13 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     vm_wait<0>();
   } else if (loader) {
     u64x2 R[2][NJ];  // R[(s+1)&1] holds x(s+1) during step s
-    load_x(0, R[0]);
+    load_x(0, R[0], mask_of(0));
     store_x(0, R[0]);
-    load_x(1, R[1]);
-    load_x(2, R[0]);
+    load_x(1, R[1], mask_of(1));
+    load_x(2, R[0], mask_of(2));
+    uint64_t mnext = mask_of(3);  // panel s + 3's mask word, loaded during step s - 1
     barrier();
+    tr_rel(255, t_entry, 0);
     if (AB & 128) {
       stamp(1, now());
       pf_mark = __builtin_amdgcn_s_memtime();
@@ -514,9 +530,14 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       for (int i = 0; i < 2; ++i) {
         const uint32_t s = base + i;  // parity of s == parity of i
         if (!PAD && s >= npu) break;
+        const uint64_t m3 = mnext;
+        mnext = mask_of(s + 4);
         if (s + 1 < npu) store_x(s + 1, R[(i + 1) & 1]);
-        load_x(s + 3, R[(i + 1) & 1]);
+        const uint32_t t_ready = (AB & 8192) ? tr_now() : 0;  // panel s + 1 landed and stored
+        load_x(s + 3, R[(i + 1) & 1], m3);
+        const uint32_t t_arr = (AB & 8192) ? tr_now() : 0;
         pbarrier();
+        tr_rel(s, t_ready, t_arr);
       }
     }
   } else {
@@ -584,7 +605,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
           if (CX) {
             if (!PAD || s < npu) apply_cx(s, EC[i], EV[i]);
           } else {
-            apply(s, EC[i], EV[i]);
+            if (!PAD || s < npu) apply(s, EC[i], EV[i]);
           }
           if (AB & 8192) {  // the apply's LDS work retired, then the next loads issued
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

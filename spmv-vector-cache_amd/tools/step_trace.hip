@@ -68,15 +68,19 @@ int main(int argc, char** argv) {
   a.vals.assign(reinterpret_cast<uint64_t*>(v.data()), reinterpret_cast<uint64_t*>(v.data()) + a.nnz);
   std::vector<double> x(n);
   for (uint32_t i = 0; i < n; ++i) x[i] = uniform11(splitmix64_at(3, i));
-  const VcGeom g = kVcSplit;
+  // "ordered": the ORDERED geometry (SPLIT 1, 8 register-staged loader waves, its x-line mask)
+  const bool ordered = argc > 1 && std::string(argv[1]) == "ordered";
+  const VcGeom g = ordered ? kVcOrdered : kVcSplit;
   VcacheLayout L;
   build_vcache(a, g, L);
   const bool row_order = argc > 1 && std::string(argv[1]) == "roworder";
-  if (!row_order) place_segments_banked(L, kVcSplitCT);  // the product layout (capi.cpp upload_vc)
+  if (!row_order) place_segments_banked(L, ordered ? kVcOrderedCT : kVcSplitCT);  // the product layouts (upload_vc)
+  std::vector<uint64_t> xm;
+  if (ordered) build_xmask(L, kVcOrderedLoaders, xm);
   const uint32_t units = L.nblocks * g.split;
   if (!vcache_grid_ok(a.rows, a.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels, L.npad,
                       (uint32_t)g.panel, g.split, g) ||
-      L.npad + 1 > 255 || L.max_seg > 13u * 64 * 2) {
+      L.npad + 1 > 255 || L.max_seg > (ordered ? 8u * 64 * 3 : 13u * 64 * 2)) {
     std::printf("geometry check failed\n");
     return 1;
   }
@@ -90,19 +94,25 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dpart, part_bytes));
   uint32_t* dtick = up(std::vector<uint32_t>(4 * L.nblocks + 8 * units, 0));
   const uint32_t* dseg = up(L.seg);
+  const uint64_t* dxm = ordered ? up(xm) : nullptr;
   const uint32_t* dcode = up(std::vector<uint32_t>(L.code.begin(), L.code.end()));
   const double* dvals = reinterpret_cast<const double*>(up(std::vector<uint64_t>(L.vals.begin(), L.vals.end())));
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(units), dim3(kVcThreads), 0, nullptr, dseg, dcode, dvals, dx, (const double*)dy,
                        dy, dpart, dtick, a.rows, a.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels,
-                       L.npad, a.nnz - 1, 0, 0u, (const uint64_t*)nullptr);
+                       L.npad, a.nnz - 1, 0, 0u, dxm);
   };
   // the product: xlane 5 on the banked layout (runs inside 16-lane rows), xlane 3 on the row-order one
   const bool x5 = !row_order && L.row_runs;
-  auto product = x5 ? k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 5> : k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 3>;
-  auto traced = x5 ? k_vcache<double, 3, 3, 4, 2, 8192 | 64, 0, false, 1, 5>
-                   : k_vcache<double, 3, 3, 4, 2, 8192 | 64, 0, false, 1, 3>;
-  auto nocomb = x5 ? k_vcache<double, 3, 3, 4, 2, 64, 0, false, 1, 5> : k_vcache<double, 3, 3, 4, 2, 64, 0, false, 1, 3>;
+  auto product = ordered ? k_vcache<double, 1, 8, 4, 3, 0, 0, false, 0, 0>
+                 : x5    ? k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 5>
+                         : k_vcache<double, 3, 3, 4, 2, 0, 0, false, 1, 3>;
+  auto traced = ordered ? k_vcache<double, 1, 8, 4, 3, 8192 | 64, 0, false, 0, 0>
+                : x5    ? k_vcache<double, 3, 3, 4, 2, 8192 | 64, 0, false, 1, 5>
+                        : k_vcache<double, 3, 3, 4, 2, 8192 | 64, 0, false, 1, 3>;
+  auto nocomb = ordered ? product
+                : x5    ? k_vcache<double, 3, 3, 4, 2, 64, 0, false, 1, 5>
+                        : k_vcache<double, 3, 3, 4, 2, 64, 0, false, 1, 3>;
   // configurations on the same layout (the register window must hold every segment)
   struct V {
     const char* name;
@@ -138,7 +148,7 @@ int main(int argc, char** argv) {
   std::vector<double> y0(n), y1(n);
   launch(product);
   CK(hipMemcpy(y0.data(), dy, 8ull * n, hipMemcpyDeviceToHost));
-  for (int round = 0; round < 3; ++round)
+  for (int round = 0; round < (ordered ? 0 : 3); ++round)
     for (const V& v : vars) {
       if (L.max_seg > v.window) continue;
       const double us = timeit(v.k, 100);
@@ -148,21 +158,22 @@ int main(int argc, char** argv) {
       for (uint32_t i = 0; i < n; ++i) md = std::max(md, std::fabs(y1[i] - y0[i]) / (std::fabs(y0[i]) + 1e-300));
       std::printf("round %d  %-26s %8.2f us  max rel diff vs product %.1e\n", round, v.name, us, md);
     }
-  std::printf("C3 FAST, %u units, %u steps per unit: product %.2f us, without combine %.2f us, traced %.2f us\n",
-              units, L.part_panels, timeit(product, 100), timeit(nocomb, 100), timeit(traced, 100));
+  std::printf("C3 %s, %u units, %u steps per unit: product %.2f us, without combine %.2f us, traced %.2f us\n",
+              ordered ? "ORDERED" : "FAST", units, L.part_panels, timeit(product, 100), timeit(nocomb, 100),
+              timeit(traced, 100));
   CK(hipMemset(dpart, 0, 16ull * units * 16 * 256));
   for (int i = 0; i < 20; ++i) launch(traced);
   CK(hipDeviceSynchronize());
   std::vector<uint32_t> tr(4ull * units * 16 * 256);
   CK(hipMemcpy(tr.data(), dpart, 4ull * tr.size(), hipMemcpyDeviceToHost));
   auto at = [&](uint32_t u, uint32_t w, uint32_t s, int f) { return tr[(((size_t)u * 16 + w) * 256 + s) * 4 + f]; };
-  constexpr uint32_t WL = 3;
+  const uint32_t WL = ordered ? 8 : 3;
   Q step, crit_mem, crit_apply, crit_issue, crit_loader_mem, slack, comp_mem, comp_apply, comp_issue, loader_mem,
       prologue, spread;
   uint64_t crit_load = 0, crit_comp = 0;
   for (uint32_t u = 0; u < units; ++u) {
-    const uint32_t h = (u % (8 * 3)) / std::min(8u, L.nblocks - u / 24 * 8);
-    const uint32_t npu = vc_part_first(h + 1, L.npanels, 3) - vc_part_first(h, L.npanels, 3);
+    const uint32_t h = ordered ? 0 : (u % (8 * 3)) / std::min(8u, L.nblocks - u / 24 * 8);
+    const uint32_t npu = ordered ? L.npanels : vc_part_first(h + 1, L.npanels, 3) - vc_part_first(h, L.npanels, 3);
     uint32_t r_prev = UINT32_MAX, ent = UINT32_MAX;
     for (uint32_t w = 0; w < 16; ++w) {
       r_prev = std::min(r_prev, at(u, w, 255, 2));
