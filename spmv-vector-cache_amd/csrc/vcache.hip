@@ -272,15 +272,39 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     }
     ylds[row] = acc;
   };
+  // A row has one run per step (its entries of a panel are consecutive in the
+  // segment), so the run heads of a step name distinct rows: every slot's x and
+  // y reads issue before any y write (the compiler cannot prove the rows
+  // distinct and would chain slot j + 1's reads behind slot j's write), the
+  // same additions in the same order.
   auto apply = [&](uint32_t s, const uint32_t* c, const T* v) {
     if (AB & 8) return;
     const T* xs = xb[s & 1];
     const uint32_t beg = segl[s], end = segl[s + 1];
+    T acc[EPT];
+    bool head[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const uint32_t q = beg + ct + j * CT;
-      if (q < end && !(c[j] & kVcCont)) run(q, c[j], v[j], xs);
+      head[j] = q < end && !(c[j] & kVcCont);
+      const uint32_t row = (c[j] >> 16) & 0x3FFF;
+      const T xv = xs[head[j] ? (c[j] & 0xFFFF) : 0u], yv = ylds[head[j] ? row : 0u];
+      acc[j] = madd(yv, v[j], xv);
     }
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      if (head[j] && (c[j] & kVcMore)) {  // run continuation, re-read from memory (rare)
+        uint32_t i = beg + ct + j * CT, code = c[j];
+        while (code & kVcMore) {
+          ++i;
+          code = ecode[i];
+          acc[j] = madd(acc[j], evals[i], xs[code & 0xFFFF]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < EPT; ++j)
+      if (head[j]) ylds[(c[j] >> 16) & 0x3FFF] = acc[j];
     for (uint32_t q = beg + EPT * CT + ct; q < end; q += CT) {  // beyond the register window (slow path)
       const uint32_t code = ecode[q];
       if (!(code & kVcCont)) run(q, code, evals[q], xs);
