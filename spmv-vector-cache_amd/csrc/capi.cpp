@@ -1049,7 +1049,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
     if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_nt = value;
   } else if (k == "vcache_xlane") {
-    if (value < -1 || value > 5) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < -1 || value > 6) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_xlane = (int)value;
   } else if (k == "mode") {
     if (value != HIPSPMV_MODE_ORDERED && value != HIPSPMV_MODE_FAST) return HIPSPMV_ERR_INVALID_ARG;

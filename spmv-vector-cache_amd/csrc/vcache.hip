@@ -291,14 +291,41 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       const T xv = xs[head[j] ? (c[j] & 0xFFFF) : 0u], yv = ylds[head[j] ? row : 0u];
       acc[j] = madd(yv, v[j], xv);
     }
+    if constexpr (CX == 6) {
+      // the layout keeps every run inside its 16-lane row (place_segments_banked): a run head takes its
+      // first continuation entry from the next lane by DPP (every lane executes the DPP), and re-reads
+      // from memory only from the third entry of a run on (C3: runs of two, 24 % of the steps)
+      uint32_t cn[EPT];
+      T vn[EPT], xn[EPT];
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-      if (head[j] && (c[j] & kVcMore)) {  // run continuation, re-read from memory (rare)
-        uint32_t i = beg + ct + j * CT, code = c[j];
-        while (code & kVcMore) {
-          ++i;
-          code = ecode[i];
-          acc[j] = madd(acc[j], evals[i], xs[code & 0xFFFF]);
+      for (int j = 0; j < EPT; ++j) {
+        cn[j] = dpp_next32(c[j]);
+        vn[j] = dpp_next(v[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) xn[j] = xs[head[j] && (c[j] & kVcMore) ? (cn[j] & 0xFFFF) : 0u];
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        if (head[j] && (c[j] & kVcMore)) {
+          acc[j] = madd(acc[j], vn[j], xn[j]);
+          uint32_t i = beg + ct + j * CT + 1, code = cn[j];
+          while (code & kVcMore) {  // runs of three or more
+            ++i;
+            code = ecode[i];
+            acc[j] = madd(acc[j], evals[i], xs[code & 0xFFFF]);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        if (head[j] && (c[j] & kVcMore)) {  // run continuation, re-read from memory (rare)
+          uint32_t i = beg + ct + j * CT, code = c[j];
+          while (code & kVcMore) {
+            ++i;
+            code = ecode[i];
+            acc[j] = madd(acc[j], evals[i], xs[code & 0xFFFF]);
+          }
         }
       }
     }
@@ -490,7 +517,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
   // loop drains the two-panel x ring before every odd step's stores, and
   // padding fixed that but cost its three extra steps and measured 2 % slower:
   // 171.9 against 168-170 us, profiles/r05/logs/ab_xmask_b_pad.log.)
-  constexpr bool PAD = CX >= 2;
+  constexpr bool PAD = CX >= 2 && CX != 6;
   constexpr uint32_t ALIGN = (DE % 2 == 0) ? DE : 2 * DE;
   const uint32_t nsteps = PAD ? (npu + ALIGN - 1) / ALIGN * ALIGN : npu;
   __syncthreads();  // segl visible
@@ -626,7 +653,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
             vm_wait<1 + (2 * EPT + 1) * (DE - 1)>();
             t_ready = tr_now();
           }
-          if (CX) {
+          if (CX && CX != 6) {
             if (!PAD || s < npu) apply_cx(s, EC[i], EV[i]);
           } else {
             if (!PAD || s < npu) apply(s, EC[i], EV[i]);
@@ -708,6 +735,8 @@ static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
     launch_one<T, SPLIT, 0, 3, MAP>(a, s);
   } else if (cx == 5) {  // (a banked layout: runs inside 16-lane rows)
     launch_one<T, SPLIT, 0, 5, MAP>(a, s);
+  } else if (cx == 6) {  // the ordered geometry on a banked layout: CX 0 with the DPP first continuation
+    launch_one<T, SPLIT, 0, 6, MAP>(a, s);
   } else if (cx == 0) {
     ld == 1 ? launch_one<T, SPLIT, 1, 0, MAP>(a, s) : launch_one<T, SPLIT, 0, 0, MAP>(a, s);
   } else if (cx == 1) {
@@ -741,8 +770,11 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   // -1 (default): 5 for the split geometry where the layout allows it, else 3
   // (C3: 131.7 us against 135.7 with the run continuation re-read from
   // memory), 0 for the others.
+  // 6 (ordered, a layout whose runs stay inside 16-lane rows): 0 with the
+  // first continuation step by DPP.
   int xl = a.xlane < 0 ? (a.split >= 3 ? (a.row_runs ? 5 : 3) : 0) : a.xlane;
   if (xl == 5 && !a.row_runs) xl = 3;
+  if (xl == 6 && (!a.row_runs || a.split != 1)) xl = 0;
   const int cx = xl && a.max_seg <= window(a.split) ? xl : 0;
   // dma -1 (default): register-staged x loaders; the split geometry's two
   // loader waves always stage by LDS-DMA (dispatch)

@@ -28,6 +28,10 @@ SETS = {
     # round 5: the ORDERED loaders skipping the x lines no entry of a panel uses (option vcache_xmask)
     "xmask": [("ordered (product: xmask)", "vcache", {}), ("ordered xmask off", "vcache", {"vcache_xmask": 0}),
               ("ordered row order xmask", "bank0:vcache", {})],
+    # round 5: ORDERED's first run continuation by DPP (xlane 6, the default on banked layouts) against
+    # re-reading it from memory (xlane 0)
+    "ordered6": [("ordered (product)", "vcache", {}), ("ordered xlane 0", "vcache", {"vcache_xlane": 0}),
+                 ("ordered xlane 6", "vcache", {"vcache_xlane": 6})],
     # round 5: k_vcache's four-part geometry (banked, LDS-DMA loaders, xlane 5, resident entries) against the
     # product; "v4:" a handle created with HIPSPMV_SPLIT4_VCACHE=1
     "split4": [("split (product)", "vcache_split", {}), ("vcache 4 parts", "v4:vcache_split4", {}),
@@ -127,7 +131,7 @@ def main():
         for k in opts:
             cur[0].set_option(k, {"vquad_variant": 0, "vcache_nt": -1, "vcache_map": 0, "vcache_xmask": 1}.get(k, -1))
 
-    mode = hs.MODE_ORDERED if a.set in ("ordered", "xmask") else hs.MODE_FAST
+    mode = hs.MODE_ORDERED if a.set in ("ordered", "xmask", "ordered6") else hs.MODE_FAST
 
     def run(k):
         for _ in range(k):

@@ -19,6 +19,7 @@ import hipspmv as hs  # noqa: E402
 
 # settings: (label, {option: value or ("groups", fraction)})
 SETS = {
+    "one": [("product", {})],
     "reduce": [("compact reduce", {}), ("all-rows reduce", {"wcsr_reduce": 1})],
     "res": [("all nt (product)", {}), ("resident 1/8", {"wcsr_res": ("groups", 0.125)}),
             ("resident 1/4", {"wcsr_res": ("groups", 0.25)}), ("resident 3/8", {"wcsr_res": ("groups", 0.375)}),

@@ -635,6 +635,50 @@ def test_vcache_split_entry_loads(gpu, xlane):  # 3: clamped entry loads; 4: mas
     assert ran >= 3
 
 
+@pytest.mark.parametrize("xlane,xmask", [(-1, 1), (0, 1), (6, 1), (6, 0), (0, 0)])
+def test_ordered_vcache_continuation_and_xmask(gpu, xlane, xmask):
+    # the ORDERED vcache's run continuations (6, the default on banked layouts: the first continuation
+    # entry from the next lane by DPP, the rest re-read from memory; 0: all re-read) and its x-line mask
+    # (loaders skip the x lines no entry of a panel uses): bit-exact to SoftwareSpMV, f64 and u64, on
+    # rows with runs of one, two and many entries per panel (dense rows: runs up to hundreds long)
+    cases = [(65536, 1 << 20, None), (5000, 20001, 0.002), (257, 12161, 0.3), (70000, 13001, 0.0008)]
+    for rows, cols, dens in cases:
+        rng = np.random.default_rng(rows + cols)
+        if dens is None:
+            rowptr, colind, vals = hs.gen_stripe_csr(3, rows, cols, 32)
+        else:
+            lens = rng.binomial(cols, dens, rows)
+            rowptr = np.zeros(rows + 1, np.uint32)
+            rowptr[1:] = np.cumsum(lens)
+            colind = np.concatenate([np.sort(rng.choice(cols, n, replace=False)) for n in lens]).astype(np.uint32)
+            vals = rng.uniform(-1, 1, colind.size)
+        x = rng.uniform(-1, 1, cols)
+        h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+        if not h.stat("vcache_eligible"):
+            h.close()
+            continue
+        h.set_kernel("vcache")
+        h.set_option("vcache_xlane", xlane)
+        h.set_option("vcache_xmask", xmask)
+        colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+        for beta in (0, 1):
+            y0 = rng.uniform(-1, 1, rows)
+            y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else None), rows=rows)
+            assert h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_ORDERED).tobytes() == y_ref.tobytes(), \
+                (rows, cols, beta)
+        uv = rng.integers(0, 2**64, colind.size, dtype=np.uint64)
+        ux = rng.integers(0, 2**64, cols, dtype=np.uint64)
+        hu = hs.Handle.from_csr(rowptr, colind, uv, rows, cols)
+        hu.set_kernel("vcache")
+        hu.set_option("vcache_xlane", xlane)
+        hu.set_option("vcache_xmask", xmask)
+        _, _, cuv = oracle.csr2csc(rows, cols, rowptr, colind, uv)
+        assert hu.exec(ux, beta=0, mode=hs.MODE_ORDERED).tobytes() == \
+            oracle.spmv_csc(colptr, rowind, cuv, ux, rows=rows).tobytes(), (rows, cols)
+        hu.close()
+        h.close()
+
+
 def test_vquad_c3_full_size(gpu):
     # the four-part kernel on full C3: x streamed into LDS per launch is 64 row
     # blocks x 8 MB (three parts: 85 x 8 MB); deterministic and within the bound
