@@ -27,9 +27,12 @@
 #include "hipspmv_internal.h"
 #include "vc_map.h"
 
+#include <atomic>
+#include <thread>
+
 using namespace hipspmv;
 
-static int g_errors = 0;
+static thread_local int g_errors = 0;  // per replay thread (main runs the cases in parallel)
 #define CHECK(cond, ...)                                   \
   do {                                                     \
     if (!(cond)) {                                         \
@@ -525,7 +528,15 @@ int main(int argc, char** argv) {
     std::printf("grid guard (incident geometry rejected, product accepted): %s\n", ok ? "ok" : "FAIL");
     failures += !ok;
   }
-  for (auto& cs : cases) {
+  // the cases replay in parallel (a case's lines are printed together, in case order)
+  std::vector<std::string> outs(cases.size());
+  std::atomic<int> fails{failures};
+  std::atomic<size_t> next{0};
+  auto run_case = [&](Case& cs, std::string& text) {
+    char* buf = nullptr;
+    size_t len = 0;
+    FILE* fo = open_memstream(&buf, &len);
+    int nfail = 0;
     // host-side planning beside the replay: CSC -> CSR (csc_to_csr, the
     // hipspmv_create path) reproduces the case's CSR exactly, and the
     // csr_vector row groups tile the rows
@@ -627,8 +638,8 @@ int main(int argc, char** argv) {
         build_row_groups(G, gg);
         wins = wins && gg.front() == 0 && gg.back() == G.rows;
       }
-      failures += !(same && tiles && shards && wins);
-      std::printf("%-28s csc_to_csr %s, row groups %s, shard groups %s, windowed segments %s\n", cs.name.c_str(),
+      nfail += !(same && tiles && shards && wins);
+      std::fprintf(fo, "%-28s csc_to_csr %s, row groups %s, shard groups %s, windowed segments %s\n", cs.name.c_str(),
                   same ? "ok" : "FAIL", tiles ? "ok" : "FAIL", shards ? "ok" : "FAIL", wins ? "ok" : "FAIL");
     }
     std::vector<double> x(cs.A.cols), yin(cs.A.rows);
@@ -638,7 +649,7 @@ int main(int argc, char** argv) {
       VcGeom g{c.VR, c.VP, c.SPLIT, c.CB};
       if (c.LD == 2) g.segmax = kWgWindow.segmax;  // k_wgather's segment table
       if (!vcache_eligible(cs.A, g)) {
-        std::printf("%-28s split=%d ld=%d: not eligible\n", cs.name.c_str(), c.SPLIT, c.LD);
+        std::fprintf(fo, "%-28s split=%d ld=%d: not eligible\n", cs.name.c_str(), c.SPLIT, c.LD);
         continue;
       }
       VcacheLayout L;
@@ -650,19 +661,19 @@ int main(int argc, char** argv) {
         build_vcache(cs.A, g, D, true);
         if (!(R.code == L.code && R.vals == L.vals && R.seg == L.seg && D.code == L.code && D.vals == L.vals &&
               D.seg == L.seg)) {
-          std::printf("%-28s sort_segments_by_line differs from the stable-sort reference\n", cs.name.c_str());
-          ++failures;
+          std::fprintf(fo, "%-28s sort_segments_by_line differs from the stable-sort reference\n", cs.name.c_str());
+          ++nfail;
         }
       }
       // the launcher's guard (vcache_grid_ok) accepts every product layout
       if (!vcache_grid_ok(cs.A.rows, cs.A.cols, L.rows_per_block, L.nblocks, L.npanels, L.part_panels, L.npad,
                           L.geom.panel, c.SPLIT, g)) {
-        std::printf("%-28s split=%d: product layout REJECTED by vcache_grid_ok\n", cs.name.c_str(), c.SPLIT);
-        ++failures;
+        std::fprintf(fo, "%-28s split=%d: product layout REJECTED by vcache_grid_ok\n", cs.name.c_str(), c.SPLIT);
+        ++nfail;
         continue;
       }
       if (c.CX && L.max_seg > (uint32_t)((16 - c.WL) * 64 * c.EPT)) {  // launch_vcache falls back to CX 0
-        std::printf("%-28s split=%d cx=%d: segments exceed the window, CX 0 runs\n", cs.name.c_str(), c.SPLIT, c.CX);
+        std::fprintf(fo, "%-28s split=%d cx=%d: segments exceed the window, CX 0 runs\n", cs.name.c_str(), c.SPLIT, c.CX);
         continue;
       }
       // the product's bank-aware placement (plan.cpp place_segments_banked):
@@ -693,8 +704,8 @@ int main(int argc, char** argv) {
             perm = perm && a0 == a1;
           }
         if (!perm) {
-          std::printf("%-28s place_segments_banked: not a run-preserving permutation\n", cs.name.c_str());
-          ++failures;
+          std::fprintf(fo, "%-28s place_segments_banked: not a run-preserving permutation\n", cs.name.c_str());
+          ++nfail;
         }
       }
       for (int beta = 0; beta < 2; ++beta) {
@@ -703,8 +714,8 @@ int main(int argc, char** argv) {
         if (banked) {
           const auto yb = simulate(cs.A, B, c, x, yin, beta);
           if (std::memcmp(y.data(), yb.data(), 8ull * cs.A.rows) != 0) {
-            std::printf("%-28s banked placement changes result bits\n", cs.name.c_str());
-            ++failures;
+            std::fprintf(fo, "%-28s banked placement changes result bits\n", cs.name.c_str());
+            ++nfail;
           }
           if (c.SPLIT == 1 && c.LD == 0 && c.WL == (int)kVcOrderedLoaders) {
             // the ordered loaders skipping the x lines no entry of a panel uses: the same bits
@@ -714,10 +725,10 @@ int main(int argc, char** argv) {
             size_t skipped = 0, total = 0;
             for (uint64_t w : xm) skipped += 64 - __builtin_popcountll(w), total += 64;
             if (std::memcmp(y.data(), ym.data(), 8ull * cs.A.rows) != 0) {
-              std::printf("%-28s x-line mask changes result bits\n", cs.name.c_str());
-              ++failures;
+              std::fprintf(fo, "%-28s x-line mask changes result bits\n", cs.name.c_str());
+              ++nfail;
             } else if (beta == 0) {
-              std::printf("%-28s x-line mask: same bits, %.1f %% of line slots skipped\n", cs.name.c_str(),
+              std::fprintf(fo, "%-28s x-line mask: same bits, %.1f %% of line slots skipped\n", cs.name.c_str(),
                           100.0 * skipped / std::max<size_t>(total, 1));
             }
           }
@@ -743,12 +754,25 @@ int main(int argc, char** argv) {
           }
         }
         const bool ok = bad == 0 && g_errors == 0;
-        failures += !ok;
-        std::printf("%-28s split=%d ld=%d cx=%d beta=%d units=%u panels=%u: %s (%zu rows off, %d violations)\n",
+        nfail += !ok;
+        std::fprintf(fo, "%-28s split=%d ld=%d cx=%d beta=%d units=%u panels=%u: %s (%zu rows off, %d violations)\n",
                     cs.name.c_str(), c.SPLIT, c.LD, c.CX, beta, L.nblocks * c.SPLIT, L.npanels, ok ? "ok" : "FAIL",
                     bad, g_errors);
       }
     }
-  }
+      std::fclose(fo);
+    text.assign(buf, len);
+    std::free(buf);
+    fails += nfail;
+  };
+  std::vector<std::thread> pool;
+  const unsigned nt = std::max(1u, std::min<unsigned>(8, std::thread::hardware_concurrency()));
+  for (unsigned t = 0; t < nt; ++t)
+    pool.emplace_back([&] {
+      for (size_t i; (i = next++) < cases.size();) run_case(cases[i], outs[i]);
+    });
+  for (auto& th : pool) th.join();
+  for (const auto& o : outs) std::fputs(o.c_str(), stdout);
+  failures = fails;
   return failures ? 1 : 0;
 }
