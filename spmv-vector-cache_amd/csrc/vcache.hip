@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
       return;
     }
     const uint32_t beg = beg_in != ~0u ? beg_in : segl[min(s, npad)];
-    if constexpr (CX == 4) {
+    if constexpr (CX == 4 || CX == 6) {
       // masked: a lane past the step's segment gets an out-of-range offset in
       // a descriptor of the unit's entries -- zero, and no memory request
       // (clamped lanes re-read the next segment: 1.1x the entry requests here,
@@ -283,10 +283,17 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     const uint32_t beg = segl[s], end = segl[s + 1];
     T acc[EPT];
     bool head[EPT];
+    // CX 6: a slot no lane of this wave holds an entry of (wave-uniform) issues none of its LDS reads
+    // (the ordered geometry's 512 lanes x 3 slots hold ~1000 entries per step: the third is empty)
+    const uint32_t wq0 = __builtin_amdgcn_readfirstlane(beg + (ct & ~63u));
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
       const uint32_t q = beg + ct + j * CT;
       head[j] = q < end && !(c[j] & kVcCont);
+      if (CX == 6 && wq0 + j * CT >= end) {
+        acc[j] = T(0);
+        continue;
+      }
       const uint32_t row = (c[j] >> 16) & 0x3FFF;
       const T xv = xs[head[j] ? (c[j] & 0xFFFF) : 0u], yv = ylds[head[j] ? row : 0u];
       acc[j] = madd(yv, v[j], xv);
