@@ -743,7 +743,7 @@ static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
   } else if (cx == 5) {  // (a banked layout: runs inside 16-lane rows)
     launch_one<T, SPLIT, 0, 5, MAP>(a, s);
   } else if (cx == 6) {  // the ordered geometry on a banked layout: CX 0 with the DPP first continuation
-    launch_one<T, SPLIT, 0, 6, MAP>(a, s);
+    ld == 1 ? launch_one<T, SPLIT, 1, 6, MAP>(a, s) : launch_one<T, SPLIT, 0, 6, MAP>(a, s);
   } else if (cx == 0) {
     ld == 1 ? launch_one<T, SPLIT, 1, 0, MAP>(a, s) : launch_one<T, SPLIT, 0, 0, MAP>(a, s);
   } else if (cx == 1) {

@@ -31,7 +31,9 @@ SETS = {
     # round 5: ORDERED's first run continuation by DPP (xlane 6, the default on banked layouts) against
     # re-reading it from memory (xlane 0)
     "ordered6": [("ordered (product)", "vcache", {}), ("ordered xlane 0", "vcache", {"vcache_xlane": 0}),
-                 ("ordered xlane 6", "vcache", {"vcache_xlane": 6})],
+                 ("ordered xlane 6", "vcache", {"vcache_xlane": 6}),
+                 ("ordered LDS-DMA x", "vcache", {"vcache_dma": 1}),
+                 ("ordered LDS-DMA x xlane 6", "vcache", {"vcache_dma": 1, "vcache_xlane": 6})],
     # round 5: k_vcache's four-part geometry (banked, LDS-DMA loaders, xlane 5, resident entries) against the
     # product; "v4:" a handle created with HIPSPMV_SPLIT4_VCACHE=1
     "split4": [("split (product)", "vcache_split", {}), ("vcache 4 parts", "v4:vcache_split4", {}),
