@@ -113,7 +113,9 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
  * cross-lane and padded loops with the compiler's own waits -- 2 and 3 keep
  * the DE-deep entry prefetch in flight across the loop header; 5 = 3 with the
  * first continuation step by DPP, for VCACHE_SPLIT layouts whose runs stay in
- * 16-lane rows -- the default there), "vcache_map"
+ * 16-lane rows -- the default there; 6 = VCACHE (ordered) on such a layout:
+ * the first continuation entry from the next lane by DPP, entry loads past a
+ * step masked -- the same bits, measured no faster), "vcache_map"
  * (1 = VCACHE_SPLIT4 places column part h on XCDs 2h and 2h+1, so each XCD's
  * L2 serves a quarter of x; experimental), "profile" (1 = VCACHE and
  * VCACHE_SPLIT launches run in their default configuration with in-kernel
@@ -155,7 +157,10 @@ int hipspmv_exec(hipspmv_t *h, const void *x, void *y, int beta, int mode);
  * handle's scratch (VCACHE_SPLIT, VCACHE_SPLIT4, SELL in FAST / u64 with hub
  * pieces) are ordered by the handle itself: such a launch waits, on the device,
  * for the previous one when that went to another stream (hipspmv_exec's
- * internal stream included). */
+ * internal stream included) -- the handle records its event on that previous
+ * stream at the switch, so a stream such a launch used must stay alive until the
+ * handle's next launch on another stream or its destruction.  Launches that
+ * stay on one stream record nothing between them. */
 int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void *d_y_out, int beta, int mode,
                         void *stream);
 

@@ -544,7 +544,10 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   DeviceGuard g(h->device);
   HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   for (auto& e : h->ev) HIP_TRY(hipEventCreate(&e));
-  HIP_TRY(hipEventCreateWithFlags(&h->scratch_ev, hipEventDisableTiming));
+  // device-scope only: the event orders two launches of this handle on one device, so its record
+  // needs no system-scope release (cache writeback) -- with one, every eager launch of a
+  // scratch-using kernel was followed by a ~6 us gap (profiles/r05/logs/gaps_*.log)
+  HIP_TRY(hipEventCreateWithFlags(&h->scratch_ev, hipEventDisableTiming | hipEventDisableSystemFence));
   for (uint32_t r = 0; r < a.rows; ++r) {
     const uint32_t len = a.rowptr[r + 1] - a.rowptr[r];
     h->max_row_len = len > h->max_row_len ? len : h->max_row_len;
@@ -773,8 +776,15 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (scratch) HIP_TRY(hipStreamIsCapturing(s, &cap));
   const bool capturing = cap != hipStreamCaptureStatusNone;
-  if (scratch && !capturing && h->scratch_used && h->scratch_stream != s)
+  // The event is recorded on the previous stream only now, when a launch
+  // comes on another one (everything enqueued there so far, the previous
+  // scratch launch included, precedes the record): a record after every
+  // launch put a barrier packet between back-to-back eager launches on one
+  // stream (~4.5 us gaps, profiles/r05/logs/gaps_*.log).
+  if (scratch && !capturing && h->scratch_used && h->scratch_stream != s) {
+    HIP_TRY(hipEventRecord(h->scratch_ev, h->scratch_stream));
     HIP_TRY(hipStreamWaitEvent(s, h->scratch_ev, 0));
+  }
   if (kernel == HIPSPMV_KERNEL_SELL) {
     const auto& q = h->sell;
     SellArgs a{q.d_off,     q.d_width,   q.d_row,     q.d_len, q.d_col,  q.d_vals,
@@ -865,7 +875,6 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   }
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
   if (scratch && !capturing) {
-    HIP_TRY(hipEventRecord(h->scratch_ev, s));
     h->scratch_stream = s;
     h->scratch_used = true;
   }

@@ -45,6 +45,9 @@ __device__ __forceinline__ void owner_combine(const T* ylds, uint32_t* scratch, 
   const u64x2* const yl2 = reinterpret_cast<const u64x2*>(ylds);
   const uint32_t npairs = (nr + 1) / 2;
   const __amdgpu_buffer_rsrc_t mine = buf_rsrc(partial + ((size_t)h * nblocks + b) * VRP, 8 * VRP);
+  // y written through (sc1) like the partials: the launch then ends with no dirty y lines in L2, so
+  // the next eager launch does not wait for their write-back at the kernel boundary
+  const __amdgpu_buffer_rsrc_t yr = buf_rsrc(y, 8 * nr);
   auto pair_of = [&](uint32_t q, int j) { return q * QP + (uint32_t)t + (uint32_t)j * VT; };
   auto in_share = [&](uint32_t q, int j) {
     return (QP % VT == 0 || (uint32_t)t + (uint32_t)j * VT < QP) && pair_of(q, j) < PAIRS;
@@ -76,9 +79,10 @@ __device__ __forceinline__ void owner_combine(const T* ylds, uint32_t* scratch, 
         a1 = a1 + __builtin_bit_cast(T, (uint64_t)v[o][j].y);
       }
       const uint32_t p = pair_of(q, j);
-      if (in_share(q, j)) {
-        if (2 * p < nr) y[2 * p] = a0;
-        if (2 * p + 1 < nr) y[2 * p + 1] = a1;
+      if (in_share(q, j)) {  // rows past nr fall outside the descriptor: no store
+        typedef unsigned int u32x2c __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2c, a0), yr, (int)(16 * p), 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2c, a1), yr, (int)(16 * p + 8), 0, 16);
       }
     }
   };
