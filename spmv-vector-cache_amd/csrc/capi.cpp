@@ -145,6 +145,8 @@ struct hipspmv_handle {
   // with the default policy (Infinity-Cache resident); 0 default: all non-temporal
   int64_t wcsr_res = 0;
   int wcsr_reduce = 0;    // option "wcsr_reduce": 0 the compact reduce over rows with segments, 1 every row
+  int wcsr_fill = -1;     // option "wcsr_fill": 1 the rows without segments written by the segment pass's
+                          // launch, 0 by the reduce's; -1 (default) 1 when two thirds of the rows are empty
   // option "sell_nt": SELL slices s >= sell_nt load their entries
   // non-temporally (-1 default: the second half of the slices)
   int64_t sell_nt = -1;
@@ -867,6 +869,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
       a.nebits = w.d_nebits;
       a.cgroups = w.d_cgroups;
       a.ncgroups = w.ncgroups;
+      a.fill_early = h->wcsr_fill >= 0 ? h->wcsr_fill : 3ull * (h->rows - w.nrows_ne) >= 2ull * h->rows;
     }
     e = launch_wcsr(h->dtype, a, s);
   } else {
@@ -1048,6 +1051,9 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "sell_nt") {  // first SELL slice whose entries load non-temporally (-1: half)
     if (value < -1 || value > (int64_t)UINT32_MAX) return HIPSPMV_ERR_INVALID_ARG;
     h->sell_nt = value;
+  } else if (k == "wcsr_fill") {  // 1: empty rows filled beside the segment pass; 0: after the reduce; -1: by rule
+    if (value < -1 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
+    h->wcsr_fill = (int)value;
   } else if (k == "wcsr_reduce") {  // 0: compact reduce over the rows with segments (default); 1: every row
     if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
     h->wcsr_reduce = (int)value;

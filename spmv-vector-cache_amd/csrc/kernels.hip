@@ -260,6 +260,35 @@ __global__ __launch_bounds__(256) void k_wpass(const uint32_t* __restrict__ rowp
     csr_vector_rows<T, 0>(rowptr, colind, vals, xv, out, groups[g], groups[g + 1], heads[w]);
 }
 
+// k_wpass_fill (wcsr segment pass, with the compact reduce): blocks below
+// nfill write the rows without segments (y_in or +0.0, from the bitmap), the
+// others run the segment pass's groups -- the streaming writes ride along
+// the gather-bound pass instead of following the reduce (option wcsr_fill;
+// the layout takes it when two thirds of the rows have no entry: C5 shard 7
+// 270.3 -> 264.7 us, shards 5 / 6 (60 / 49 % empty) 2-3 us slower with it,
+// fill blocks placed after the groups instead gained nothing;
+// profiles/r05/logs/c5_ab_fill_*.log)
+template <typename T>
+__global__ __launch_bounds__(256) void k_wpass_fill(const uint32_t* __restrict__ rowptr,
+                                                     const uint32_t* __restrict__ colind, const T* __restrict__ vals,
+                                                     const T* __restrict__ x, T* __restrict__ ypart,
+                                                     const uint32_t* __restrict__ groups, uint32_t ngroups,
+                                                     const uint32_t* __restrict__ nebits, const T* __restrict__ y_in,
+                                                     T* __restrict__ y_out, uint32_t rows, int beta, uint32_t nfill) {
+  if (blockIdx.x < nfill) {
+    const uint32_t stride = nfill * 256;
+    for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < rows; r += stride)
+      if (!((nebits[r >> 5] >> (r & 31)) & 1u)) y_out[r] = beta ? y_in[r] : T(0);
+    return;
+  }
+  __shared__ uint32_t heads[4][kCvGroupNnz / 32];
+  const int w = threadIdx.x >> 6;
+  const uint32_t g = (blockIdx.x - nfill) * 4 + w;
+  if (g >= ngroups) return;  // wave-uniform
+  csr_vector_rows<T, 1>(rowptr, colind, vals, [&](uint32_t c) { return x[c]; },
+                        RowOut<T>{(const T*)nullptr, ypart, 0}, groups[g], groups[g + 1], heads[w]);
+}
+
 // k_wreduce (wcsr): y[r] = (y_in[r] +) the sum of row r's segment partials
 // ypart[segidx[k]], k in [rowseg[r], rowseg[r+1]) (window order), over the
 // reduce's own balanced row groups -- a fixed order, so wcsr is
@@ -334,6 +363,12 @@ hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
   if (a.nchunks)
     hipLaunchKernelGGL(k_wseg<T>, dim3(a.nchunks), dim3(1024), 0, s, a.chunks, a.groups, a.seg_rowptr, a.seg_colind,
                        (const T*)a.seg_vals, (const T*)a.x, a.cols, (T*)a.ypart);
+  const bool fill_early = a.rrow && a.fill_early && !a.nchunks && !a.res_groups;
+  const uint32_t nfill = std::min((a.rows + 255) / 256, 1024u);
+  if (fill_early)
+    hipLaunchKernelGGL(k_wpass_fill<T>, dim3(nfill + (a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr,
+                       a.seg_colind, (const T*)a.seg_vals, (const T*)a.x, (T*)a.ypart, a.groups, a.ngroups, a.nebits,
+                       (const T*)a.y_in, (T*)a.y_out, a.rows, a.beta, nfill);
   else if (a.ngroups && a.res_groups)
     hipLaunchKernelGGL(k_wpass<T>, dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,
                        (const T*)a.seg_vals, (const T*)a.x, (T*)a.ypart, a.groups, a.ngroups, a.res_groups);
@@ -343,7 +378,7 @@ hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
                        a.groups, a.ngroups, 0);
   if (a.rrow) {
     // the fill: at most 1024 blocks, grid-stride (one block per 256 rows measured as a dispatch tail)
-    const uint32_t red = (a.ncgroups + 3) / 4, fill = std::min((a.rows + 255) / 256, 1024u);
+    const uint32_t red = (a.ncgroups + 3) / 4, fill = fill_early ? 0u : nfill;
     hipLaunchKernelGGL(k_wreduce_c<T>, dim3(red + fill), dim3(256), 0, s, a.rsegc, a.segidx, (const T*)a.ypart,
                        a.rrow, a.nebits, (const T*)a.y_in, (T*)a.y_out, a.cgroups, a.ncgroups, red, a.rows, a.beta);
   } else {

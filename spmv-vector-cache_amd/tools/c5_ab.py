@@ -20,6 +20,7 @@ import hipspmv as hs  # noqa: E402
 # settings: (label, {option: value or ("groups", fraction)})
 SETS = {
     "one": [("product", {})],
+    "fill": [("fill beside the segment pass", {"wcsr_fill": 1}), ("fill after the reduce", {"wcsr_fill": 0})],
     "reduce": [("compact reduce", {}), ("all-rows reduce", {"wcsr_reduce": 1})],
     "res": [("all nt (product)", {}), ("resident 1/8", {"wcsr_res": ("groups", 0.125)}),
             ("resident 1/4", {"wcsr_res": ("groups", 0.25)}), ("resident 3/8", {"wcsr_res": ("groups", 0.375)}),
@@ -55,7 +56,7 @@ def main():
 
         def reset(o):
             for k in o:
-                h.set_option(k, 0)
+                h.set_option(k, {"wcsr_fill": -1}.get(k, 0))
 
         def run(k):
             for _ in range(k):

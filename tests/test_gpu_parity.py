@@ -225,6 +225,12 @@ def test_wcsr_wide_windows(gpu, dtype):
     assert y1[empty].tobytes() == y0[empty].tobytes()
     y_zero = h.exec(x, y0.copy(), beta=0, mode=hs.MODE_FAST)
     assert np.all(y_zero[empty] == 0) and not np.signbit(y_zero[empty].astype(np.float64)).any()
+    # the empty rows written after the reduce (option wcsr_fill 0) or beside the segment pass (1)
+    for fill in (0, 1):
+        h.set_option("wcsr_fill", fill)
+        assert h.exec(x, y0.copy(), beta=1, mode=hs.MODE_FAST).tobytes() == y1.tobytes()
+        assert h.exec(x, y0.copy(), beta=0, mode=hs.MODE_FAST).tobytes() == y_zero.tobytes()
+    h.set_option("wcsr_fill", -1)
     # the all-rows reduce (option wcsr_reduce 1): also deterministic and within the bound
     h.set_option("wcsr_reduce", 1)
     for beta in (0, 1):
