@@ -195,6 +195,11 @@ def test_c5_multi_create_balanced_shards(gpu):
         for h, y in zip(hs_, ys):
             h.exec_device(xd, y, beta=0, mode=hs.MODE_FAST, stream=s)
     torch.cuda.synchronize()
+    # earlier tests' handles freed by the garbage collector inside a timed loop stall the host (hipFree
+    # synchronises the device) while the events keep counting: collect first, and not during the loops
+    import gc
+    gc.collect()
+    gc.disable()
     times = []
     for h, y in zip(hs_, ys):
         assert h.kernel_name(hs.MODE_FAST) == "wcsr"
@@ -205,6 +210,7 @@ def test_c5_multi_create_balanced_shards(gpu):
         e1.record(s)
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1) * 1e3 / 20)
+    gc.enable()
     rng = np.random.default_rng(0)
     for i, y in enumerate(ys):
         r0, r1 = int(bounds[i]), int(bounds[i + 1])
