@@ -159,8 +159,9 @@ int hipspmv_exec(hipspmv_t *h, const void *x, void *y, int beta, int mode);
  * for the previous one when that went to another stream (hipspmv_exec's
  * internal stream included) -- the handle records its event on that previous
  * stream at the switch, so a stream such a launch used must stay alive until the
- * handle's next launch on another stream or its destruction.  Launches that
- * stay on one stream record nothing between them. */
+ * handle's next launch on another stream or its destruction (hipspmv_exec
+ * synchronises the device instead).  Launches that stay on one stream record
+ * nothing between them. */
 int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void *d_y_out, int beta, int mode,
                         void *stream);
 

@@ -1102,6 +1102,13 @@ int hipspmv_exec(hipspmv_t* h, const void* x, void* y, int beta, int mode) {
       h->device_bytes += by;
     }
     hipStream_t s = h->stream;
+    // the synchronous path orders itself after a device-resident launch on a
+    // caller's stream by a device synchronisation, not by recording on that
+    // stream (which the caller may have destroyed since)
+    if (h->scratch_used && h->scratch_stream != s) {
+      HIP_TRY(hipDeviceSynchronize());
+      h->scratch_stream = s;
+    }
     HIP_TRY(hipEventRecord(h->ev[0], s));
     HIP_TRY(hipMemcpyAsync(h->d_x, x, bx, hipMemcpyHostToDevice, s));
     if (beta) HIP_TRY(hipMemcpyAsync(h->d_y, y, by, hipMemcpyHostToDevice, s));
