@@ -28,6 +28,11 @@ SETS = {
     # round 5: the ORDERED loaders skipping the x lines no entry of a panel uses (option vcache_xmask)
     "xmask": [("ordered (product: xmask)", "vcache", {}), ("ordered xmask off", "vcache", {"vcache_xmask": 0}),
               ("ordered row order xmask", "bank0:vcache", {})],
+    # round 5: ORDERED with 1/4 .. 3/4 of its row blocks' entries Infinity-Cache resident (256 blocks)
+    "ordered_res": [("ordered (product: 1/2)", "vcache", {}), ("ordered resident 1/4", "vcache", {"vcache_nt": 64}),
+                    ("ordered resident 3/8", "vcache", {"vcache_nt": 96}),
+                    ("ordered resident 5/8", "vcache", {"vcache_nt": 160}),
+                    ("ordered resident 3/4", "vcache", {"vcache_nt": 192}), ("ordered all nt", "vcache", {"vcache_nt": 0})],
     # round 5: ORDERED's first run continuation by DPP (xlane 6, the default on banked layouts) against
     # re-reading it from memory (xlane 0)
     "ordered6": [("ordered (product)", "vcache", {}), ("ordered xlane 0", "vcache", {"vcache_xlane": 0}),
@@ -133,7 +138,7 @@ def main():
         for k in opts:
             cur[0].set_option(k, {"vquad_variant": 0, "vcache_nt": -1, "vcache_map": 0, "vcache_xmask": 1}.get(k, -1))
 
-    mode = hs.MODE_ORDERED if a.set in ("ordered", "xmask", "ordered6") else hs.MODE_FAST
+    mode = hs.MODE_ORDERED if a.set in ("ordered", "xmask", "ordered6", "ordered_res") else hs.MODE_FAST
 
     def run(k):
         for _ in range(k):
