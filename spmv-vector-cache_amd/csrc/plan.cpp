@@ -1074,17 +1074,20 @@ void build_xmask(const VcacheLayout& L, uint32_t WL, std::vector<uint64_t>& out)
   const uint32_t units = L.nblocks * (uint32_t)L.geom.split, P = L.npanels, stride = L.npad + 1;
   const uint32_t cmask = (1u << L.geom.colbits) - 1u, lines_per_j = 8 * WL;
   out.assign((size_t)units * P * WL, 0ull);
-  par_chunks(units, plan_threads(), [&](unsigned, uint64_t lo, uint64_t hi) {
-   for (uint64_t u = lo; u < hi; ++u) {
+  auto unit = [&](uint64_t u) {
     const uint32_t* sp = L.seg.data() + (size_t)u * stride;
     for (uint32_t s = 0; s < P && s < stride - 1; ++s) {
       uint64_t* w = out.data() + ((size_t)u * P + s) * WL;
       for (uint32_t e = sp[s]; e < sp[s + 1]; ++e) {
+        // lines past 64 bits of a wave's word have no bit: the kernel applies the mask only where
+        // every line has one (k_vcache XMASK: NJ * 8 <= 64)
         const uint32_t line = (L.code[e] & cmask) >> 4, j = line / lines_per_j, r = line % lines_per_j;
         if (j < 8) w[r / 8] |= 1ull << (j * 8 + r % 8);
       }
     }
-   }
+  };
+  par_chunks(units, plan_threads(), [&](unsigned, uint64_t lo, uint64_t hi) {
+    for (uint64_t u = lo; u < hi; ++u) unit(u);
   });
 }
 
