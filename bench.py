@@ -97,6 +97,9 @@ def parse():
     p.add_argument("--strong-scale", type=int, default=24, help="log2 of the strong block's matrix dimension (C4: 24)")
     p.add_argument("--no-c5-shards", action="store_true",
                    help="c3 at N=1: skip the C5 per-shard block (every shard of the 8-way partition timed on this GPU)")
+    p.add_argument("--no-c4-shards", action="store_true",
+                   help="skip timing C4 shards alone at N=1 (the c4_shards block)")
+    p.add_argument("--c4-shards", default="0,7", help="which of the 8 C4 shards the c4_shards block times")
     p.add_argument("--c5-scale", type=int, default=24, help="log2 of the C5 block's R-MAT dimension (C5: 24)")
     p.add_argument("--c5-parts", type=int, default=8)
     p.add_argument("--c5-partition", default="cost", choices=["cost", "nnz"],
@@ -526,9 +529,18 @@ def run_strong(a, dist, dev, local: int, rank: int, world: int, stream) -> dict:
     setup_ns = h.stat("setup_ns")
     phases = {k: h.stat(f"setup_{k}_ns") for k in ("csr", "upload", "scan", "layouts")}
     h.close()
-    del xd, yd
+    hs.release_wait()
+    del yd
     torch.cuda.empty_cache()
-    return {"workload": f"C4 stripe-uniform CSR {n}x{n}, {k} nnz/row, {world} equal row blocks (rows of rank 0: "
+    c4_shards = None
+    if world == 1 and not a.no_c4_shards:
+        try:
+            c4_shards = run_c4_shards(a, rowptr, colind, vals, n, xd, dev, stream)
+        except Exception as e:  # reported, never fatal
+            c4_shards = {"error": f"{type(e).__name__}: {e}"}
+    del xd
+    torch.cuda.empty_cache()
+    return c4_shards, {"workload": f"C4 stripe-uniform CSR {n}x{n}, {k} nnz/row, {world} equal row blocks (rows of rank 0: "
                         f"[{row0},{row1}))", "scaling": "strong", "mode": "fast", "kernel": kname,
             "value": round(2.0 * nnz_total / (ms * 1e-3) / 1e9, 2), "unit": "GFLOP/s", "ms_per_step": round(ms, 5),
             "nnz_total": nnz_total, "rows_per_rank": rows,
@@ -538,6 +550,55 @@ def run_strong(a, dist, dev, local: int, rank: int, world: int, stream) -> dict:
             "alg_bytes_rank0": alg, "x_bcast_us": None if bcast_us is None else round(bcast_us, 2),
             "rank_parity": parities, "gen_s": round(gen_s, 3), "setup_s": round(setup_s, 3),
             "setup_ns_lib": setup_ns, "setup_phases_ns": phases}
+
+
+def time_shard(a, h, x, y, stream, steps: int) -> float:
+    """Per-launch microseconds of `steps` back-to-back FAST launches after 3 untimed ones, HIP events on
+    the launch stream (the C4 / C5 shard blocks)."""
+    for _ in range(3):
+        h.exec_device(x, y, beta=0, mode=hs.MODE_FAST, stream=stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        h.exec_device(x, y, beta=0, mode=hs.MODE_FAST, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / steps
+
+
+def run_c4_shards(a, rowptr, colind, vals, n: int, x, dev, stream) -> dict:
+    """shards 0 and 7 (--c4-shards) of the library's 8-way partition of C4
+    (hipspmv_partition_rows on the full matrix the strong block just ran), each created and timed alone
+    on this GPU like the C5 shards: AUTO's FAST kernel, --c5-steps launches, per-shard roofline
+    fraction, sampled rows against the oracle -- the per-GPU compute time of an 8-GPU C4 step."""
+    parts = 8
+    bounds = hs.partition_rows_cost(rowptr, colind, n, parts)
+    shards = []
+    for r in (int(v) for v in a.c4_shards.split(",")):
+        row0, row1 = int(bounds[r]), int(bounds[r + 1])
+        rp, ci, va = csr_slice(rowptr, colind, vals, row0, row1)
+        ts = time.perf_counter()
+        h = hs.Handle.from_csr(rp, ci, va, row1 - row0, n, device=dev.index or 0)
+        setup_s = time.perf_counter() - ts
+        y = torch.empty(row1 - row0, dtype=torch.float64, device=dev)
+        kname = h.kernel_name(hs.MODE_FAST)
+        us = time_shard(a, h, x, y, stream, a.c5_steps)
+        alg = h.stat("alg_bytes")
+        parity = shard_parity(rp, ci, va, x.cpu().numpy(), y.cpu().numpy(), hs.MODE_FAST, sample_rows(rp, 200, seed=r))
+        shards.append({"shard": r, "rows": [row0, row1], "nnz": int(ci.size), "kernel": kname,
+                       "kernel_us": round(us, 3), "roofline_frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                       "alg_bytes": alg, "parity": parity, "setup_s": round(setup_s, 2)})
+        h.close()
+        hs.release_wait()
+        del y
+        torch.cuda.empty_cache()
+    return {"workload": f"C4 stripe-uniform CSR {n}x{n}, 32 nnz/row, {parts} row shards (library "
+                        f"hipspmv_partition_rows partition), shards {a.c4_shards} each run alone on this GPU",
+            "mode": "fast", "steps": a.c5_steps, "shards": shards,
+            "min_roofline_frac": min(s["roofline_frac"] for s in shards),
+            "slowest_us": max(s["kernel_us"] for s in shards),
+            "note": "x (all 2^24 columns) replicated per GPU; the per-GPU compute time of one 8-GPU C4 step"}
 
 
 def c5_matrix(scale: int, parts: int, model: str):
@@ -585,16 +646,7 @@ def run_c5_shards(a, dev, stream) -> dict:
         setup_s = time.perf_counter() - ts
         y = torch.empty(row1 - row0, dtype=torch.float64, device=dev)
         kname = h.kernel_name(hs.MODE_FAST)
-        for _ in range(3):
-            h.exec_device(x, y, beta=0, mode=hs.MODE_FAST, stream=stream)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(a.c5_steps):
-            h.exec_device(x, y, beta=0, mode=hs.MODE_FAST, stream=stream)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / a.c5_steps
+        us = time_shard(a, h, x, y, stream, a.c5_steps)
         alg = h.stat("alg_bytes")
         parity = shard_parity(rowptr, colind, vals, x.cpu().numpy(), y.cpu().numpy(), hs.MODE_FAST,
                               sample_rows(rowptr, 200, seed=r))
@@ -604,6 +656,7 @@ def run_c5_shards(a, dev, stream) -> dict:
                        "parity": parity, "setup_s": round(setup_s, 2)})
         total_nnz += int(colind.size)
         h.close()
+        hs.release_wait()
         del y
         torch.cuda.empty_cache()
     del full_rowptr, full_colind, full_vals
@@ -766,6 +819,8 @@ def main():
     wall_max, kern_ms, rank_kern_ms = timed(mode)
     y_main = yd.cpu().numpy().copy()
     launch_us = per_launch_us(mode)
+    # entry bytes the headline launches left in the Infinity Cache for the next one (default cache policy)
+    resident_bytes = h.stat("resident_entry_bytes")
     if a.rocprof_child:  # only the SpMV kernel in the profiler's table
         copy_gbs, read_gbs, copy_src, h2d_us, d2h_us = 0.0, None, None, 0.0, 0.0
     else:
@@ -795,6 +850,27 @@ def main():
             secondary = {"mode": other, "error": str(e)}
             y_other = None
 
+    # the same-run control: the headline kernel with every entry loaded
+    # non-temporally (option vcache_nt 0: nothing left resident between launches), K launches
+    # after W, HIP events on the launch stream -- the share of the headline the Infinity Cache gives
+    no_res = None
+    if resident_bytes and kname in ("vcache_split", "vcache", "wgather") and not a.rocprof_child:
+        h.set_option("vcache_nt", 0)
+        for _ in range(a.warmup):
+            h.exec_device(xd, yd, beta=0, mode=mode, stream=stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(a.steps):
+            h.exec_device(xd, yd, beta=0, mode=mode, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        nres_us = e0.elapsed_time(e1) * 1e3 / a.steps
+        h.set_option("vcache_nt", -1)
+        no_res = {"kernel_us_no_residency": round(nres_us, 3),
+                  "frac_no_residency": round(h.stat("alg_bytes") / (nres_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                  "no_residency_control": (f"{a.steps} launches after {a.warmup} with option vcache_nt 0 (every "
+                                           "entry non-temporal), HIP events on the launch stream, this run")}
+
     traffic, traffic_src = None, None
     ksub = ("k_vquad" if kname == "vcache_split4" else "k_vcache" if "vcache" in kname else ["k_csr_vector<double, true>", "k_wreduce"] if kname == "wcsr"
             else "k_" + kname)
@@ -821,9 +897,10 @@ def main():
 
     # C4 strong-scaling block beside the weak-scaled C3 headline
     strong = None
+    c4_shards = None
     if a.workload == "c3" and not a.no_strong and not a.rocprof_child:
         try:
-            strong = run_strong(a, dist, dev, local, rank, world, stream)
+            c4_shards, strong = run_strong(a, dist, dev, local, rank, world, stream)
         except Exception as e:  # reported, never fatal for the headline line
             strong = {"error": f"{type(e).__name__}: {e}"}
 
@@ -911,7 +988,11 @@ def main():
                          "frac_of_measured_copy": round(achieved / copy_gbs, 4) if copy_gbs > 0 else None,
                          "measured_read_gbs": None if not read_gbs else round(read_gbs, 1),
                          "frac_of_measured_read": round(achieved / read_gbs, 4) if read_gbs else None,
-                         "measured_source": copy_src},
+                         "measured_source": copy_src,
+                         # entries left in the 256 MiB Infinity Cache between launches (the library's
+                         # default: ~192 MiB of a vcache layout); the control below loads none that way
+                         "resident_entry_bytes": resident_bytes,
+                         **(no_res or {})},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,
             "parity": parity,
@@ -934,6 +1015,7 @@ def main():
             "rank_kernel_us": [round(v * 1e3, 3) for v in rank_kern_ms],
             "rank_parity": rank_parity,
             "strong": strong,
+            "c4_shards": c4_shards,
             "c5_shards": c5,
             # host time to generate the synthetic shard / to build the handle (transpose-free CSR
             # create: validation, upload, every layout AUTO runs); setup_ns_lib: the library's own

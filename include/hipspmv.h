@@ -153,15 +153,17 @@ int hipspmv_exec(hipspmv_t *h, const void *x, void *y, int beta, int mode);
  * stream, as in every HIP API) and returns without synchronising.  d_y_in may
  * equal d_y_out and is ignored for beta == 0.  Concurrency: a handle is used
  * from one host thread at a time.  Launches of one handle on different streams
- * may be in flight together; the kernels that combine column parts through the
- * handle's scratch (VCACHE_SPLIT, VCACHE_SPLIT4, SELL in FAST / u64 with hub
- * pieces) are ordered by the handle itself: such a launch waits, on the device,
- * for the previous one when that went to another stream (hipspmv_exec's
- * internal stream included) -- the handle records its event on that previous
- * stream at the switch, so a stream such a launch used must stay alive until the
- * handle's next launch on another stream or its destruction (hipspmv_exec
- * synchronises the device instead).  Launches that stay on one stream record
- * nothing between them. */
+ * may be in flight together: the kernels that combine partial sums through
+ * scratch memory (VCACHE_SPLIT, VCACHE_SPLIT4, WCSR, SELL in FAST / u64 with
+ * hub pieces) get one scratch set per stream (told apart by the stream value;
+ * hipspmv_exec's internal stream has its own), so launches on different streams
+ * share nothing and the handle records or waits on nothing between launches --
+ * a stream may be destroyed right after its last launch.  Up to four streams
+ * keep their sets; a fifth takes over the least recently used set after a
+ * device synchronisation (stat "scratch_evictions").  Inside a stream capture
+ * nothing is allocated or synchronised: the captured launch uses the capturing
+ * stream's set if a launch on that stream made one, else the first set, and the
+ * caller orders a graph's replays against the handle's other launches. */
 int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void *d_y_out, int beta, int mode,
                         void *stream);
 
@@ -180,6 +182,11 @@ int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void 
  * "sell_padding" "sell_iso_hubs" (SELL layout, 0 until the sell kernel is
  * selected) "wcsr_segments" "wcsr_max_segment" "wcsr_window_log2"
  * "wcsr_chunks" (wcsr layout)
+ * "resident_entry_bytes" (entry bytes the last launch loaded with the default
+ * cache policy, which may stay in the Infinity Cache until the next launch;
+ * the rest load non-temporally: options vcache_nt / sell_nt)
+ * "scratch_streams" "scratch_evictions" (per-stream combine scratch sets, see
+ * hipspmv_exec_device)
  * "max_row_len" "empty_rows" "execs" "handoff_fallbacks" (VCACHE_SPLIT4
  * combine owners that gave up waiting, since create); the reference accelerator's cache
  * statistics for the last launch: "total_cycles" "active_cycles" "read_misses"
@@ -210,7 +217,18 @@ int hipspmv_attach_pmc(hipspmv_t *h, const char *csv_path);
 /* Name of the kernel that HIPSPMV_MODE `mode` would run (static string). */
 const char *hipspmv_kernel_name(hipspmv_t *h, int mode);
 
+/* Replaces the HardwareSpMV destructor (software/HardwareSpMV.cpp:27).
+ * Returns at once: the handle's device memory, events and stream are released
+ * by the library's release thread once the device has finished the work
+ * submitted before this call (launches of the handle on any stream, destroyed
+ * streams included), so destroying a handle never makes the calling thread
+ * wait for the device (hipFree would: an implicit device synchronisation).
+ * The handle pointer is invalid on return. */
 int hipspmv_destroy(hipspmv_t *h);
+
+/* Blocks until every release queued by hipspmv_destroy / hipspmv_multi_destroy
+ * so far has completed (the memory is back with the device allocator). */
+int hipspmv_release_wait(void);
 
 /* Matrix preprocessing statistics on the GPU.  Replaces
  * SoftwareSpMV::measurePreprocessingTimes (software/SoftwareSpMV.cpp:72-95)

@@ -7,12 +7,16 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <deque>
 #include <fstream>
+#include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 
 #include "hipspmv.h"
 #include "hipspmv_internal.h"
@@ -63,9 +67,94 @@ uint64_t now_ns() {
       .count();
 }
 
+// Deferred release: hipFree waits for the whole device
+// (an implicit hipDeviceSynchronize), so a destroy on the caller's thread
+// stalled every launch that thread had queued behind it -- a garbage-collected
+// handle inside a timed loop reads as one 1.6 ms launch.  A
+// destroyed handle's buffers, events and stream go to this thread instead: it
+// waits for the device there (every launch submitted before the destroy,
+// on any stream, live or destroyed since, has then finished) and frees them.
+// The caller's thread never waits.  Drained at process exit (the object is
+// constructed after the HIP runtime, so it is destroyed before it).
+class Reclaimer {
+ public:
+  struct Item {
+    int device = 0;
+    std::vector<void*> ptrs;
+    std::vector<hipEvent_t> events;
+    std::vector<hipStream_t> streams;
+  };
+  static Reclaimer& get() {
+    static Reclaimer r;
+    return r;
+  }
+  void push(Item it) {
+    std::unique_lock<std::mutex> lk(m_);
+    if (!th_.joinable()) th_ = std::thread([this] { run(); });
+    q_.push_back(std::move(it));
+    ++queued_;
+    cv_.notify_all();
+  }
+  // until everything pushed so far is released
+  void wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    const uint64_t target = queued_;
+    done_cv_.wait(lk, [&] { return released_ >= target; });
+  }
+  ~Reclaimer() {
+    {
+      std::unique_lock<std::mutex> lk(m_);
+      stop_ = true;
+      cv_.notify_all();
+    }
+    if (th_.joinable()) th_.join();
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      Item it;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;  // stop_ and drained
+        it = std::move(q_.front());
+        q_.pop_front();
+      }
+      (void)hipSetDevice(it.device);
+      (void)hipDeviceSynchronize();  // this thread only
+      for (void* p : it.ptrs)
+        if (p) (void)hipFree(p);
+      for (hipEvent_t e : it.events)
+        if (e) (void)hipEventDestroy(e);
+      for (hipStream_t s : it.streams)
+        if (s) (void)hipStreamDestroy(s);
+      std::unique_lock<std::mutex> lk(m_);
+      ++released_;
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  std::deque<Item> q_;
+  std::thread th_;
+  uint64_t queued_ = 0, released_ = 0;
+  bool stop_ = false;
+};
+
 }  // namespace
 
 void hipspmv::set_last_error(const std::string& what) { g_last_error = what; }
+
+void hipspmv::defer_release(int device, std::vector<void*> ptrs, std::vector<void*> events,
+                            std::vector<void*> streams) {
+  Reclaimer::Item it;
+  it.device = device;
+  it.ptrs = std::move(ptrs);
+  for (void* e : events) it.events.push_back(static_cast<hipEvent_t>(e));
+  for (void* s : streams) it.streams.push_back(static_cast<hipStream_t>(s));
+  Reclaimer::get().push(std::move(it));
+}
 
 struct hipspmv_handle {
   int device = 0, dtype = HIPSPMV_F64;
@@ -81,6 +170,8 @@ struct hipspmv_handle {
     uint64_t* d_xmask = nullptr;  // [0] ordered: the x lines each unit's panels use (build_xmask)
     uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, part_panels = 0, npad = 0, max_seg = 0, max_run = 0;
     uint64_t n_cont = 0;
+    uint64_t ticket_words = 0, partial_bytes = 0;  // the combine scratch of one stream (split geometries)
+    std::vector<uint32_t> block_first;  // nblocks + 1: first entry of each row block (last: nnz)
     int split = 1;
     bool row_runs = false;  // place_segments_banked: runs inside 16-lane rows (xlane 5 applies)
     bool vc4 = false;       // [2] built for k_vcache's four-part geometry (HIPSPMV_SPLIT4_VCACHE=1), not k_vquad
@@ -102,8 +193,9 @@ struct hipspmv_handle {
     uint32_t *d_width = nullptr, *d_row = nullptr, *d_len = nullptr, *d_col = nullptr, *d_hubs = nullptr;
     uint32_t *d_pieces = nullptr, *d_tickets = nullptr;
     uint64_t *d_vals = nullptr, *d_partial = nullptr;
-    uint32_t nslices = 0, nhubs = 0, npieces = 0, niso = 0;
+    uint32_t nslices = 0, nhubs = 0, npieces = 0, niso = 0, ntickets = 0;
     uint64_t padding = 0;
+    std::vector<uint64_t> off;  // nslices + 1: first (padded) entry of each slice, on the host
   } sell;
   uint64_t wc_segments = 0;  // segments the wcsr layout would have (counted at create for wide x, else 0)
   struct Wc {  // wcsr: the column-windowed segment matrix (built when AUTO picks it, else on first selection)
@@ -114,6 +206,7 @@ struct hipspmv_handle {
     uint32_t *d_rrow = nullptr, *d_rsegc = nullptr, *d_cgroups = nullptr, *d_nebits = nullptr;
     uint64_t *d_vals = nullptr, *d_ypart = nullptr;
     uint32_t nseg = 0, ngroups = 0, rgroups = 0, ncgroups = 0, nrows_ne = 0, max_seg = 0, log2w = 0, nchunks = 0;
+    std::vector<uint32_t> group_first;  // ngroups + 1: first entry of each segment-pass group (host)
   } wc;
   int vcache_dma = -1;   // option "vcache_dma": LDS-DMA x loader (-1 default: on for the split geometry)
   int vcache_xlane = -1;  // option "vcache_xlane": run continuation form (-1 default: cross-lane for split)
@@ -166,15 +259,39 @@ struct hipspmv_handle {
   uint32_t max_row_len = 0, empty_rows = 0;
   int clock_khz = 0;  // shader clock (hipDeviceAttributeClockRate), for the cycle statistics
   int last_kernel = 0;
+  // bytes of the last launch's entry stream loaded with the default cache policy (they may stay in
+  // the Infinity Cache until the next launch; the rest load non-temporally): stat "resident_entry_bytes"
+  uint64_t resident_entry_bytes = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool pending = false;  // kernel events recorded by exec_device, not yet read
-  // The column-part combine scratch (vcache_split/split4 tickets + partials,
-  // SELL FAST hub-piece tickets + partials) is one per handle: a launch that
-  // uses it is ordered after the previous such launch when that one went to
-  // another stream (device-side wait on scratch_ev, no host synchronisation).
-  hipEvent_t scratch_ev = nullptr;
-  hipStream_t scratch_stream = nullptr;
-  bool scratch_used = false;
+  // The combine scratch (vcache_split/split4 tickets + partials, SELL FAST
+  // hub-piece tickets + partials, wcsr segment partials) is one set per stream
+  // (VERDICT r05 item 6): launches on different streams share none of it, so
+  // the handle orders nothing across streams and records nothing on a
+  // caller's stream -- a stream may be destroyed right after its last launch.
+  // Set 0 is the layouts' own buffers, claimed by the first stream that
+  // launches; sets 1.. are allocated on a stream's first launch of a kind
+  // (zeroed on that stream, ahead of it).  Beyond kScratchSets streams the
+  // least recently used set is taken over after a device synchronisation.
+  // Streams are told apart by their handle value (hipStreamGetId is newer
+  // than the HIP runtime PyTorch ships): a destroyed stream's value can come
+  // back for a new stream only once the queue is gone, and HIP deletes a queue
+  // after the work queued on it (hipStreamDestroy waits for it on ROCm --
+  // checked by tests/test_gpu_streams.py), so a set is never shared by two
+  // launches in flight.
+  static constexpr int kScratchSets = 4;
+  struct Scratch {
+    bool assigned = false;
+    uintptr_t sid = 0;  // the stream's handle value (NULL: the default stream)
+    uint64_t last = 0;  // LRU tick
+    uint32_t* vc_tickets[3] = {nullptr, nullptr, nullptr};
+    uint64_t* vc_partial[3] = {nullptr, nullptr, nullptr};
+    uint32_t* sell_tickets = nullptr;
+    uint64_t* sell_partial = nullptr;
+    uint64_t* wc_ypart = nullptr;
+  } scratch[kScratchSets];
+  uint64_t scratch_tick = 0, scratch_evictions = 0;
+  uint32_t* prof_tickets = nullptr;  // the tickets buffer the last profiled split launch stamped
   // option "profile" (DESIGN.md §6.9): vcache / vcache_split launches run with
   // the kernel's profile stamps; the NewCache state statistics come from them
   int profile = 0;
@@ -188,35 +305,33 @@ struct hipspmv_handle {
   } prof;
 };
 
+// Everything the handle owns on the device goes to the release thread
+// (defer_release): the caller's thread does not wait for the device.
 static void release(hipspmv_t* h) {
   if (!h) return;
-  DeviceGuard g(h->device);
-  void* ptrs[] = {h->d_rowptr, h->d_colind, h->d_groups, h->d_vals, h->d_x, h->d_y, h->d_prof, h->d_status};
-  for (void* p : ptrs)
-    if (p) (void)hipFree(p);
-  for (auto& v : h->vc) {
-    void* vp[] = {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial, v.d_xmask};
-    for (void* p : vp)
-      if (p) (void)hipFree(p);
-  }
+  std::vector<void*> ptrs = {h->d_rowptr, h->d_colind, h->d_groups, h->d_vals, h->d_x, h->d_y, h->d_prof, h->d_status};
+  for (auto& v : h->vc) ptrs.insert(ptrs.end(), {v.d_seg, v.d_code, v.d_tickets, v.d_vals, v.d_partial, v.d_xmask});
   {
     auto& q = h->sell;
-    void* sp[] = {q.d_off, q.d_width, q.d_row, q.d_len, q.d_col, q.d_hubs, q.d_vals, q.d_pieces, q.d_tickets,
-                  q.d_partial};
-    for (void* p : sp)
-      if (p) (void)hipFree(p);
+    ptrs.insert(ptrs.end(), {q.d_off, q.d_width, q.d_row, q.d_len, q.d_col, q.d_hubs, q.d_vals, q.d_pieces,
+                             q.d_tickets, q.d_partial});
   }
   {
     auto& w = h->wc;
-    void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart,
-                  w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits};
-    for (void* p : wp)
-      if (p) (void)hipFree(p);
+    ptrs.insert(ptrs.end(), {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks,
+                             w.d_vals, w.d_ypart, w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits});
   }
-  for (hipEvent_t e : h->ev)
-    if (e) (void)hipEventDestroy(e);
-  if (h->scratch_ev) (void)hipEventDestroy(h->scratch_ev);
-  if (h->stream) (void)hipStreamDestroy(h->stream);
+  for (int i = 1; i < hipspmv_handle::kScratchSets; ++i) {  // set 0 is the layouts' own (above)
+    auto& c = h->scratch[i];
+    for (int k = 0; k < 3; ++k) ptrs.insert(ptrs.end(), {c.vc_tickets[k], c.vc_partial[k]});
+    ptrs.insert(ptrs.end(), {c.sell_tickets, c.sell_partial, c.wc_ypart});
+  }
+  std::vector<void*> evs;
+  for (hipEvent_t e : h->ev) evs.push_back(e);
+  try {
+    defer_release(h->device, std::move(ptrs), std::move(evs), {h->stream});
+  } catch (...) {  // host OOM while queueing: the device memory leaks, nothing is freed under a live launch
+  }
   delete h;
 }
 
@@ -256,6 +371,8 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
   v.max_run = L.max_run;
   v.n_cont = L.n_cont;
   v.row_runs = L.row_runs;
+  v.block_first.assign(L.nblocks + 1, (uint32_t)L.code.size());
+  for (uint32_t b = 0; b < L.nblocks; ++b) v.block_first[b] = L.seg[(size_t)b * L.geom.split * (L.npad + 1)];
   auto fail = [&](int st) {
     free_vc(h, k);
     h->device_bytes = bytes0;
@@ -282,6 +399,8 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
     const hipError_t e = hipMalloc(reinterpret_cast<void**>(&v.d_partial), pbytes);
     if (e != hipSuccess) return fail(hip_fail(e, "hipMalloc(partials)"));
     h->device_bytes += pbytes;
+    v.ticket_words = zeros.size();
+    v.partial_bytes = pbytes;
   }
   v.ok = true;
   return HIPSPMV_OK;
@@ -372,6 +491,8 @@ static int build_sell_layout(hipspmv_t* h, const HostCSR& a) {
     if ((st = dev_upload(&q.d_partial, none.data(), none.size(), h->device_bytes))) return fail(st);
   }
   q.npieces = L.npieces;
+  q.ntickets = L.ntickets;
+  q.off = L.off;
   q.nslices = L.nslices;
   q.nhubs = L.nhubs;
   q.niso = L.niso;
@@ -481,6 +602,8 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   }
   w.nseg = L.nseg;
   w.ngroups = (uint32_t)groups.size() - 1;
+  w.group_first.resize(groups.size());
+  for (size_t g = 0; g < groups.size(); ++g) w.group_first[g] = L.seg.rowptr[groups[g]];
   w.max_seg = L.max_seg;
   w.log2w = L.log2w;
   w.built = true;
@@ -546,10 +669,6 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   DeviceGuard g(h->device);
   HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   for (auto& e : h->ev) HIP_TRY(hipEventCreate(&e));
-  // device-scope only: the event orders two launches of this handle on one device, so its record
-  // needs no system-scope release (cache writeback) -- with one, every eager launch of a
-  // scratch-using kernel was followed by a ~6 us gap (profiles/r05/logs/gaps_*.log)
-  HIP_TRY(hipEventCreateWithFlags(&h->scratch_ev, hipEventDisableTiming | hipEventDisableSystemFence));
   for (uint32_t r = 0; r < a.rows; ++r) {
     const uint32_t len = a.rowptr[r + 1] - a.rowptr[r];
     h->max_row_len = len > h->max_row_len ? len : h->max_row_len;
@@ -762,6 +881,82 @@ static uint32_t resident_blocks(uint32_t nblocks, uint64_t nnz) {
   return (uint32_t)((double)nblocks * (double)kVcResidentBytes / entry_bytes);
 }
 
+// Set 0 of the combine scratch: the buffers the layouts allocated.
+static void scratch_set0(hipspmv_t* h) {
+  auto& c = h->scratch[0];
+  for (int k = 0; k < 3; ++k) {
+    c.vc_tickets[k] = h->vc[k].d_tickets;
+    c.vc_partial[k] = h->vc[k].d_partial;
+  }
+  c.sell_tickets = h->sell.d_tickets;
+  c.sell_partial = h->sell.d_partial;
+  c.wc_ypart = h->wc.d_ypart;
+}
+
+// The combine scratch of stream s for a launch of `kernel` (vc layout k):
+// *out points at a set whose buffers for that kernel exist.  A capturing
+// stream takes its own set when it has one with those buffers (a warm-up
+// launch on it made them), else set 0 -- nothing is allocated or
+// synchronised inside a capture; the caller orders a graph's replays against
+// other launches of the handle (include/hipspmv.h).
+static int scratch_for(hipspmv_t* h, hipStream_t s, bool capturing, int kernel, int k,
+                       hipspmv_handle::Scratch** out) {
+  scratch_set0(h);  // (layouts built since the last launch)
+  const uintptr_t sid = (uintptr_t)s;
+  auto has = [&](const hipspmv_handle::Scratch& c) {
+    if (kernel == HIPSPMV_KERNEL_SELL) return c.sell_tickets && c.sell_partial;
+    if (kernel == HIPSPMV_KERNEL_WCSR) return c.wc_ypart != nullptr;
+    return c.vc_tickets[k] && c.vc_partial[k];
+  };
+  constexpr int NS = hipspmv_handle::kScratchSets;
+  int si = -1;
+  for (int i = 0; i < NS; ++i)
+    if (h->scratch[i].assigned && h->scratch[i].sid == sid) si = i;
+  if (capturing) {
+    if (si < 0 || !has(h->scratch[si])) si = 0;
+    if (!h->scratch[si].assigned) {
+      h->scratch[si].assigned = true;
+      h->scratch[si].sid = sid;
+    }
+  } else if (si < 0) {
+    for (int i = 0; i < NS && si < 0; ++i)
+      if (!h->scratch[i].assigned) si = i;
+    if (si < 0) {  // a fifth stream: the least recently used set, once its launches have finished
+      si = 0;
+      for (int i = 1; i < NS; ++i)
+        if (h->scratch[i].last < h->scratch[si].last) si = i;
+      HIP_TRY(hipDeviceSynchronize());
+      ++h->scratch_evictions;
+    }
+    h->scratch[si].assigned = true;
+    h->scratch[si].sid = sid;
+  }
+  auto& c = h->scratch[si];
+  c.last = ++h->scratch_tick;
+  if (!capturing && si > 0 && !has(c)) {  // this stream's own buffers for the kernel, zeroed on it
+    auto alloc = [&](auto** p, uint64_t bytes, bool zero) -> int {
+      if (*p) return HIPSPMV_OK;
+      bytes = std::max<uint64_t>(bytes, 8);
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(p), bytes));
+      h->device_bytes += bytes;
+      if (zero) HIP_TRY(hipMemsetAsync(*p, 0, bytes, s));
+      return HIPSPMV_OK;
+    };
+    int st;
+    if (kernel == HIPSPMV_KERNEL_SELL) {
+      if ((st = alloc(&c.sell_tickets, 4ull * h->sell.ntickets, true))) return st;
+      if ((st = alloc(&c.sell_partial, 8ull * h->sell.npieces, true))) return st;
+    } else if (kernel == HIPSPMV_KERNEL_WCSR) {
+      if ((st = alloc(&c.wc_ypart, 8ull * h->wc.nseg, false))) return st;
+    } else {
+      if ((st = alloc(&c.vc_tickets[k], 4ull * h->vc[k].ticket_words, true))) return st;
+      if ((st = alloc(&c.vc_partial[k], h->vc[k].partial_bytes, false))) return st;
+    }
+  }
+  *out = &c;
+  return HIPSPMV_OK;
+}
+
 static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in, void* d_y_out, int beta,
                   hipStream_t s, int mode) {
   hipError_t e = hipSuccess;
@@ -770,30 +965,24 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                        kernel == HIPSPMV_KERNEL_WCSR ||
                        (kernel == HIPSPMV_KERNEL_SELL && h->sell.npieces &&
                         (mode != HIPSPMV_MODE_ORDERED || h->dtype == HIPSPMV_U64));
-  // Inside a stream capture the handle does not order anything: a graph's
-  // launches are ordered by the graph and the stream it is replayed on, and a
-  // wait on (or a record of) scratch_ev there would tie the graph to an event
-  // recorded outside it.  The caller orders replays against other launches of
-  // the handle (include/hipspmv.h).
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (scratch) HIP_TRY(hipStreamIsCapturing(s, &cap));
-  const bool capturing = cap != hipStreamCaptureStatusNone;
-  // The event is recorded on the previous stream only now, when a launch
-  // comes on another one (everything enqueued there so far, the previous
-  // scratch launch included, precedes the record): a record after every
-  // launch put a barrier packet between back-to-back eager launches on one
-  // stream (~4.5 us gaps, profiles/r05/logs/gaps_*.log).
-  if (scratch && !capturing && h->scratch_used && h->scratch_stream != s) {
-    HIP_TRY(hipEventRecord(h->scratch_ev, h->scratch_stream));
-    HIP_TRY(hipStreamWaitEvent(s, h->scratch_ev, 0));
+  // the stream's own combine scratch: nothing is recorded or waited on between
+  // launches (on one stream they are ordered by it, across streams they share
+  // nothing) -- back-to-back eager launches have no packet between them
+  hipspmv_handle::Scratch* sc = nullptr;
+  if (scratch) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(s, &cap));
+    const int k = kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1 : 2;
+    if (int st = scratch_for(h, s, cap != hipStreamCaptureStatusNone, kernel, k, &sc)) return st;
   }
   if (kernel == HIPSPMV_KERNEL_SELL) {
     const auto& q = h->sell;
     SellArgs a{q.d_off,     q.d_width,   q.d_row,     q.d_len, q.d_col,  q.d_vals,
                q.d_hubs,    h->d_rowptr, h->d_colind, h->d_vals, d_x,    d_y_in,
                d_y_out,     q.nslices,   q.nhubs,     beta,    mode == HIPSPMV_MODE_ORDERED ? 1 : 0,
-               q.d_pieces,  q.npieces,   q.d_partial, q.d_tickets};
+               q.d_pieces,  q.npieces,   sc ? sc->sell_partial : q.d_partial, sc ? sc->sell_tickets : q.d_tickets};
     a.nt_from = h->sell_nt >= 0 ? (uint32_t)std::min<int64_t>(h->sell_nt, UINT32_MAX) : q.nslices / 2;
+    h->resident_entry_bytes = q.off.empty() ? 0 : 12ull * q.off[std::min(a.nt_from, q.nslices)];
     a.chain_g = h->sell_chain_g;
     a.niso = q.niso;
     if (h->sell_only == 1) a.nslices = 0;  // experimental timing probe: the hub work alone
@@ -808,12 +997,15 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     const int k = kernel == HIPSPMV_KERNEL_VCACHE ? 0 : kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1 : 2;
     const auto& v = h->vc[k];
     const VcGeom geoms[3] = {kVcOrdered, kVcSplit, v.vc4 ? kVcSplit4 : kVcQuad};
-    VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    v.d_partial,
-                 v.d_tickets, h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
+    VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,
+                 sc ? sc->vc_partial[k] : v.d_partial,
+                 sc ? sc->vc_tickets[k] : v.d_tickets,
+                 h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
                  v.npad,      h->nnz - 1, v.split,   beta, h->vcache_dma, (uint32_t)geoms[k].panel,
                  h->vcache_xlane, v.max_seg, h->vcache_map};
     a.nt_from = h->vcache_nt >= 0 ? (uint32_t)std::min<int64_t>(h->vcache_nt, UINT32_MAX)
                 : k < 2 || v.vc4 ? resident_blocks(v.nblocks, h->nnz) : ~0u;
+    h->resident_entry_bytes = v.block_first.empty() ? 0 : 12ull * v.block_first[std::min(a.nt_from, v.nblocks)];
     a.row_runs = v.row_runs;
     if (h->vcache_xmask) a.xmask = v.d_xmask;
     // an unprofiled launch leaves an unread profile of an earlier launch readable
@@ -832,6 +1024,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
       }
       if (k == 0) a.partial = h->d_prof;
       e = launch_vcache_profiled(h->dtype, a, s);
+      h->prof_tickets = a.tickets;
       h->prof_pending = e == hipSuccess;
       h->prof_valid = false;
       h->prof_stream = s;
@@ -854,14 +1047,16 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     a.chunk = h->wgather_chunk;
     // entries non-temporal unless option vcache_nt > 0 (full C4: 3391 us against 3594)
     a.nt_from = h->vcache_nt > 0 ? ~0u : 0u;
+    h->resident_entry_bytes = a.nt_from ? 12ull * h->nnz : 0;
     e = launch_wgather(h->dtype, a, s);
   } else if (kernel == HIPSPMV_KERNEL_WCSR) {
     const auto& w = h->wc;
     WcsrArgs a{w.d_rowptr, w.d_colind, w.d_vals, w.d_groups, w.ngroups, w.d_rowseg, w.d_segidx,
-               w.d_rgroups, w.rgroups,   w.d_ypart, d_x,      d_y_in,     d_y_out,  h->rows, beta};
+               w.d_rgroups, w.rgroups,   sc ? sc->wc_ypart : w.d_ypart, d_x, d_y_in, d_y_out, h->rows, beta};
     a.chunks = w.d_chunks;
     a.nchunks = w.nchunks;
     a.res_groups = (uint32_t)std::min<int64_t>(h->wcsr_res, w.ngroups);
+    h->resident_entry_bytes = w.group_first.empty() ? 0 : 12ull * w.group_first[a.res_groups];
     a.cols = h->cols;
     if (h->wcsr_reduce == 0 && w.d_rrow) {  // the compact reduce (default; option wcsr_reduce 1: all rows)
       a.rrow = w.d_rrow;
@@ -874,13 +1069,10 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     e = launch_wcsr(h->dtype, a, s);
   } else {
     CsrArgs a{h->d_rowptr, h->d_colind, h->d_vals, d_x, d_y_in, d_y_out, h->d_groups, h->rows, h->ngroups, beta};
+    h->resident_entry_bytes = 12ull * h->nnz;  // (default policy throughout)
     e = kernel == HIPSPMV_KERNEL_CSR_LANE ? launch_csr_lane(h->dtype, a, s) : launch_csr_vector(h->dtype, a, s);
   }
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
-  if (scratch && !capturing) {
-    h->scratch_stream = s;
-    h->scratch_used = true;
-  }
   h->last_kernel = kernel;
   h->last_beta = beta;
   h->execs++;
@@ -950,7 +1142,7 @@ static int resolve_profile(hipspmv_t* h) {
   const auto& v = h->vc[h->prof_layout];
   const uint32_t units = v.nblocks * v.split;
   std::vector<uint32_t> st((size_t)kVcProfWords * units);
-  const uint32_t* src = h->prof_layout == 0 ? h->d_prof : v.d_tickets + 4ull * v.nblocks;
+  const uint32_t* src = h->prof_layout == 0 ? h->d_prof : h->prof_tickets + 4ull * v.nblocks;
   HIP_TRY(hipMemcpy(st.data(), src, 4ull * st.size(), hipMemcpyDeviceToHost));
   const double cyc_per_tick = h->clock_khz / 1e5;
   auto at = [&](uint32_t u, int k) { return st[(size_t)kVcProfWords * u + k]; };
@@ -1101,14 +1293,7 @@ int hipspmv_exec(hipspmv_t* h, const void* x, void* y, int beta, int mode) {
       HIP_TRY(hipMalloc(&h->d_y, by));
       h->device_bytes += by;
     }
-    hipStream_t s = h->stream;
-    // the synchronous path orders itself after a device-resident launch on a
-    // caller's stream by a device synchronisation, not by recording on that
-    // stream (which the caller may have destroyed since)
-    if (h->scratch_used && h->scratch_stream != s) {
-      HIP_TRY(hipDeviceSynchronize());
-      h->scratch_stream = s;
-    }
+    hipStream_t s = h->stream;  // (its own combine scratch set: no ordering against other streams)
     HIP_TRY(hipEventRecord(h->ev[0], s));
     HIP_TRY(hipMemcpyAsync(h->d_x, x, bx, hipMemcpyHostToDevice, s));
     if (beta) HIP_TRY(hipMemcpyAsync(h->d_y, y, by, hipMemcpyHostToDevice, s));
@@ -1195,12 +1380,16 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   // columns once (split: its two halves read one half each)
   else if (k == "vcache_x_bytes") *out = h->vc0_eligible ? 8ull * h->vc[0].nblocks * h->cols : 0;
   else if (k == "vcache_split_x_bytes") *out = h->vc[1].ok ? 8ull * h->vc[1].nblocks * h->cols : 0;
-  else if (k == "vcache_split4_eligible") {  // builds the k_vquad layout if it is not built yet
-    if (!h->vc[2].ok && h->vq_eligible) {
-      const int st = ensure_layout(h, HIPSPMV_KERNEL_VCACHE_SPLIT4);
-      if (st && st != HIPSPMV_ERR_UNSUPPORTED) return st;
-    }
-    *out = h->vc[2].ok;
+  // the four-part geometry's eligibility by shape (a read builds nothing, ADVICE r05: selecting
+  // the kernel builds the layout, which can still prove unplaceable -- HIPSPMV_ERR_UNSUPPORTED)
+  else if (k == "vcache_split4_eligible") *out = h->vc[2].ok || h->vq_eligible;
+  else if (k == "scratch_evictions") *out = h->scratch_evictions;
+  // entry bytes the last launch loaded with the default cache policy -- they may stay in the 256 MiB
+  // Infinity Cache until the next launch (options vcache_nt / sell_nt / wcsr_res); the rest non-temporal
+  else if (k == "resident_entry_bytes") *out = h->resident_entry_bytes;  // a fifth stream took over a scratch set
+  else if (k == "scratch_streams") {  // streams holding a combine scratch set
+    *out = 0;
+    for (const auto& c : h->scratch) *out += c.assigned;
   }
   else if (k == "wgather_eligible") *out = h->vc[3].ok || h->wg_eligible;
   else if (k == "wgather_max_run") *out = h->wg_max_run;
@@ -1224,7 +1413,9 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "max_row_len") *out = h->max_row_len;
   else if (k == "empty_rows") *out = h->empty_rows;
   else if (k == "execs") *out = h->execs;
-  else if (k == "handoff_fallbacks") {  // k_vquad owners that gave up waiting (publish-and-count path), since create
+  // k_vquad owners that gave up waiting (publish-and-count path), since create; "handoff_timeouts"
+  // is its round-4 name, kept as an alias
+  else if (k == "handoff_fallbacks" || k == "handoff_timeouts") {
     uint32_t v = 0;
     if (int st = read_status(h, &v)) return st;
     *out = v;
@@ -1331,6 +1522,11 @@ int hipspmv_attach_pmc(hipspmv_t* h, const char* csv_path) {
 int hipspmv_destroy(hipspmv_t* h) {
   if (!h) return HIPSPMV_ERR_INVALID_ARG;
   release(h);
+  return HIPSPMV_OK;
+}
+
+int hipspmv_release_wait(void) {
+  Reclaimer::get().wait();
   return HIPSPMV_OK;
 }
 

@@ -367,6 +367,10 @@ void build_row_groups(const uint32_t* rowptr, uint32_t rows, std::vector<uint32_
 
 // hipspmv_last_error() text for this thread (capi.cpp).
 void set_last_error(const std::string& what);
+// Releases device buffers, events (hipEvent_t) and streams (hipStream_t) of a
+// destroyed object on the library's release thread, once the device has
+// finished the work submitted before this call; returns at once (capi.cpp).
+void defer_release(int device, std::vector<void*> ptrs, std::vector<void*> events, std::vector<void*> streams);
 
 // csrc/prep.hip: the bodies of hipspmv_prep_stats / hipspmv_mark_row_starts.
 int prep_stats(const uint32_t* colptr, const uint32_t* rowind, uint32_t rows, uint32_t cols, uint32_t nnz,

@@ -114,14 +114,13 @@ struct hipspmv_multi {
 
 static void release_multi(hipspmv_multi_t* m) {
   if (!m) return;
-  for (auto& s : m->shards) {
-    DevGuard g(s.device);
+  for (auto& s : m->shards) {  // released on the library's release thread (capi.cpp defer_release)
     if (s.h) hipspmv_destroy(s.h);
-    if (s.d_x) (void)hipFree(s.d_x);
-    if (s.d_y) (void)hipFree(s.d_y);
-    for (hipEvent_t e : s.ev)
-      if (e) (void)hipEventDestroy(e);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
+    std::vector<void*> evs(std::begin(s.ev), std::end(s.ev));
+    try {
+      defer_release(s.device, {s.d_x, s.d_y}, std::move(evs), {s.stream});
+    } catch (...) {  // host OOM while queueing: leaked, never freed under a live launch
+    }
   }
   for (ncclComm_t c : m->comms) rccl().commDestroy(c);
   delete m;

@@ -16,6 +16,7 @@ import ctypes as C
 import os
 import re
 import subprocess
+import weakref
 
 import numpy as np
 
@@ -98,6 +99,7 @@ def load_hipspmv() -> C.CDLL:
     lib.hipspmv_kernel_name.argtypes = [vp, C.c_int]
     lib.hipspmv_kernel_name.restype = C.c_char_p
     lib.hipspmv_destroy.argtypes = [vp]
+    lib.hipspmv_release_wait.argtypes = []
     lib.hipspmv_pmc_counter.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_double),
                                         C.POINTER(C.c_uint64)]
     lib.hipspmv_attach_pmc.argtypes = [vp, C.c_char_p]
@@ -127,7 +129,7 @@ def load_hipspmv() -> C.CDLL:
                  "hipspmv_multi_set_option", "hipspmv_multi_exec", "hipspmv_multi_stat", "hipspmv_multi_destroy"):
         getattr(lib, name).restype = C.c_int
     for name in ("hipspmv_create", "hipspmv_create_csr", "hipspmv_set_option", "hipspmv_exec",
-                 "hipspmv_exec_device", "hipspmv_stat", "hipspmv_destroy", "hipspmv_abi_version",
+                 "hipspmv_exec_device", "hipspmv_stat", "hipspmv_destroy", "hipspmv_release_wait", "hipspmv_abi_version",
                  "hipspmv_device_count", "hipspmv_prep_stats", "hipspmv_mark_row_starts"):
         getattr(lib, name).restype = C.c_int
     _hip = lib
@@ -223,13 +225,13 @@ class Handle:
         return cls(rowptr, colind, vals, rows, cols, csr=True, device=device)
 
     def set_option(self, key: str, value: int) -> None:
-        _check(self._lib.hipspmv_set_option(self._h, key.encode(), int(value)), f"set_option({key})")
+        _check(self._lib.hipspmv_set_option(self._handle(), key.encode(), int(value)), f"set_option({key})")
 
     def set_kernel(self, name: str) -> None:
         self.set_option("kernel", KERNELS[name])
 
     def kernel_name(self, mode: int = MODE_AUTO) -> str:
-        return self._lib.hipspmv_kernel_name(self._h, mode).decode()
+        return self._lib.hipspmv_kernel_name(self._handle(), mode).decode()
 
     def exec(self, x: np.ndarray, y: np.ndarray | None = None, beta: int = 0, mode: int = MODE_ORDERED):
         """Host-buffer exec (synchronous); returns y."""
@@ -239,7 +241,7 @@ class Handle:
             y = np.zeros(self.rows, dtype=npdt)
         if x.size != self.cols or y.size != self.rows or y.dtype != npdt or not y.flags.c_contiguous:
             raise ValueError(f"x needs {self.cols} and y {self.rows} contiguous {np.dtype(npdt).name} elements")
-        _check(self._lib.hipspmv_exec(self._h, x.ctypes.data, y.ctypes.data, beta, mode), "hipspmv_exec")
+        _check(self._lib.hipspmv_exec(self._handle(), x.ctypes.data, y.ctypes.data, beta, mode), "hipspmv_exec")
         return y
 
     def exec_device(self, x, y_out, y_in=None, beta: int = 0, mode: int = MODE_ORDERED, stream=None) -> None:
@@ -260,32 +262,40 @@ class Handle:
             if not ok:
                 raise ValueError(f"{name}: needs a contiguous 8-byte tensor of {n} elements on cuda:{self.device}")
         yin = _ptr(y_in) if y_in is not None else None
-        _check(self._lib.hipspmv_exec_device(self._h, _ptr(x), yin, _ptr(y_out), beta, mode, s),
+        _check(self._lib.hipspmv_exec_device(self._handle(), _ptr(x), yin, _ptr(y_out), beta, mode, s),
                "hipspmv_exec_device")
 
     def stat(self, key: str) -> int:
         v = C.c_uint64()
-        _check(self._lib.hipspmv_stat(self._h, key.encode(), C.byref(v)), f"stat({key})")
+        _check(self._lib.hipspmv_stat(self._handle(), key.encode(), C.byref(v)), f"stat({key})")
         return int(v.value)
 
     def attach_pmc(self, csv_path: str | None) -> None:
         """A rocprofv3 --pmc counter CSV of this handle's kernel backs read_misses /
         hazard_stalls / capacity_stalls (include/hipspmv.h); None detaches."""
-        _check(self._lib.hipspmv_attach_pmc(self._h, (csv_path or "").encode()), "attach_pmc")
+        _check(self._lib.hipspmv_attach_pmc(self._handle(), (csv_path or "").encode()), "attach_pmc")
 
     @classmethod
-    def _borrowed(cls, h, rows: int, cols: int, nnz: int, dtype: int, device: int):
-        """A view of a handle owned elsewhere (a MultiHandle block): never destroyed here."""
+    def _borrowed(cls, h, rows: int, cols: int, nnz: int, dtype: int, device: int, parent):
+        """A view of a handle owned elsewhere (a MultiHandle block): never destroyed
+        here.  It keeps its parent alive, and the parent's close() invalidates it
+        (a later call raises instead of reaching freed native memory)."""
         self = cls.__new__(cls)
         self.rows, self.cols, self.nnz, self.dtype, self.device = rows, cols, nnz, dtype, device
-        self._h, self._lib, self._owner = h, load_hipspmv(), False
+        self._h, self._lib, self._owner, self._parent = h, load_hipspmv(), False, parent
         return self
+
+    def _handle(self):
+        if not getattr(self, "_h", None):
+            raise HipSpMVError(1, "handle closed (or its MultiHandle was)")
+        return self._h
 
     def close(self) -> None:
         if getattr(self, "_h", None):
             if getattr(self, "_owner", True):
                 self._lib.hipspmv_destroy(self._h)
             self._h = None
+            self._parent = None
 
     def __del__(self):
         try:
@@ -339,6 +349,7 @@ class MultiHandle:
                   self._keep[1].size, U64 if self.dtype == np.uint64 else F64, devs,
                   len(devices), C.byref(self._h)), "multi_create")
         self._keep = None
+        self._views = []  # borrowed shard Handles, invalidated by close()
 
     def shard(self, i: int):
         """Block i's own Handle (owned by this MultiHandle; None for a block without rows)."""
@@ -346,8 +357,10 @@ class MultiHandle:
         _check(load_hipspmv().hipspmv_multi_shard(self._h, i, C.byref(h)), "multi_shard")
         if not h.value:
             return None
-        return Handle._borrowed(h, self.stat(f"shard{i}_rows"), self.cols, self.stat(f"shard{i}_nz"),
-                                U64 if self.dtype == np.uint64 else F64, self.devices[i])
+        sh = Handle._borrowed(h, self.stat(f"shard{i}_rows"), self.cols, self.stat(f"shard{i}_nz"),
+                              U64 if self.dtype == np.uint64 else F64, self.devices[i], self)
+        self._views.append(weakref.ref(sh))
+        return sh
 
     def set_option(self, key: str, value: int) -> None:
         _check(load_hipspmv().hipspmv_multi_set_option(self._h, key.encode(), value), f"multi_set_option({key})")
@@ -369,6 +382,11 @@ class MultiHandle:
         return int(v.value)
 
     def close(self) -> None:
+        for ref in getattr(self, "_views", []):
+            sh = ref()
+            if sh is not None:
+                sh._h = None
+        self._views = []
         if self._h:
             load_hipspmv().hipspmv_multi_destroy(self._h)
             self._h = C.c_void_p()
@@ -604,3 +622,9 @@ def permute_longest_row_first(colptr, rowind, vals, rows: int):
     load_host().spmvhost_permute_longest_row_first(rows, cols, nz, colptr, rowind, vals.view(np.uint64), perm, cp,
                                                    ri, v)
     return perm, cp, ri, v.view(vals.dtype)
+
+
+def release_wait() -> None:
+    """Until every handle destroyed so far has had its device memory released
+    (hipspmv_release_wait; destroy itself returns at once)."""
+    _check(load_hipspmv().hipspmv_release_wait(), "release_wait")

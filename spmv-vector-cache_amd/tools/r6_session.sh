@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-6 GPU session steps (each with its own time limit; a crash/abort/timeout ends the session).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 2
+mkdir -p gpurun_out
+OUT=gpurun_out
+export TMPDIR=/tmp
+step() {  # step NAME TIMEOUT CMD...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" | tee -a $OUT/session.log
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a $OUT/session.log
+  tail -4 "$OUT/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -gt 1 ]; then echo "stopping session after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+PYT="python -u -m pytest -x -v -p no:cacheprovider --timeout 120 --timeout-method thread"
+for s in ${STEPS:-streams}; do
+  case $s in
+    streams) step pytest_streams 400 $PYT -m gpu tests/test_gpu_streams.py -s ;;
+    scratch) step pytest_scratch 600 $PYT -m gpu tests/test_gpu_parity.py -k "split or sell or wcsr or graph or concurrent" ;;
+    multi) step pytest_multi 600 $PYT -m gpu tests/test_gpu_multi.py ;;
+    gaps) step gaps 300 rocprofv3 --kernel-trace -d $OUT/gaps -o run --output-format csv -- python3 spmv-vector-cache_amd/tools/launch_gaps.py --launches 40 &&
+          step gaps_summary 60 python3 spmv-vector-cache_amd/tools/launch_gaps_csv.py $OUT/gaps 40 ;;
+    pytest) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    bench) step bench 600 python bench.py ;;
+    bench20) step bench20 600 python bench.py --steps 20 --warmup 5 ;;
+  esac
+done
+echo "session done"

@@ -53,6 +53,8 @@ class FakeHandle:
             return 250
         if key == "wcsr_segments":
             return 0
+        if key == "resident_entry_bytes":  # the library's default: about half a vcache layout's entries
+            return 6 * self.nnz
         assert key == "alg_bytes"
         return 12 * self.nnz + 4 * (self.rows + 1) + 8 * self.cols + 8 * self.rows
 
@@ -78,6 +80,7 @@ class FakeStream:
 def _patch(monkeypatch):
     import bench
     monkeypatch.setattr(bench.hs.Handle, "from_csr", FakeHandle.from_csr)
+    monkeypatch.setattr(bench.hs, "release_wait", lambda: None)
     monkeypatch.setattr(torch.cuda, "set_device", lambda d: None)
     monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: None)
     monkeypatch.setattr(torch.cuda, "current_stream", lambda *a: FakeStream())
@@ -152,6 +155,13 @@ def test_bench_json_contract_single(monkeypatch):
     assert c5["shards"][0]["rows"][0] == 0 and c5["shards"][-1]["rows"][1] == 1 << 14
     assert all(s["parity"].startswith("within FAST bound") for s in c5["shards"] if s["kernel"]), c5
     assert c5["max_over_min"] >= 1.0 and c5["value"] > 0
+    # the residency share of the headline and the C4 shard block
+    assert rf["resident_entry_bytes"] == 6 * (32 << 12) and 0 < rf["frac_no_residency"]
+    assert rf["kernel_us_no_residency"] > 0 and "vcache_nt 0" in rf["no_residency_control"]
+    c4 = out["c4_shards"]
+    assert [s["shard"] for s in c4["shards"]] == [0, 7] and c4["min_roofline_frac"] > 0
+    assert c4["shards"][0]["rows"][0] == 0 and c4["shards"][1]["rows"][1] == 1 << 12
+    assert all(s["parity"].startswith("within FAST bound") for s in c4["shards"]), c4
 
 
 FAKE_ROCPROF = """#!/usr/bin/env python3
