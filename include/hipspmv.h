@@ -78,6 +78,12 @@ extern "C" {
                                  windows (window-major), then each row's window
                                  partials summed in a fixed order; fast,
                                  deterministic; wide, skewed x (C5 shards) */
+#define HIPSPMV_KERNEL_VFLOW 9 /* "vcache_flow": the vector cache over four column
+                                  parts of 16384-row blocks, x in a 3-slot LDS ring
+                                  handed over by LDS flags (no workgroup barrier per
+                                  step), each compute wave owning its y rows;
+                                  fast, deterministic; layout built on first
+                                  selection (stat "vflow_eligible") */
 #define HIPSPMV_KERNEL_SELL 7 /* SELL-C-sigma: one lane per row over slices of
                                  256 length-sorted rows, coalesced entries; rows
                                  over 256 entries one wave each (ORDERED: rows of

@@ -176,6 +176,18 @@ struct hipspmv_handle {
     bool row_runs = false;  // place_segments_banked: runs inside 16-lane rows (xlane 5 applies)
     bool vc4 = false;       // [2] built for k_vcache's four-part geometry (HIPSPMV_SPLIT4_VCACHE=1), not k_vquad
   } vc[4];  // [0] ordered (kVcOrdered), [1] split (kVcSplit); experimental: [2] split4; [3] wgather windows
+  struct Vf {  // k_vflow layout (build_vflow), built on first selection ("kernel" VFLOW) or by AUTO
+    bool ok = false, tried = false;
+    uint32_t *d_code = nullptr, *d_wbeg = nullptr, *d_wend = nullptr, *d_tickets = nullptr;
+    uint32_t* d_status = nullptr;  // bit 1: a flag wait gave up (the results of that launch are wrong)
+    uint64_t *d_vals = nullptr, *d_partial = nullptr;
+    uint32_t rows_per_block = 0, nblocks = 0, npanels = 0, part_panels = 0, npad = 0, max_group = 0;
+    uint64_t ticket_words = 0, partial_bytes = 0;
+    std::vector<uint32_t> block_first;  // nblocks + 1: first entry of each row block (last: nnz)
+  } vf;
+  int vflow_map = 0;  // option "vflow_map": 1 = XCDs 2h, 2h + 1 take column part h (vc_map.h MAP 1)
+  int vflow_de = 4;   // option "vflow_de": steps of entries in flight per compute wave (2, 3, 4, 8)
+  uint32_t* d_vfprof = nullptr;  // option "vflow_prof" (diagnostic): k_vflow's per-wave cycle stamps
   // The ordered vcache layout is only ever selected by name: its eligibility
   // and geometry are known at create, its entries built on first selection.
   bool vc0_eligible = false;
@@ -289,6 +301,8 @@ struct hipspmv_handle {
     uint32_t* sell_tickets = nullptr;
     uint64_t* sell_partial = nullptr;
     uint64_t* wc_ypart = nullptr;
+    uint32_t* vf_tickets = nullptr;
+    uint64_t* vf_partial = nullptr;
   } scratch[kScratchSets];
   uint64_t scratch_tick = 0, scratch_evictions = 0;
   uint32_t* prof_tickets = nullptr;  // the tickets buffer the last profiled split launch stamped
@@ -321,13 +335,28 @@ static void release(hipspmv_t* h) {
     ptrs.insert(ptrs.end(), {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks,
                              w.d_vals, w.d_ypart, w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits});
   }
+  ptrs.push_back(h->d_vfprof);
+  ptrs.insert(ptrs.end(), {h->vf.d_code, h->vf.d_wbeg, h->vf.d_wend, h->vf.d_tickets, h->vf.d_vals, h->vf.d_partial,
+                           h->vf.d_status});
   for (int i = 1; i < hipspmv_handle::kScratchSets; ++i) {  // set 0 is the layouts' own (above)
     auto& c = h->scratch[i];
     for (int k = 0; k < 3; ++k) ptrs.insert(ptrs.end(), {c.vc_tickets[k], c.vc_partial[k]});
-    ptrs.insert(ptrs.end(), {c.sell_tickets, c.sell_partial, c.wc_ypart});
+    ptrs.insert(ptrs.end(), {c.sell_tickets, c.sell_partial, c.wc_ypart, c.vf_tickets, c.vf_partial});
   }
   std::vector<void*> evs;
   for (hipEvent_t e : h->ev) evs.push_back(e);
+  // HIPSPMV_SYNC_RELEASE=1 (diagnostic, tools/destroy_probe.py): the round-5 form, every buffer freed by
+  // hipFree on the caller's thread -- the A/B that shows what a destroy inside a launch loop cost
+  if (const char* sr = std::getenv("HIPSPMV_SYNC_RELEASE"); sr && std::strcmp(sr, "1") == 0) {
+    DeviceGuard g(h->device);
+    for (void* p : ptrs)
+      if (p) (void)hipFree(p);
+    for (void* e : evs)
+      if (e) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return;
+  }
   try {
     defer_release(h->device, std::move(ptrs), std::move(evs), {h->stream});
   } catch (...) {  // host OOM while queueing: the device memory leaks, nothing is freed under a live launch
@@ -817,6 +846,9 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
       return fast_ok ? HIPSPMV_KERNEL_WCSR : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_VECTOR:
       return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : -HIPSPMV_ERR_UNSUPPORTED;
+    case HIPSPMV_KERNEL_VFLOW:  // fast; layout built on first selection (may prove not eligible)
+      if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
+      return h->vf.ok || !h->vf.tried ? HIPSPMV_KERNEL_VFLOW : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_AUTO:
       return auto_pick(h, fast_ok, true);
     default:
@@ -827,12 +859,63 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
 // The layout a kernel selected by name needs, built on its first selection
 // from the device CSR copy (AUTO's layouts exist since create); the time is
 // added to the handle's setup time.
+// The k_vflow layout from the CSR `a` (build_vflow); HIPSPMV_ERR_UNSUPPORTED
+// when the matrix does not fit it (then never tried again).
+static int build_vflow_layout(hipspmv_t* h, const HostCSR& a) {
+  auto& f = h->vf;
+  if (f.ok) return HIPSPMV_OK;
+  if (f.tried) return HIPSPMV_ERR_UNSUPPORTED;
+  f.tried = true;
+  VflowLayout V;
+  if (!build_vflow(a, V)) return HIPSPMV_ERR_UNSUPPORTED;
+  const VcacheLayout& L = V.L;
+  DeviceGuard g(h->device);
+  const uint64_t bytes0 = h->device_bytes;
+  auto fail = [&](int st) {
+    void* fp[] = {f.d_code, f.d_wbeg, f.d_wend, f.d_tickets, f.d_vals, f.d_partial, f.d_status};
+    for (void* p : fp)
+      if (p) (void)hipFree(p);
+    f = hipspmv_handle::Vf{};
+    f.tried = true;
+    h->device_bytes = bytes0;
+    return st;
+  };
+  int st;
+  if ((st = dev_upload(&f.d_code, L.code.data(), L.code.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&f.d_vals, L.vals.data(), L.vals.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&f.d_wbeg, V.wbeg.data(), V.wbeg.size(), h->device_bytes))) return fail(st);
+  if ((st = dev_upload(&f.d_wend, V.wend.data(), V.wend.size(), h->device_bytes))) return fail(st);
+  const std::vector<uint32_t> zeros(4ull * L.nblocks, 0u);  // owner-combine share counters
+  if ((st = dev_upload(&f.d_tickets, zeros.data(), zeros.size(), h->device_bytes))) return fail(st);
+  const uint64_t pbytes = 8ull * kVfGeom.split * L.nblocks * (uint32_t)kVfGeom.rows;
+  const hipError_t e = hipMalloc(reinterpret_cast<void**>(&f.d_partial), pbytes);
+  if (e != hipSuccess) return fail(hip_fail(e, "hipMalloc(vflow partials)"));
+  h->device_bytes += pbytes;
+  {
+    const uint32_t z = 0;
+    if ((st = dev_upload(&f.d_status, &z, 1, h->device_bytes))) return fail(st);
+  }
+  f.rows_per_block = L.rows_per_block;
+  f.nblocks = L.nblocks;
+  f.npanels = L.npanels;
+  f.part_panels = L.part_panels;
+  f.npad = L.npad;
+  f.max_group = V.max_group;
+  f.ticket_words = zeros.size();
+  f.partial_bytes = pbytes;
+  f.block_first.assign(L.nblocks + 1, (uint32_t)L.code.size());
+  for (uint32_t b = 0; b < L.nblocks; ++b) f.block_first[b] = L.seg[(size_t)b * kVfGeom.split * (L.npad + 1)];
+  f.ok = true;
+  return HIPSPMV_OK;
+}
+
 static int ensure_layout(hipspmv_t* h, int kernel) {
   const bool need = (kernel == HIPSPMV_KERNEL_SELL && !h->sell.built) ||
                     (kernel == HIPSPMV_KERNEL_WGATHER && !h->vc[3].ok) ||
                     (kernel == HIPSPMV_KERNEL_VCACHE && !h->vc[0].ok) ||
                     (kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4 && !h->vc[2].ok) ||
-                    (kernel == HIPSPMV_KERNEL_WCSR && !h->wc.built);
+                    (kernel == HIPSPMV_KERNEL_WCSR && !h->wc.built) ||
+                    (kernel == HIPSPMV_KERNEL_VFLOW && !h->vf.ok);
   if (!need) return HIPSPMV_OK;
   const uint64_t t0 = now_ns();
   int st;
@@ -843,6 +926,7 @@ static int ensure_layout(hipspmv_t* h, int kernel) {
     if (!st) {
       if (kernel == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
       else if (kernel == HIPSPMV_KERNEL_WCSR) st = build_wcsr_layout(h, a);
+      else if (kernel == HIPSPMV_KERNEL_VFLOW) st = build_vflow_layout(h, a);
       else if (kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
         // every segment inside the kernel's register window, runs placeable
         // (build_vcache_lanes); otherwise not eligible from now on
@@ -891,6 +975,8 @@ static void scratch_set0(hipspmv_t* h) {
   c.sell_tickets = h->sell.d_tickets;
   c.sell_partial = h->sell.d_partial;
   c.wc_ypart = h->wc.d_ypart;
+  c.vf_tickets = h->vf.d_tickets;
+  c.vf_partial = h->vf.d_partial;
 }
 
 // The combine scratch of stream s for a launch of `kernel` (vc layout k):
@@ -906,6 +992,7 @@ static int scratch_for(hipspmv_t* h, hipStream_t s, bool capturing, int kernel, 
   auto has = [&](const hipspmv_handle::Scratch& c) {
     if (kernel == HIPSPMV_KERNEL_SELL) return c.sell_tickets && c.sell_partial;
     if (kernel == HIPSPMV_KERNEL_WCSR) return c.wc_ypart != nullptr;
+    if (kernel == HIPSPMV_KERNEL_VFLOW) return c.vf_tickets && c.vf_partial;
     return c.vc_tickets[k] && c.vc_partial[k];
   };
   constexpr int NS = hipspmv_handle::kScratchSets;
@@ -948,6 +1035,9 @@ static int scratch_for(hipspmv_t* h, hipStream_t s, bool capturing, int kernel, 
       if ((st = alloc(&c.sell_partial, 8ull * h->sell.npieces, true))) return st;
     } else if (kernel == HIPSPMV_KERNEL_WCSR) {
       if ((st = alloc(&c.wc_ypart, 8ull * h->wc.nseg, false))) return st;
+    } else if (kernel == HIPSPMV_KERNEL_VFLOW) {
+      if ((st = alloc(&c.vf_tickets, 4ull * h->vf.ticket_words, true))) return st;
+      if ((st = alloc(&c.vf_partial, h->vf.partial_bytes, false))) return st;
     } else {
       if ((st = alloc(&c.vc_tickets[k], 4ull * h->vc[k].ticket_words, true))) return st;
       if ((st = alloc(&c.vc_partial[k], h->vc[k].partial_bytes, false))) return st;
@@ -962,7 +1052,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   hipError_t e = hipSuccess;
   if (mode == HIPSPMV_MODE_AUTO) mode = h->mode_opt;
   const bool scratch = kernel == HIPSPMV_KERNEL_VCACHE_SPLIT || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4 ||
-                       kernel == HIPSPMV_KERNEL_WCSR ||
+                       kernel == HIPSPMV_KERNEL_WCSR || kernel == HIPSPMV_KERNEL_VFLOW ||
                        (kernel == HIPSPMV_KERNEL_SELL && h->sell.npieces &&
                         (mode != HIPSPMV_MODE_ORDERED || h->dtype == HIPSPMV_U64));
   // the stream's own combine scratch: nothing is recorded or waited on between
@@ -1038,6 +1128,18 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     } else {
       e = launch_vcache(h->dtype, a, s);
     }
+  } else if (kernel == HIPSPMV_KERNEL_VFLOW) {
+    const auto& f = h->vf;
+    VflowArgs a{f.d_wbeg,  f.d_wend, f.d_code,   f.d_vals,        d_x,       d_y_in,    d_y_out,
+                sc->vf_partial, sc->vf_tickets, f.d_status, h->rows, h->cols, f.rows_per_block, f.nblocks,
+                f.npanels, f.part_panels, f.npad, beta};
+    a.nt_from = h->vcache_nt >= 0 ? (uint32_t)std::min<int64_t>(h->vcache_nt, UINT32_MAX)
+                                  : resident_blocks(f.nblocks, h->nnz);
+    a.map = h->vflow_map;
+    a.de = h->vflow_de;
+    a.prof = h->d_vfprof;
+    h->resident_entry_bytes = 12ull * f.block_first[std::min(a.nt_from, f.nblocks)];
+    e = launch_vflow(h->dtype, a, s);
   } else if (kernel == HIPSPMV_KERNEL_WGATHER) {
     const auto& v = h->vc[3];
     VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    nullptr,
@@ -1104,6 +1206,7 @@ static std::string kernel_symbol(const hipspmv_t* h) {
     case HIPSPMV_KERNEL_CSR_LANE: return "k_csr_lane<" + T + ">";
     case HIPSPMV_KERNEL_CSR_VECTOR: return "k_csr_vector<" + T + ", false>";
     case HIPSPMV_KERNEL_WCSR: return "k_csr_vector<" + T + ", true>";
+    case HIPSPMV_KERNEL_VFLOW: return "k_vflow<" + T + ",";
     case HIPSPMV_KERNEL_SELL: return "k_sell";
     default: return "hipspmv::";
   }
@@ -1206,7 +1309,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   if (!h || !key) return HIPSPMV_ERR_INVALID_ARG;
   const std::string k(key);
   if (k == "kernel") {
-    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_WCSR) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_VFLOW) return HIPSPMV_ERR_INVALID_ARG;
     if (value == HIPSPMV_KERNEL_VCACHE && !h->vc0_eligible) return HIPSPMV_ERR_UNSUPPORTED;
     if (value == HIPSPMV_KERNEL_WGATHER && !h->wg_eligible) return HIPSPMV_ERR_UNSUPPORTED;
     if (int st = ensure_layout(h, (int)value)) return st;
@@ -1217,6 +1320,24 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "vcache_map") {  // 1: split4 XCD pairs; 2: split, one column part per XCD where it can
     if (value < 0 || value > 2) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_map = (int)value;
+  } else if (k == "vflow_map") {  // 1: k_vflow's column part h on XCDs 2h and 2h + 1
+    if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
+    h->vflow_map = (int)value;
+  } else if (k == "vflow_prof") {  // diagnostic: k_vflow launches write per-wave cycle stamps
+    DeviceGuard g(h->device);
+    if (value && !h->d_vfprof) {
+      const size_t bytes = 4ull * 4 * 16 * 4096;  // 4 words x 16 waves x up to 4096 units
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&h->d_vfprof), bytes));
+      HIP_TRY(hipMemset(h->d_vfprof, 0, bytes));
+      h->device_bytes += bytes;
+    } else if (!value && h->d_vfprof) {
+      HIP_TRY(hipDeviceSynchronize());
+      HIP_TRY(hipFree(h->d_vfprof));
+      h->d_vfprof = nullptr;
+    }
+  } else if (k == "vflow_de") {  // k_vflow's entry ring depth
+    if (value != 2 && value != 3 && value != 4 && value != 8) return HIPSPMV_ERR_INVALID_ARG;
+    h->vflow_de = (int)value;
   } else if (k == "vcache_xmask") {
     if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
     h->vcache_xmask = (int)value;
@@ -1384,6 +1505,39 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   // the kernel builds the layout, which can still prove unplaceable -- HIPSPMV_ERR_UNSUPPORTED)
   else if (k == "vcache_split4_eligible") *out = h->vc[2].ok || h->vq_eligible;
   else if (k == "scratch_evictions") *out = h->scratch_evictions;
+  else if (k == "vflow_eligible") *out = h->vf.ok;
+  else if (k.rfind("vflow_prof_", 0) == 0) {  // means over the units of the last profiled launch, cycles
+    // vflow_prof_loader_{freewait,dma,total}, vflow_prof_compute_{panelwait,apply,loads,total}
+    if (!h->d_vfprof || !h->vf.ok) return HIPSPMV_ERR_UNSUPPORTED;
+    DeviceGuard g(h->device);
+    const uint32_t units = h->vf.nblocks * kVfGeom.split;
+    std::vector<uint32_t> st(4ull * 16 * units);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(st.data(), h->d_vfprof, 4 * st.size(), hipMemcpyDeviceToHost));
+    const std::string f = k.substr(11);
+    const bool loader = f.rfind("loader_", 0) == 0;
+    const std::string what = f.substr(loader ? 7 : 8);
+    const int idx = loader ? (what == "freewait" ? 0 : what == "dma" ? 1 : what == "total" ? 3 : -1)
+                           : (what == "panelwait" ? 0 : what == "apply" ? 1 : what == "loads" ? 2 : what == "total" ? 3 : -1);
+    if (idx < 0) return HIPSPMV_ERR_KEY;
+    double sum = 0;
+    uint64_t n = 0;
+    for (uint32_t u = 0; u < units; ++u)
+      for (int w = loader ? 0 : kVfLoaders; w < (loader ? kVfLoaders : 16); ++w, ++n) sum += st[4ull * (u * 16 + w) + idx];
+    *out = n ? (uint64_t)(sum / n) : 0;
+  }  // the k_vflow layout is built (selected, and it fits)
+  else if (k == "vflow_units") *out = (uint64_t)h->vf.nblocks * kVfGeom.split;
+  else if (k == "vflow_max_group") *out = h->vf.max_group;
+  else if (k == "vflow_x_bytes") *out = h->vf.ok ? 8ull * h->vf.nblocks * h->cols : 0;
+  else if (k == "vflow_timeouts") {  // a k_vflow flag wait gave up since the layout was built (results wrong)
+    uint32_t v = 0;
+    if (h->vf.d_status) {
+      DeviceGuard g(h->device);
+      HIP_TRY(hipDeviceSynchronize());
+      HIP_TRY(hipMemcpy(&v, h->vf.d_status, 4, hipMemcpyDeviceToHost));
+    }
+    *out = (v >> 1) & 1u;
+  }
   // entry bytes the last launch loaded with the default cache policy -- they may stay in the 256 MiB
   // Infinity Cache until the next launch (options vcache_nt / sell_nt / wcsr_res); the rest non-temporal
   else if (k == "resident_entry_bytes") *out = h->resident_entry_bytes;  // a fifth stream took over a scratch set
@@ -1500,6 +1654,7 @@ const char* hipspmv_kernel_name(hipspmv_t* h, int mode) {
     case HIPSPMV_KERNEL_CSR_VECTOR: return "csr_vector";
     case HIPSPMV_KERNEL_SELL: return "sell";
     case HIPSPMV_KERNEL_WCSR: return "wcsr";
+    case HIPSPMV_KERNEL_VFLOW: return "vcache_flow";
     default: return "unsupported";
   }
 }

@@ -75,6 +75,17 @@ constexpr uint32_t kVqLMore = 1u << 28;
 // the k_vquad geometry: 16384 rows, 1984-column panels, 4 parts, 12 column
 // bits (the code holds row_local << 12 and the flags in bits 28-31)
 constexpr VcGeom kVcQuad{16384, 1984, 4, 12};
+// ---- k_vflow (csrc/vflow.hip): four column parts of
+// 16384-row blocks (x per CU a quarter of x, 64 x 4 = 256 units on C3); x in a
+// ring of kVfSlots panels of 1280 columns handed from the loader waves to the
+// compute waves by LDS flags instead of a workgroup barrier per step.  Compute
+// wave w owns the block rows with vf_wave_of(row_local) == w -- every update of
+// a y row comes from one wave, in step order, so waves may be at different
+// steps.  LDS: 16384 * 8 + 3 * 1280 * 8 + 64 flag bytes.
+constexpr VcGeom kVfGeom{16384, 1280, 4, 16, 4096};
+constexpr int kVfLoaders = 2, kVfWaves = 14, kVfSlots = 3;
+constexpr uint32_t kVfGroupMax = 128;  // entries of one (step, wave) group: two 64-lane slots
+constexpr uint32_t vf_wave_of(uint32_t row_local) { return (row_local >> 5) % (uint32_t)kVfWaves; }
 constexpr uint32_t kVqLanes = 13 * 64;
 // k_vcache's split geometry: compute lanes (16 - 3 loader waves) * 64 (VcCfg<3>)
 constexpr uint32_t kVcSplitCT = 13 * 64;
@@ -342,6 +353,14 @@ void sort_segments_by_line(VcacheLayout& L);
 // k_vcache split: entries of each segment re-placed for LDS banks (plan.cpp;
 // the same sums, bit-identical results)
 void place_segments_banked(VcacheLayout& L, uint32_t CT);
+struct VflowLayout {
+  VcacheLayout L;              // blocks, panels, parts; entries regrouped by (unit, step, wave)
+  hvec<uint32_t> wbeg, wend;   // [unit][wave][step < npad]: the group's entries [wbeg, wend)
+  uint32_t max_group = 0;
+};
+// false: not eligible (a group past kVfGroupMax entries, or a run that cannot
+// stay inside a 16-lane DPP row)
+bool build_vflow(const HostCSR& a, VflowLayout& out);
 // k_vquad's placement of the same entries for CT compute lanes (plan.cpp)
 bool build_vcache_lanes(const HostCSR& a, const VcGeom& g, uint32_t CT, VcacheLayout& out);
 // The ordered geometry's x-line mask (k_vcache SPLIT 1, register-staged loaders): per unit, panel

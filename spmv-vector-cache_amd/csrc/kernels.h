@@ -102,6 +102,26 @@ struct SellArgs {
   uint32_t chain_g = 0;         // exact: 0 product; 1 no isolated chains; 2 / 3 isolated stages of G = 12 / 30 (experimental)
 };
 
+struct VflowArgs {  // k_vflow (csrc/vflow.hip) over a build_vflow layout
+  const uint32_t* wbeg;  // [unit][wave][npad]
+  const uint32_t* wend;
+  const uint32_t* code;
+  const void* vals;
+  const void* x;
+  const void* y_in;
+  void* y_out;
+  void* partial;       // [4][nblocks][16384] column-part partials
+  uint32_t* tickets;   // [4 * nblocks] combine share counters, zero between launches
+  uint32_t* status;    // bit 1: a flag wait gave up (results wrong; never a hang)
+  uint32_t rows, cols, rows_per_block, nblocks, npanels, part_panels, npad;
+  int beta;
+  uint32_t nt_from = ~0u;  // row blocks b >= nt_from load their entries non-temporally
+  int map = 0;             // 1: XCDs 2h, 2h + 1 take column part h (vc_map.h MAP 1)
+  int de = 4;              // steps of entries in flight per compute wave (2, 3, 4, 8)
+  uint32_t* prof = nullptr;  // diagnostic stamps (option "vflow_prof"): 4 u32 per (unit, wave)
+};
+hipError_t launch_vflow(int dtype, const VflowArgs& a, hipStream_t s);
+
 hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s);
 // The same kernel in its default configuration (ordered: register-staged
 // loaders; split 3: LDS-DMA loaders, cross-lane runs when the layout fits)

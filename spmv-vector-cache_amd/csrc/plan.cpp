@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -664,6 +665,99 @@ void place_segments_banked(VcacheLayout& L, uint32_t CT) {
   });
   // a segment left in (row, column) order may hold a run across a DPP row
   L.row_runs = all;
+}
+
+// k_vflow's layout (csrc/vflow.hip): build_vcache's segments over kVfGeom,
+// each segment regrouped by owning compute wave (vf_wave_of of the row,
+// stable: every row keeps its one run and its column order), each group then
+// placed for LDS banks with its runs inside 16-lane DPP rows (BankPlacer, the
+// group is the wave's two 64-lane slots; where it cannot pack the runs, the
+// group keeps (row, column) order and only a run across a slot is refused).  Group (u, w, i) -- unit u, wave w,
+// step i -- holds entries [wbeg, wend).  Only the order of rows inside a step
+// changes, so every row's sum is the same sequence as in (row, column) order.
+bool build_vflow(const HostCSR& a, VflowLayout& out) {
+  const VcGeom& g = kVfGeom;
+  if (!vcache_eligible(a, g) || vcache_max_run(a, (uint32_t)g.panel) > 16) return false;
+  VcacheLayout& L = out.L;
+  build_vcache(a, g, L);
+  const uint32_t units = L.nblocks * (uint32_t)g.split, npad = L.npad, W = (uint32_t)kVfWaves;
+  out.wbeg.resize((size_t)units * W * npad);
+  out.wend.resize((size_t)units * W * npad);
+  const unsigned nt = std::max(1u, std::min(plan_threads(), units));
+  std::atomic<bool> ok{true};
+  std::vector<uint32_t> tmax(nt, 0);
+  par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
+    BankPlacer place(64);
+    std::vector<uint32_t> code;
+    std::vector<uint64_t> vals;
+    for (uint64_t t = t0; t < t1; ++t)
+      for (uint32_t u = (uint32_t)t; u < units && ok; u += nt) {
+        const uint32_t* sg = &L.seg[(size_t)u * (npad + 1)];
+        for (uint32_t i = 0; i < npad; ++i) {
+          const uint32_t s0 = sg[i], s1 = sg[i + 1];
+          uint32_t cnt[kVfWaves + 1] = {0};
+          for (uint32_t e = s0; e < s1; ++e) cnt[vf_wave_of((L.code[e] >> 16) & 0x3FFFu) + 1]++;
+          for (uint32_t w = 0; w < W; ++w) {
+            tmax[t] = std::max(tmax[t], cnt[w + 1]);
+            if (cnt[w + 1] > kVfGroupMax) ok = false;
+            cnt[w + 1] += cnt[w];
+          }
+          code.assign(L.code.begin() + s0, L.code.begin() + s1);
+          vals.assign(L.vals.begin() + s0, L.vals.begin() + s1);
+          uint32_t cur[kVfWaves];
+          for (uint32_t w = 0; w < W; ++w) {
+            cur[w] = s0 + cnt[w];
+            out.wbeg[((size_t)u * W + w) * npad + i] = s0 + cnt[w];
+            out.wend[((size_t)u * W + w) * npad + i] = s0 + cnt[w + 1];
+          }
+          for (uint32_t q = 0; q < s1 - s0; ++q) {
+            const uint32_t d = cur[vf_wave_of((code[q] >> 16) & 0x3FFFu)]++;
+            L.code[d] = code[q];
+            L.vals[d] = vals[q];
+          }
+          for (uint32_t w = 0; w < W && ok; ++w) {
+            const uint32_t b0 = s0 + cnt[w], b1 = s0 + cnt[w + 1];
+            if (b1 - b0 > kVfGroupMax) break;
+            if (place(L.code.data(), L.vals.data(), b0, b1)) continue;
+            // kept in (row, column) order (too few singles to pad the runs into 16-lane rows): a run
+            // may cross a DPP row -- the kernel takes such a continuation by shuffle -- but never a
+            // 64-lane slot
+            for (uint32_t e = b0; e < b1; ++e)
+              if ((L.code[e] & kVcCont) && ((e - b0) % 64) == 0) ok = false;
+          }
+        }
+      }
+  });
+  if (!ok) return false;
+  // wave-major inside each unit: wave w's groups of all steps back to back, so a wave streams one
+  // contiguous range and only the boundary lines between its consecutive steps are shared (by the
+  // same wave, one step apart); step-major order split every step's entries into 14 groups whose
+  // boundary lines two waves fetched (measured 203 us on C3)
+  par_chunks(nt, nt, [&](unsigned, uint64_t t0, uint64_t t1) {
+    std::vector<uint32_t> code;
+    std::vector<uint64_t> vals;
+    for (uint64_t t = t0; t < t1; ++t)
+      for (uint32_t u = (uint32_t)t; u < units; u += nt) {
+        const uint32_t u0 = L.seg[(size_t)u * (npad + 1)], u1 = L.seg[(size_t)u * (npad + 1) + npad];
+        code.assign(L.code.begin() + u0, L.code.begin() + u1);
+        vals.assign(L.vals.begin() + u0, L.vals.begin() + u1);
+        uint32_t d = u0;
+        for (uint32_t w = 0; w < W; ++w)
+          for (uint32_t i = 0; i < npad; ++i) {
+            const size_t gi = ((size_t)u * W + w) * npad + i;
+            const uint32_t b0 = out.wbeg[gi], b1 = out.wend[gi];
+            out.wbeg[gi] = d;
+            for (uint32_t e = b0; e < b1; ++e, ++d) {
+              L.code[d] = code[e - u0];
+              L.vals[d] = vals[e - u0];
+            }
+            out.wend[gi] = d;
+          }
+      }
+  });
+  out.max_group = *std::max_element(tmax.begin(), tmax.end());
+  L.row_runs = ok;
+  return ok;
 }
 
 // The k_vquad form of the vcache layout: the same blocks,

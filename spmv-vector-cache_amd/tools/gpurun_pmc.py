@@ -23,7 +23,7 @@ del rp, ci, v
 x = torch.from_numpy(hs.gen_vector(n, 3)).cuda(); y = torch.empty(rows, dtype=torch.float64, device="cuda")
 s = torch.cuda.current_stream()
 h.set_kernel(kernel)
-mode = hs.MODE_FAST if any(k in kernel for k in ("split", "vector", "wcsr")) else hs.MODE_ORDERED
+mode = hs.MODE_FAST if any(k in kernel for k in ("split", "vector", "wcsr", "flow")) else hs.MODE_ORDERED
 for _ in range(10): h.exec_device(x, y, beta=0, mode=mode, stream=s)
 torch.cuda.synchronize()
 print("ran", h.kernel_name(mode), "x10", flush=True)

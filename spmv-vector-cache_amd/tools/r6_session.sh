@@ -22,6 +22,9 @@ for s in ${STEPS:-streams}; do
     multi) step pytest_multi 600 $PYT -m gpu tests/test_gpu_multi.py ;;
     gaps) step gaps 300 rocprofv3 --kernel-trace -d $OUT/gaps -o run --output-format csv -- python3 spmv-vector-cache_amd/tools/launch_gaps.py --launches 40 &&
           step gaps_summary 60 python3 spmv-vector-cache_amd/tools/launch_gaps_csv.py $OUT/gaps 40 ;;
+    vflow) step pytest_vflow 300 $PYT -m gpu tests/test_gpu_parity.py -k "vcache_flow or vflow" ;;
+    vfprof) step vf_prof 300 python -u spmv-vector-cache_amd/tools/vf_prof.py ${VFPROF_ARGS:-} ;;
+    vfab) step vf_ab 300 python -u spmv-vector-cache_amd/tools/vf_ab.py ${VFAB_ARGS:-} ;;
     pytest) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;
     bench20) step bench20 600 python bench.py --steps 20 --warmup 5 ;;

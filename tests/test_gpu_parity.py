@@ -38,7 +38,12 @@ def _check(name, rows, cols, colptr, rowind, vals, x, kernel, beta, mode=hs.MODE
             (kernel == "vcache_split" and not h.stat("vcache_split_eligible")) or \
             (kernel == "vcache_split4" and not h.stat("vcache_split4_eligible")):
         pytest.skip("vcache not eligible")
-    h.set_kernel(kernel)
+    try:
+        h.set_kernel(kernel)
+    except hs.HipSpMVError as e:  # the four-part layouts are placed on selection, and may not fit
+        if kernel in ("vcache_split4", "vcache_flow") and e.status == 5:
+            pytest.skip(f"{kernel}: layout not placeable for this matrix")
+        raise
     npdt = vals.dtype
     if y0 is None:
         y0 = (np.random.default_rng(11).uniform(-1, 1, rows) if npdt == np.float64
@@ -60,7 +65,7 @@ def _check(name, rows, cols, colptr, rowind, vals, x, kernel, beta, mode=hs.MODE
 
 @pytest.mark.parametrize("name", fx.ALL_FIXTURES)
 @pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr",
-                                    "vcache_split4"])
+                                    "vcache_split4", "vcache_flow"])
 @pytest.mark.parametrize("beta", [0, 1])
 def test_fixtures(gpu, name, kernel, beta):
     rows, cols, colptr, rowind, vals = fx.load(name)
@@ -78,7 +83,7 @@ def _tile_columns(cols, colptr, rowind, vals, k):
 
 
 @pytest.mark.parametrize("name", ["circuit204", "circuit204-uint64"])
-@pytest.mark.parametrize("kernel", ["vcache_split", "vcache_split4"])
+@pytest.mark.parametrize("kernel", ["vcache_split", "vcache_split4", "vcache_flow"])
 @pytest.mark.parametrize("beta", [0, 1])
 def test_tiled_fixture_column_parts(gpu, name, kernel, beta):
     # the headline FAST kernels on a reference-held matrix: circuit204 tiled to
@@ -89,6 +94,8 @@ def test_tiled_fixture_column_parts(gpu, name, kernel, beta):
     h = hs.Handle.from_csc(tcp, tri, tv, rows, tcols)
     if kernel == "vcache_split":
         assert h.stat("vcache_split_eligible"), (name, tcols)  # the product FAST kernel runs it
+    elif kernel == "vcache_flow":
+        pass  # (placed on selection in _check; circuit204's rows are short: it fits)
     elif not h.stat("vcache_split4_eligible"):
         # k_vquad holds a segment in registers (<= 1664 entries); circuit204's 1020 rows
         # put ~2 x 5.9 k entries into each 1984-column panel
@@ -133,7 +140,7 @@ def _random_csc(rows, cols, density, rng, dtype=np.float64, empty_rows=True, lon
 @pytest.mark.parametrize("shape", [(1, 1), (1, 300), (300, 1), (257, 1000), (5000, 333), (3000, 20000),
                                    (700, 20001), (900, 14001)])
 @pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr",
-                                    "vcache_split4"])
+                                    "vcache_split4", "vcache_flow"])
 def test_random_ragged(gpu, shape, kernel):
     rng = np.random.default_rng(shape[0] * 31 + shape[1])
     rows, cols = shape
@@ -146,7 +153,7 @@ def test_random_ragged(gpu, shape, kernel):
 
 
 @pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr",
-                                    "vcache_split4"])
+                                    "vcache_split4", "vcache_flow"])
 def test_random_u64_wraparound(gpu, kernel):
     rng = np.random.default_rng(5)
     rows, cols = 4000, 9000
@@ -157,7 +164,7 @@ def test_random_u64_wraparound(gpu, kernel):
 
 
 @pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr",
-                                    "vcache_split4"])
+                                    "vcache_split4", "vcache_flow"])
 def test_random_duplicates(gpu, kernel):
     # repeated (row, col) entries (5 % of a ragged matrix with a full-width row):
     # ORDERED kernels add each copy in CSC order, bit for bit; FAST within the bound
@@ -504,6 +511,42 @@ def test_c3_split_deterministic_and_within_bound(gpu):
     assert np.all(np.abs(y1 - (y_ref + y0)) <= _fast_bound(np.full(n, 33), absprod + np.abs(y0), 0) * 2)
 
 
+@pytest.mark.parametrize("vmap", [0, 1])
+def test_vflow_c3_full_size(gpu, vmap):
+    # k_vflow (csrc/vflow.hip) on full C3: 64 row blocks x 4 parts = 256 units, x streamed into LDS
+    # 64 x 8 MB per launch; deterministic (identical bits on every launch and under either XCD
+    # placement), within the FAST bound of the oracle, u64 exact, no flag wait gave up
+    n = 1 << 20
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
+    x = hs.gen_vector(n, 3)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
+    h.set_kernel("vcache_flow")
+    h.set_option("vflow_map", vmap)
+    assert h.stat("vflow_eligible") == 1 and h.stat("vflow_units") == 256
+    assert h.stat("vflow_x_bytes") == 64 * 8 * n and h.stat("vflow_max_group") <= 128
+    ys = [h.exec(x, beta=0, mode=hs.MODE_FAST) for _ in range(3)]
+    assert ys[0].tobytes() == ys[1].tobytes() == ys[2].tobytes()
+    colptr, rowind, cvals = oracle.csr2csc(n, n, rowptr, colind, vals)
+    y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, rows=n)
+    absprod = np.zeros(n)
+    np.add.at(absprod, np.repeat(np.arange(n), 32), np.abs(vals * x[colind]))
+    assert np.all(np.abs(ys[0] - y_ref) <= _fast_bound(np.full(n, 32), absprod, 0))
+    y0 = np.random.default_rng(4).uniform(-1, 1, n)
+    y1 = h.exec(x, y0.copy(), beta=1, mode=hs.MODE_FAST)
+    assert np.all(np.abs(y1 - (y_ref + y0)) <= _fast_bound(np.full(n, 33), absprod + np.abs(y0), 0) * 2)
+    assert h.stat("vflow_timeouts") == 0
+    h.close()
+    uv = (vals.view(np.uint64) >> np.uint64(7))
+    ux = np.arange(n, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    hu = hs.Handle.from_csr(rowptr, colind, uv, n, n)
+    hu.set_kernel("vcache_flow")
+    hu.set_option("vflow_map", vmap)
+    _, _, cuv = oracle.csr2csc(n, n, rowptr, colind, uv)
+    assert hu.exec(ux, beta=0, mode=hs.MODE_FAST).tobytes() == oracle.spmv_csc(colptr, rowind, cuv, ux, rows=n).tobytes()
+    assert hu.stat("vflow_timeouts") == 0
+    hu.close()
+
+
 def test_split_combine_concurrent_streams(gpu):
     # vcache_split's column-part combine uses per-handle tickets and partials;
     # launches of one handle on two streams with no host synchronisation are
@@ -557,10 +600,13 @@ def test_vquad_variants(gpu, variant):  # configurations: x / entry ring depths 
             vals = rng.uniform(-1, 1, colind.size)
         x = rng.uniform(-1, 1, cols)
         h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
-        if not h.stat("vcache_split4_eligible"):
+        try:  # the stat is the shape's eligibility; the lane placement decides on selection
+            if not h.stat("vcache_split4_eligible"):
+                raise hs.HipSpMVError(5, "not eligible")
+            h.set_kernel("vcache_split4")
+        except hs.HipSpMVError:
             h.close()
             continue
-        h.set_kernel("vcache_split4")
         h.set_option("vquad_variant", variant)
         if variant in (22, 23, 25):  # row block 0 resident (default policy), the others non-temporal
             h.set_option("vcache_nt", 1)
@@ -693,8 +739,8 @@ def test_vquad_c3_full_size(gpu):
     x = hs.gen_vector(n, 3)
     h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
     assert h.stat("vcache_split4_eligible") == 1
-    assert h.stat("vcache_split4_x_bytes") == 64 * 8 * n
     h.set_kernel("vcache_split4")
+    assert h.stat("vcache_split4_x_bytes") == 64 * 8 * n
     ys = [h.exec(x, beta=0, mode=hs.MODE_FAST) for _ in range(3)]
     assert ys[0].tobytes() == ys[1].tobytes() == ys[2].tobytes()
     colptr, rowind, cvals = oracle.csr2csc(n, n, rowptr, colind, vals)
@@ -736,7 +782,10 @@ def test_experimental_vcache_variants(gpu, kernel, dma, xlane, xmap):
                "wgather": "wgather_eligible"}.get(kernel, "vcache_eligible")
         if not h.stat(key):
             continue
-        h.set_kernel(kernel)
+        try:
+            h.set_kernel(kernel)
+        except hs.HipSpMVError:  # a four-part layout not placeable for this shape
+            continue
         h.set_option("vcache_dma", dma)
         h.set_option("vcache_xlane", xlane)
         h.set_option("vcache_map", xmap)

@@ -95,8 +95,9 @@ def test_launch_on_destroyed_side_stream_then_another(gpu):
     assert y_host.tobytes() == ref.tobytes()
     for i, y in enumerate(ys):
         assert y.cpu().numpy().tobytes() == ref.tobytes(), i
-    # current stream, A (destroyed), B, C, the handle's own: five streams over four sets
-    assert h.stat("scratch_streams") == 4 and h.stat("scratch_evictions") == 1
+    # current stream, A (destroyed), B, C, the handle's own: up to five stream values over four sets
+    # (B may receive A's value once A's queue is gone: test_hip_stream_destroy_waits_for_queued_work)
+    assert h.stat("scratch_streams") == 4 and h.stat("scratch_evictions") <= 1
     h.close()
 
 

@@ -44,3 +44,17 @@ def test_vquad_lanes_layout_replay():
         oks = [l for l in out.stdout.splitlines() if l.endswith(": ok")]
         assert any(l.startswith("stripe") for l in oks) and len(oks) >= 8, out.stdout
         assert "VIOLATION" not in out.stderr and "runtime error" not in out.stderr
+
+
+def test_vflow_layout_replay():
+    # k_vflow (csrc/vflow.hip) over build_vflow: every group within its two 64-lane slots, every x
+    # index inside its panel slot and every slot element written by the loaders' DMA, every y row
+    # updated only by the wave that owns it (the kernel's no-race premise across steps), runs inside
+    # a slot, every entry consumed once; u64 exact, f64 within the FAST bound -- plain and under
+    # ASan/UBSan (scaled stripe, odd columns, clustered runs, ragged rows, an ineligible shape)
+    for tool in ("vf_sim", "vf_sim_san"):
+        subprocess.run(["make", "-C", hs.PKG_DIR, f"lib/{tool}"], check=True, stdout=subprocess.DEVNULL)
+        out = subprocess.run([os.path.join(hs.LIB_DIR, tool)], capture_output=True, text=True, timeout=900)
+        assert out.returncode == 0, out.stdout + out.stderr[-4000:]
+        assert "vf_sim: all ok" in out.stdout and sum(l.endswith(": ok") for l in out.stdout.splitlines()) >= 8
+        assert "VIOLATION" not in out.stderr and "runtime error" not in out.stderr
