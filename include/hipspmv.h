@@ -78,7 +78,7 @@ extern "C" {
                                  windows (window-major), then each row's window
                                  partials summed in a fixed order; fast,
                                  deterministic; wide, skewed x (C5 shards) */
-#define HIPSPMV_KERNEL_VFLOW 9 /* "vcache_flow": the vector cache over four column
+#define HIPSPMV_KERNEL_VCACHE_FLOW 9 /* "vcache_flow": the vector cache over four column
                                   parts of 16384-row blocks, x in a 3-slot LDS ring
                                   handed over by LDS flags (no workgroup barrier per
                                   step), each compute wave owning its y rows;
@@ -332,6 +332,14 @@ const char *hipspmv_strerror(int status);
 /* Text of the last HIP error seen by this thread (static per-thread buffer). */
 const char *hipspmv_last_error(void);
 int hipspmv_abi_version(void);
+/* Build variant: HIPSPMV_BUILD_EXPERIMENTAL when the library carries the
+ * kernel forms AUTO never picks (VCACHE_SPLIT4 / k_vquad, the vcache
+ * continuation forms 1, 2, 4 and the ordered ones, "vcache_map", the ordered
+ * LDS-DMA loader, "vquad_variant"): make EXPERIMENTAL=1 builds them into
+ * lib/exp/libhipspmv.so.  The product library answers HIPSPMV_ERR_UNSUPPORTED
+ * to the options and kernel that select them. */
+#define HIPSPMV_BUILD_EXPERIMENTAL 1
+int hipspmv_build_flags(void);
 int hipspmv_device_count(int *count);
 
 #ifdef __cplusplus

@@ -146,6 +146,12 @@ class Reclaimer {
 
 void hipspmv::set_last_error(const std::string& what) { g_last_error = what; }
 
+#ifdef HIPSPMV_EXPERIMENTAL_KERNELS
+static constexpr bool kExperimental = true;
+#else
+static constexpr bool kExperimental = false;
+#endif
+
 void hipspmv::defer_release(int device, std::vector<void*> ptrs, std::vector<void*> events,
                             std::vector<void*> streams) {
   Reclaimer::Item it;
@@ -846,9 +852,9 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
       return fast_ok ? HIPSPMV_KERNEL_WCSR : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_VECTOR:
       return fast_ok ? HIPSPMV_KERNEL_CSR_VECTOR : -HIPSPMV_ERR_UNSUPPORTED;
-    case HIPSPMV_KERNEL_VFLOW:  // fast; layout built on first selection (may prove not eligible)
+    case HIPSPMV_KERNEL_VCACHE_FLOW:  // fast; layout built on first selection (may prove not eligible)
       if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
-      return h->vf.ok || !h->vf.tried ? HIPSPMV_KERNEL_VFLOW : -HIPSPMV_ERR_UNSUPPORTED;
+      return h->vf.ok || !h->vf.tried ? HIPSPMV_KERNEL_VCACHE_FLOW : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_AUTO:
       return auto_pick(h, fast_ok, true);
     default:
@@ -915,7 +921,7 @@ static int ensure_layout(hipspmv_t* h, int kernel) {
                     (kernel == HIPSPMV_KERNEL_VCACHE && !h->vc[0].ok) ||
                     (kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4 && !h->vc[2].ok) ||
                     (kernel == HIPSPMV_KERNEL_WCSR && !h->wc.built) ||
-                    (kernel == HIPSPMV_KERNEL_VFLOW && !h->vf.ok);
+                    (kernel == HIPSPMV_KERNEL_VCACHE_FLOW && !h->vf.ok);
   if (!need) return HIPSPMV_OK;
   const uint64_t t0 = now_ns();
   int st;
@@ -926,7 +932,7 @@ static int ensure_layout(hipspmv_t* h, int kernel) {
     if (!st) {
       if (kernel == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
       else if (kernel == HIPSPMV_KERNEL_WCSR) st = build_wcsr_layout(h, a);
-      else if (kernel == HIPSPMV_KERNEL_VFLOW) st = build_vflow_layout(h, a);
+      else if (kernel == HIPSPMV_KERNEL_VCACHE_FLOW) st = build_vflow_layout(h, a);
       else if (kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4) {
         // every segment inside the kernel's register window, runs placeable
         // (build_vcache_lanes); otherwise not eligible from now on
@@ -992,7 +998,7 @@ static int scratch_for(hipspmv_t* h, hipStream_t s, bool capturing, int kernel, 
   auto has = [&](const hipspmv_handle::Scratch& c) {
     if (kernel == HIPSPMV_KERNEL_SELL) return c.sell_tickets && c.sell_partial;
     if (kernel == HIPSPMV_KERNEL_WCSR) return c.wc_ypart != nullptr;
-    if (kernel == HIPSPMV_KERNEL_VFLOW) return c.vf_tickets && c.vf_partial;
+    if (kernel == HIPSPMV_KERNEL_VCACHE_FLOW) return c.vf_tickets && c.vf_partial;
     return c.vc_tickets[k] && c.vc_partial[k];
   };
   constexpr int NS = hipspmv_handle::kScratchSets;
@@ -1035,7 +1041,7 @@ static int scratch_for(hipspmv_t* h, hipStream_t s, bool capturing, int kernel, 
       if ((st = alloc(&c.sell_partial, 8ull * h->sell.npieces, true))) return st;
     } else if (kernel == HIPSPMV_KERNEL_WCSR) {
       if ((st = alloc(&c.wc_ypart, 8ull * h->wc.nseg, false))) return st;
-    } else if (kernel == HIPSPMV_KERNEL_VFLOW) {
+    } else if (kernel == HIPSPMV_KERNEL_VCACHE_FLOW) {
       if ((st = alloc(&c.vf_tickets, 4ull * h->vf.ticket_words, true))) return st;
       if ((st = alloc(&c.vf_partial, h->vf.partial_bytes, false))) return st;
     } else {
@@ -1052,7 +1058,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   hipError_t e = hipSuccess;
   if (mode == HIPSPMV_MODE_AUTO) mode = h->mode_opt;
   const bool scratch = kernel == HIPSPMV_KERNEL_VCACHE_SPLIT || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4 ||
-                       kernel == HIPSPMV_KERNEL_WCSR || kernel == HIPSPMV_KERNEL_VFLOW ||
+                       kernel == HIPSPMV_KERNEL_WCSR || kernel == HIPSPMV_KERNEL_VCACHE_FLOW ||
                        (kernel == HIPSPMV_KERNEL_SELL && h->sell.npieces &&
                         (mode != HIPSPMV_MODE_ORDERED || h->dtype == HIPSPMV_U64));
   // the stream's own combine scratch: nothing is recorded or waited on between
@@ -1128,7 +1134,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     } else {
       e = launch_vcache(h->dtype, a, s);
     }
-  } else if (kernel == HIPSPMV_KERNEL_VFLOW) {
+  } else if (kernel == HIPSPMV_KERNEL_VCACHE_FLOW) {
     const auto& f = h->vf;
     VflowArgs a{f.d_wbeg,  f.d_wend, f.d_code,   f.d_vals,        d_x,       d_y_in,    d_y_out,
                 sc->vf_partial, sc->vf_tickets, f.d_status, h->rows, h->cols, f.rows_per_block, f.nblocks,
@@ -1206,7 +1212,7 @@ static std::string kernel_symbol(const hipspmv_t* h) {
     case HIPSPMV_KERNEL_CSR_LANE: return "k_csr_lane<" + T + ">";
     case HIPSPMV_KERNEL_CSR_VECTOR: return "k_csr_vector<" + T + ", false>";
     case HIPSPMV_KERNEL_WCSR: return "k_csr_vector<" + T + ", true>";
-    case HIPSPMV_KERNEL_VFLOW: return "k_vflow<" + T + ",";
+    case HIPSPMV_KERNEL_VCACHE_FLOW: return "k_vflow<" + T + ",";
     case HIPSPMV_KERNEL_SELL: return "k_sell";
     default: return "hipspmv::";
   }
@@ -1309,16 +1315,20 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   if (!h || !key) return HIPSPMV_ERR_INVALID_ARG;
   const std::string k(key);
   if (k == "kernel") {
-    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_VFLOW) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_VCACHE_FLOW) return HIPSPMV_ERR_INVALID_ARG;
+    if ((value == HIPSPMV_KERNEL_VCACHE_SPLIT4 || value == HIPSPMV_KERNEL_VCACHE_FLOW) && !kExperimental)
+      return HIPSPMV_ERR_UNSUPPORTED;
     if (value == HIPSPMV_KERNEL_VCACHE && !h->vc0_eligible) return HIPSPMV_ERR_UNSUPPORTED;
     if (value == HIPSPMV_KERNEL_WGATHER && !h->wg_eligible) return HIPSPMV_ERR_UNSUPPORTED;
     if (int st = ensure_layout(h, (int)value)) return st;
     h->kernel_opt = (int)value;
   } else if (k == "vcache_dma") {
     if (value < -1 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
+    if (value == 1 && !kExperimental) return HIPSPMV_ERR_UNSUPPORTED;  // (the split geometry's loaders are DMA)
     h->vcache_dma = (int)value;
   } else if (k == "vcache_map") {  // 1: split4 XCD pairs; 2: split, one column part per XCD where it can
     if (value < 0 || value > 2) return HIPSPMV_ERR_INVALID_ARG;
+    if (value && !kExperimental) return HIPSPMV_ERR_UNSUPPORTED;
     h->vcache_map = (int)value;
   } else if (k == "vflow_map") {  // 1: k_vflow's column part h on XCDs 2h and 2h + 1
     if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
@@ -1343,6 +1353,7 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
     h->vcache_xmask = (int)value;
   } else if (k == "vquad_variant") {  // k_vquad configuration (csrc/vquad.hip)
     if (value < 0 || value > 26) return HIPSPMV_ERR_INVALID_ARG;
+    if (!kExperimental) return HIPSPMV_ERR_UNSUPPORTED;
     // 6-16 are timing ablations that give wrong y (or race): experimental builds only
     const char* exp = std::getenv("HIPSPMV_EXPERIMENTAL");
     if (value >= 6 && value <= 16 && !(exp && std::strcmp(exp, "1") == 0)) return HIPSPMV_ERR_UNSUPPORTED;
@@ -1378,6 +1389,8 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
     h->vcache_nt = value;
   } else if (k == "vcache_xlane") {
     if (value < -1 || value > 6) return HIPSPMV_ERR_INVALID_ARG;
+    // the product build has the split geometry's 0 / 3 / 5 (and the ordered geometry's 0, which 6 shares)
+    if ((value == 1 || value == 2 || value == 4) && !kExperimental) return HIPSPMV_ERR_UNSUPPORTED;
     h->vcache_xlane = (int)value;
   } else if (k == "mode") {
     if (value != HIPSPMV_MODE_ORDERED && value != HIPSPMV_MODE_FAST) return HIPSPMV_ERR_INVALID_ARG;
@@ -1654,7 +1667,7 @@ const char* hipspmv_kernel_name(hipspmv_t* h, int mode) {
     case HIPSPMV_KERNEL_CSR_VECTOR: return "csr_vector";
     case HIPSPMV_KERNEL_SELL: return "sell";
     case HIPSPMV_KERNEL_WCSR: return "wcsr";
-    case HIPSPMV_KERNEL_VFLOW: return "vcache_flow";
+    case HIPSPMV_KERNEL_VCACHE_FLOW: return "vcache_flow";
     default: return "unsupported";
   }
 }
@@ -1726,6 +1739,8 @@ const char* hipspmv_strerror(int status) {
 const char* hipspmv_last_error(void) { return g_last_error.c_str(); }
 
 int hipspmv_abi_version(void) { return HIPSPMV_ABI_VERSION; }
+
+int hipspmv_build_flags(void) { return kExperimental ? HIPSPMV_BUILD_EXPERIMENTAL : 0; }
 
 int hipspmv_device_count(int* count) {
   if (!count) return HIPSPMV_ERR_INVALID_ARG;

@@ -723,6 +723,8 @@ static void launch_one(const VcacheArgs& a, hipStream_t s) {
                      a.xmask);
 }
 
+#ifdef HIPSPMV_EXPERIMENTAL_KERNELS
+// every form (make EXPERIMENTAL=1: lib/exp/libhipspmv.so, loaded under HIPSPMV_EXPERIMENTAL=1)
 template <typename T, int SPLIT, int MAP = 0>
 static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
   if constexpr (SPLIT == 3) {  // three loader waves: LDS-DMA only (a register-staged panel would spill)
@@ -754,6 +756,7 @@ static void dispatch(const VcacheArgs& a, hipStream_t s, int ld, int cx) {
     ld == 1 ? launch_one<T, SPLIT, 1, 3, MAP>(a, s) : launch_one<T, SPLIT, 0, 3, MAP>(a, s);
   }
 }
+#endif
 
 template <typename T>
 hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
@@ -787,6 +790,26 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   // loader waves always stage by LDS-DMA (dispatch)
   const int dma = a.dma < 0 ? 0 : a.dma;
   const int ld = dma ? 1 : cx == 2 ? 2 : 0;
+  (void)ld;
+#ifndef HIPSPMV_EXPERIMENTAL_KERNELS
+  // the product build instantiates what AUTO runs: the ordered geometry with its
+  // register-staged loaders (CX 0; the ordered forms of the continuation options are experimental), the
+  // split geometry with LDS-DMA loaders and the continuation its layout allows (5, else 3, else 0)
+  if (a.split == 1 && !dma) {
+    launch_one<T, 1, 0, 0>(a, s);
+    return hipGetLastError();
+  }
+  if (a.split == 3 && a.map == 0 && (cx == 0 || cx == 3 || cx == 5)) {
+    if (cx == 5)
+      launch_one<T, 3, 1, 5>(a, s);
+    else if (cx == 3)
+      launch_one<T, 3, 1, 3>(a, s);
+    else
+      launch_one<T, 3, 1, 0>(a, s);
+    return hipGetLastError();
+  }
+  return hipErrorNotSupported;
+#else
   if (a.split == 1)
     dispatch<T, 1>(a, s, ld, cx);
   else if (a.split == 3 && a.map == 2 && cx == 5)  // (option "vcache_map" 2)
@@ -800,6 +823,7 @@ hipError_t launch_vcache(const VcacheArgs& a, hipStream_t s) {
   else  // four parts otherwise: k_vquad (csrc/vquad.hip) runs that layout
     return hipErrorInvalidValue;
   return hipGetLastError();
+#endif
 }
 
 hipError_t launch_vcache(int dtype, const VcacheArgs& a, hipStream_t s) {

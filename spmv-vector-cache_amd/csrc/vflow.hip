@@ -39,12 +39,13 @@
 
 namespace hipspmv {
 
+#ifdef HIPSPMV_EXPERIMENTAL_KERNELS
 namespace {
 constexpr int kVfVT = 1024;
 constexpr uint32_t kVfSpinMax = 1u << 18;      // ~20 ms of s_sleep 1 polls: a wait past it is a fault
 constexpr uint32_t kVfPairs = (uint32_t)kVfGeom.panel / 2;  // 16-byte chunks per panel
-constexpr int kVfNdma = (int)(kVfPairs / 64 / kVfLoaders);  // wave-instructions per loader and panel
-static_assert(kVfPairs % (64 * kVfLoaders) == 0, "a panel is whole DMA wave-instructions per loader");
+constexpr int kVfNdma = (int)(kVfPairs / 64);  // DMA wave-instructions per panel (one loader loads a panel)
+static_assert(kVfPairs % 64 == 0, "a panel is whole DMA wave-instructions");
 static_assert(kVfGeom.rows * 8 + kVfSlots * kVfGeom.panel * 8 + 64 <= 163840, "LDS budget");
 static_assert(kVfLoaders + kVfWaves == kVfVT / 64, "wave roles");
 
@@ -97,8 +98,8 @@ __global__ __launch_bounds__(kVfVT) void k_vflow(const uint32_t* __restrict__ wb
   constexpr int WL = kVfLoaders, WC = kVfWaves;
   __shared__ alignas(16) T ylds[VR];
   __shared__ alignas(16) T xb[NS][VP];
-  // [0, NS * WL): full[slot][loader] = 1 + the last panel published there; [8, 8 + NS): freed[slot] =
-  // compute-wave releases of that slot so far; [11, 17): the combine's scratch (owner_combine)
+  // [0, NS): full[slot] = 1 + the last panel published there; [8, 8 + NS): freed[slot] = compute-wave
+  // releases of that slot so far; [8, 14): the combine's scratch once the main loop is over
   __shared__ uint32_t flags[16];
   uint32_t* const full = flags;
   uint32_t* const freed = flags + 8;
@@ -129,9 +130,11 @@ __global__ __launch_bounds__(kVfVT) void k_vflow(const uint32_t* __restrict__ wb
   const uint64_t t_begin = PROF ? tnow() : 0;
 
   if (wave < (uint32_t)WL) {
-    // ---- loader wave: panel s of the part into slot s % NS, this wave's chunks
-    // c = j * WL + wave (64 16-byte pairs each, clamped in bounds; odd cols: the
-    // last element patched after the DMA landed, by the lane owning its pair)
+    // ---- loader wave wl: the panels s = wl, wl + WL, ... of the part, each whole
+    // into slot s % NS (64 16-byte pairs per wave-instruction, clamped in bounds;
+    // odd cols: the last element patched after the DMA landed, by the lane owning
+    // its pair), published as soon as it landed -- so WL panels are in flight
+    // and no publish waits for a later panel's slot
     const uint32_t cmax = (cols - 2) & ~1u;
     const T xlast = x[cols - 1];
     auto dma = [&](uint32_t s) {
@@ -139,40 +142,36 @@ __global__ __launch_bounds__(kVfVT) void k_vflow(const uint32_t* __restrict__ wb
       T* slot = xb[s % NS];
 #pragma unroll
       for (int j = 0; j < kVfNdma; ++j) {
-        const uint32_t c0 = (j * WL + wave) * 64;
+        const uint32_t c0 = j * 64;
         __builtin_amdgcn_global_load_lds((const void*)(x + min(base + 2 * (c0 + lane), cmax)),
                                          (__attribute__((address_space(3))) void*)(slot + 2 * c0), 16, 0, 0);
       }
     };
-    auto publish = [&](uint32_t s) {  // panel s landed (this wave's part): patch, then its full word
+    auto publish = [&](uint32_t s) {  // panel s landed: patch, then its full word
       if ((cols & 1) && p0 + s == npanels - 1) {
         const uint32_t sl = cols - 1 - (p0 + s) * VP, c = sl >> 1;
-        if ((c / 64) % WL == wave && (c & 63) == lane) xb[s % NS][sl] = xlast;
+        if ((c & 63) == lane) xb[s % NS][sl] = xlast;
       }
       // (no release fence: at workgroup scope it waits vmcnt(0) -- for the next panel's DMA too.  The
       // vm_wait before this retired the panel's LDS-DMA writes, and the asm's memory clobber keeps this
       // store after it)
-      if (lane == 0) vf_lds_store(&full[(s % NS) * WL + wave], s + 1);
+      if (lane == 0) vf_lds_store(&full[s % NS], s + 1);
     };
     bool ok = true;
-    for (uint32_t s = 0; s < npu; ++s) {
+    for (uint32_t s = wave; s < npu; s += WL) {
       // the slot's previous panel (s - NS) released by every compute wave
       const uint64_t ta = PROF ? tnow() : 0;
       if (s >= (uint32_t)NS) ok = ok && vf_wait_ge(&freed[s % NS], (uint32_t)WC * (s / NS));
       const uint64_t tb = PROF ? tnow() : 0;
       dma(s);
-      if (s >= 1) {
-        vm_wait<kVfNdma>();  // panel s - 1's DMA landed (panel s's still in flight)
-        publish(s - 1);
-      }
+      vm_wait<0>();  // (this wave's only loads in flight)
+      publish(s);
       if (PROF) {
         const uint64_t tc = tnow();
         pc[0] += tb - ta;
         pc[1] += tc - tb;
       }
     }
-    vm_wait<0>();
-    publish(npu - 1);
     if (!ok && lane == 0) __hip_atomic_fetch_or(status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     // ---- compute wave cw: its groups of the unit's steps, DE steps ahead
@@ -184,10 +183,14 @@ __global__ __launch_bounds__(kVfVT) void k_vflow(const uint32_t* __restrict__ wb
       constexpr int aux = decltype(ntc)::value ? 2 : 0;  // nt: kept out of the Infinity Cache
       uint32_t EC[DE][2], NB[DE];
       T EV[DE][2];
-      auto load = [&](uint32_t s, uint32_t* c, T* v, uint32_t& n) {
+      // the group bounds of step s (scalar loads), one step before its entry loads need them
+      auto bounds = [&](uint32_t s, uint32_t& e0, uint32_t& n) {
         const uint32_t k = min(s, npad - 1);
-        const uint32_t e0 = gb[k];
+        e0 = gb[k];
         n = s < npu ? ge[k] - e0 : 0u;
+      };
+      auto load = [&](uint32_t e0, uint32_t n0, uint32_t* c, T* v, uint32_t& n) {
+        n = n0;
         const __amdgpu_buffer_rsrc_t dc = buf_rsrc(ecode + e0, 4 * n), dv = buf_rsrc(evals + e0, 8 * n);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {  // lanes past the group: out of the descriptor, no request
@@ -241,17 +244,20 @@ __global__ __launch_bounds__(kVfVT) void k_vflow(const uint32_t* __restrict__ wb
         }
       };
       bool ok = true;
+      uint32_t be0, bn;
 #pragma unroll
-      for (int i = 0; i < DE; ++i) load((uint32_t)i, EC[i], EV[i], NB[i]);
+      for (int i = 0; i < DE; ++i) {
+        bounds((uint32_t)i, be0, bn);
+        load(be0, bn, EC[i], EV[i], NB[i]);
+      }
+      bounds((uint32_t)DE, be0, bn);
       for (uint32_t base = 0; base < nsteps; base += DE) {
 #pragma unroll
         for (int i = 0; i < DE; ++i) {
           const uint32_t s = base + i;
           uint64_t ta = PROF ? tnow() : 0, tb = ta, tc = ta;
           if (s < npu) {
-            const uint32_t* fs = &full[(s % NS) * WL];
-            ok = ok && vf_wait_ge(fs, s + 1);  // after one wait gave up, none waits again: the launch ends
-            ok = ok && vf_wait_ge(fs + 1, s + 1);
+            ok = ok && vf_wait_ge(&full[s % NS], s + 1);  // after one wait gave up, none waits again
             if (PROF) tb = tnow();
             apply(s, EC[i], EV[i], NB[i]);
             // every x read of the slot retired, then release it to the loaders
@@ -259,7 +265,8 @@ __global__ __launch_bounds__(kVfVT) void k_vflow(const uint32_t* __restrict__ wb
             if (lane == 0) __hip_atomic_fetch_add(&freed[s % NS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (PROF) tc = tnow();
           }
-          load(s + DE, EC[i], EV[i], NB[i]);
+          load(be0, bn, EC[i], EV[i], NB[i]);  // step s + DE
+          bounds(s + DE + 1, be0, bn);
           if (PROF) {
             const uint64_t td = tnow();
             pc[0] += tb - ta;
@@ -325,5 +332,11 @@ hipError_t launch_vflow(int dtype, const VflowArgs& a, hipStream_t s) {
     go(double{});
   return hipGetLastError();
 }
+
+#else
+// the product build: AUTO does not pick k_vflow -- built with make
+// EXPERIMENTAL=1 only (lib/exp/libhipspmv.so); here selecting it reports "unsupported"
+hipError_t launch_vflow(int, const VflowArgs&, hipStream_t) { return hipErrorNotSupported; }
+#endif
 
 }  // namespace hipspmv

@@ -45,6 +45,7 @@
 
 namespace hipspmv {
 
+#ifdef HIPSPMV_EXPERIMENTAL_KERNELS
 namespace {
 
 constexpr int VR = kVcQuad.rows, VP = kVcQuad.panel, SPLIT = 4;
@@ -409,5 +410,11 @@ uint32_t vquad_max_window(int variant) { return vquad_window(variant); }
 hipError_t launch_vquad(int dtype, const VcacheArgs& a, hipStream_t s) {
   return dtype ? launch_vquad_t<uint64_t>(a, s) : launch_vquad_t<double>(a, s);
 }
+#else
+// the product build: k_vquad is never chosen by AUTO -- built with make
+// EXPERIMENTAL=1 only (lib/exp/libhipspmv.so); here selecting it reports "unsupported"
+uint32_t vquad_max_window(int) { return 0; }
+hipError_t launch_vquad(int, const VcacheArgs&, hipStream_t) { return hipErrorNotSupported; }
+#endif
 
 }  // namespace hipspmv

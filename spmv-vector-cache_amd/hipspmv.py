@@ -86,9 +86,12 @@ def load_hipspmv() -> C.CDLL:
     global _hip
     if _hip is not None:
         return _hip
-    path = os.path.join(LIB_DIR, "libhipspmv.so")
+    # HIPSPMV_EXPERIMENTAL=1: the build with every kernel form (make EXPERIMENTAL=1), else the product
+    exp = os.environ.get("HIPSPMV_EXPERIMENTAL") == "1"
+    path = os.path.join(LIB_DIR, "exp", "libhipspmv.so") if exp else os.path.join(LIB_DIR, "libhipspmv.so")
     if not os.path.exists(path):
-        raise FileNotFoundError(f"{path} missing: build with `make -C {PKG_DIR}` (no CPU fallback exists)")
+        raise FileNotFoundError(f"{path} missing: build with `make -C {PKG_DIR}{' EXPERIMENTAL=1' if exp else ''}` "
+                                "(no CPU fallback exists)")
     lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
     vp = C.c_void_p
     lib.hipspmv_create.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.POINTER(vp)]
@@ -101,6 +104,7 @@ def load_hipspmv() -> C.CDLL:
     lib.hipspmv_kernel_name.restype = C.c_char_p
     lib.hipspmv_destroy.argtypes = [vp]
     lib.hipspmv_release_wait.argtypes = []
+    lib.hipspmv_build_flags.argtypes = []
     lib.hipspmv_pmc_counter.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_double),
                                         C.POINTER(C.c_uint64)]
     lib.hipspmv_attach_pmc.argtypes = [vp, C.c_char_p]
@@ -130,7 +134,7 @@ def load_hipspmv() -> C.CDLL:
                  "hipspmv_multi_set_option", "hipspmv_multi_exec", "hipspmv_multi_stat", "hipspmv_multi_destroy"):
         getattr(lib, name).restype = C.c_int
     for name in ("hipspmv_create", "hipspmv_create_csr", "hipspmv_set_option", "hipspmv_exec",
-                 "hipspmv_exec_device", "hipspmv_stat", "hipspmv_destroy", "hipspmv_release_wait", "hipspmv_abi_version",
+                 "hipspmv_exec_device", "hipspmv_stat", "hipspmv_destroy", "hipspmv_release_wait", "hipspmv_build_flags", "hipspmv_abi_version",
                  "hipspmv_device_count", "hipspmv_prep_stats", "hipspmv_mark_row_starts"):
         getattr(lib, name).restype = C.c_int
     _hip = lib
@@ -629,3 +633,9 @@ def release_wait() -> None:
     """Until every handle destroyed so far has had its device memory released
     (hipspmv_release_wait; destroy itself returns at once)."""
     _check(load_hipspmv().hipspmv_release_wait(), "release_wait")
+
+
+def experimental_build() -> bool:
+    """True when the loaded library carries the kernel forms AUTO never picks
+    (hipspmv_build_flags; make EXPERIMENTAL=1, loaded under HIPSPMV_EXPERIMENTAL=1)."""
+    return bool(load_hipspmv().hipspmv_build_flags() & 1)

@@ -77,12 +77,12 @@ static bool replay(const char* name, const HostCSR& a, const std::vector<T>& x, 
     std::vector<int> owner(kVfGeom.rows, -1);
     std::vector<T> xs(VP);
     for (uint32_t s = 0; s < npu; ++s) {
-      // the loaders' DMA: chunk c = j * WL + wl, lane pairs clamped to cmax
+      // the DMA of loader wave s % WL (the whole panel): chunk j, lane pairs clamped to cmax
       std::vector<int> filled(VP, 0);
-      for (uint32_t wl = 0; wl < WL; ++wl)
-        for (uint32_t j = 0; j < VP / 2 / 64 / WL; ++j)
+      CHECK(s % WL < WL, "loader");
+      for (uint32_t j = 0; j < VP / 2 / 64; ++j)
           for (uint32_t lane = 0; lane < 64; ++lane) {
-            const uint32_t c0 = (j * WL + wl) * 64, pr = c0 + lane;
+            const uint32_t c0 = j * 64, pr = c0 + lane;
             const uint32_t src = std::min((p0 + s) * VP + 2 * pr, cmax);
             CHECK(src + 1 < cols, "x pair %u past cols %u", src, cols);
             CHECK(2 * pr + 1 < VP, "slot index %u", 2 * pr);

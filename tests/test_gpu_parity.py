@@ -513,6 +513,8 @@ def test_c3_split_deterministic_and_within_bound(gpu):
 
 @pytest.mark.parametrize("vmap", [0, 1])
 def test_vflow_c3_full_size(gpu, vmap):
+    if not hs.experimental_build():
+        pytest.skip("k_vflow: experimental build only (HIPSPMV_EXPERIMENTAL=1)")
     # k_vflow (csrc/vflow.hip) on full C3: 64 row blocks x 4 parts = 256 units, x streamed into LDS
     # 64 x 8 MB per launch; deterministic (identical bits on every launch and under either XCD
     # placement), within the FAST bound of the oracle, u64 exact, no flag wait gave up
@@ -585,6 +587,8 @@ def test_split_combine_concurrent_streams(gpu):
 # forced combine fallback (variant 20) counted
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26])
 def test_vquad_variants(gpu, variant):  # configurations: x / entry ring depths (csrc/vquad.hip)
+    if not hs.experimental_build():
+        pytest.skip("k_vquad: experimental build only (HIPSPMV_EXPERIMENTAL=1)")
     cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20), (20000, 1 << 22),
              (16385, 7937)]
     ran = 0
@@ -643,6 +647,8 @@ def test_vquad_variants(gpu, variant):  # configurations: x / entry ring depths 
 
 @pytest.mark.parametrize("xlane", [3, 4])
 def test_vcache_split_entry_loads(gpu, xlane):  # 3: clamped entry loads; 4: masked past the segment
+    if xlane == 4 and not hs.experimental_build():
+        pytest.skip("vcache_xlane 4: experimental build only (HIPSPMV_EXPERIMENTAL=1)")
     cases = [(1 << 20, 1 << 20), (70001, 13001), (3000, 20001), (65536, 1 << 20), (16385, 12001)]
     ran = 0
     for rows, cols in cases:
@@ -732,6 +738,8 @@ def test_ordered_vcache_continuation_and_xmask(gpu, xlane, xmask):
 
 
 def test_vquad_c3_full_size(gpu):
+    if not hs.experimental_build():
+        pytest.skip("k_vquad: experimental build only (HIPSPMV_EXPERIMENTAL=1)")
     # the four-part kernel on full C3: x streamed into LDS per launch is 64 row
     # blocks x 8 MB (three parts: 85 x 8 MB); deterministic and within the bound
     n = 1 << 20
@@ -755,7 +763,7 @@ def test_vquad_c3_full_size(gpu):
 # and the LDS-DMA x loader.  Addressing is replayed on the CPU by
 # tests/test_vcache_sim.py; on the GPU they run only with HIPSPMV_EXPERIMENTAL=1
 # until they have been measured on an MI355X.
-EXPERIMENTAL = os.environ.get("HIPSPMV_EXPERIMENTAL") == "1"
+EXPERIMENTAL = os.environ.get("HIPSPMV_EXPERIMENTAL") == "1"  # (the library is then lib/exp's)
 
 
 @pytest.mark.skipif(not EXPERIMENTAL, reason="experimental kernels: set HIPSPMV_EXPERIMENTAL=1")
