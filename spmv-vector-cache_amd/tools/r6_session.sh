@@ -25,6 +25,12 @@ for s in ${STEPS:-streams}; do
     vflow) step pytest_vflow 300 $PYT -m gpu tests/test_gpu_parity.py -k "vcache_flow or vflow" ;;
     vfprof) step vf_prof 300 python -u spmv-vector-cache_amd/tools/vf_prof.py ${VFPROF_ARGS:-} ;;
     vfab) step vf_ab 300 python -u spmv-vector-cache_amd/tools/vf_ab.py ${VFAB_ARGS:-} ;;
+    pmcord) KERNELS=vcache WORKLOAD=c3 step pmc_ordered 600 bash spmv-vector-cache_amd/tools/gpurun_pmc.sh &&
+            step pmc_ordered_summary 60 python3 spmv-vector-cache_amd/tools/pmc_summary.py $OUT/pmc_c3_vcache_summary.csv "k_vcache<double, 1," $OUT/pmc_c3_vcache_*/*counter_collection.csv ;;
+    destroy) HIPSPMV_SYNC_RELEASE=1 step destroy_sync 300 python -u spmv-vector-cache_amd/tools/destroy_probe.py &&
+             step destroy_deferred 300 python -u spmv-vector-cache_amd/tools/destroy_probe.py &&
+             HIPSPMV_SYNC_RELEASE=1 step destroy_sync_trace 300 rocprofv3 --kernel-trace -d $OUT/destroy_sync -o run --output-format csv -- python3 spmv-vector-cache_amd/tools/destroy_probe.py &&
+             step destroy_deferred_trace 300 rocprofv3 --kernel-trace -d $OUT/destroy_deferred -o run --output-format csv -- python3 spmv-vector-cache_amd/tools/destroy_probe.py ;;
     pytest) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;
     bench20) step bench20 600 python bench.py --steps 20 --warmup 5 ;;
