@@ -90,6 +90,11 @@ extern "C" {
                                  8192+ entries as isolated chains, a 1024-thread
                                  workgroup each); ordered in ORDERED mode (FAST:
                                  long rows cut into pieces); any matrix */
+#define HIPSPMV_KERNEL_WGATHER_SPLIT 10 /* "wgather_split": k_wgather over two column
+                                  halves of 16384-row blocks, part 0 on XCDs 0-3 and
+                                  part 1 on XCDs 4-7, y = p0 + p1; fast,
+                                  deterministic; chosen by AUTO (FAST) for wide x
+                                  with at most 2^21 rows (a C4 shard) */
 
 typedef struct hipspmv_handle hipspmv_t;
 
@@ -184,7 +189,8 @@ int hipspmv_exec_device(hipspmv_t *h, const void *d_x, const void *d_y_in, void 
  * "vcache_split_units" "vcache_split_rows_per_block" "vcache_x_bytes"
  * "vcache_split_x_bytes" (x bytes one launch streams into LDS)
  * "vcache_split4_eligible" "vcache_split4_x_bytes" "wgather_eligible"
- * "wgather_windows" "row_groups" "sell_slices" "sell_hubs" "sell_hub_pieces"
+ * "wgather_windows" "wgather_split_eligible" "wgather_split_rows_per_block"
+ * "wgather_split_units" "row_groups" "sell_slices" "sell_hubs" "sell_hub_pieces"
  * "sell_padding" "sell_iso_hubs" (SELL layout, 0 until the sell kernel is
  * selected) "wcsr_segments" "wcsr_max_segment" "wcsr_window_log2"
  * "wcsr_chunks" (wcsr layout)

@@ -181,7 +181,8 @@ struct hipspmv_handle {
     int split = 1;
     bool row_runs = false;  // place_segments_banked: runs inside 16-lane rows (xlane 5 applies)
     bool vc4 = false;       // [2] built for k_vcache's four-part geometry (HIPSPMV_SPLIT4_VCACHE=1), not k_vquad
-  } vc[4];  // [0] ordered (kVcOrdered), [1] split (kVcSplit); experimental: [2] split4; [3] wgather windows
+  } vc[5];  // [0] ordered (kVcOrdered), [1] split (kVcSplit); experimental: [2] split4; [3] wgather windows,
+            // [4] wgather_split (kWgSplit)
   struct Vf {  // k_vflow layout (build_vflow), built on first selection ("kernel" VFLOW) or by AUTO
     bool ok = false, tried = false;
     uint32_t *d_code = nullptr, *d_wbeg = nullptr, *d_wend = nullptr, *d_tickets = nullptr;
@@ -205,6 +206,7 @@ struct hipspmv_handle {
   // picks the kernel, else on first selection by name
   bool wg_eligible = false;
   uint32_t wg_max_run = 0;
+  bool wgs_eligible = false;  // the two-part form (kWgSplit): wgather-eligible, <= 2^21 rows
   struct Sell {  // k_sell layout: built at create when AUTO picks SELL, else on first selection
     bool built = false;
     uint64_t* d_off = nullptr;
@@ -302,8 +304,8 @@ struct hipspmv_handle {
     bool assigned = false;
     uintptr_t sid = 0;  // the stream's handle value (NULL: the default stream)
     uint64_t last = 0;  // LRU tick
-    uint32_t* vc_tickets[3] = {nullptr, nullptr, nullptr};
-    uint64_t* vc_partial[3] = {nullptr, nullptr, nullptr};
+    uint32_t* vc_tickets[5] = {};  // per vc[] layout (split geometries: 1, 2, 4)
+    uint64_t* vc_partial[5] = {};
     uint32_t* sell_tickets = nullptr;
     uint64_t* sell_partial = nullptr;
     uint64_t* wc_ypart = nullptr;
@@ -346,7 +348,7 @@ static void release(hipspmv_t* h) {
                            h->vf.d_status});
   for (int i = 1; i < hipspmv_handle::kScratchSets; ++i) {  // set 0 is the layouts' own (above)
     auto& c = h->scratch[i];
-    for (int k = 0; k < 3; ++k) ptrs.insert(ptrs.end(), {c.vc_tickets[k], c.vc_partial[k]});
+    for (int k = 0; k < 5; ++k) ptrs.insert(ptrs.end(), {c.vc_tickets[k], c.vc_partial[k]});
     ptrs.insert(ptrs.end(), {c.sell_tickets, c.sell_partial, c.wc_ypart, c.vf_tickets, c.vf_partial});
   }
   std::vector<void*> evs;
@@ -387,7 +389,7 @@ static int upload_vc(hipspmv_t* h, int k, const HostCSR& a, const VcGeom& g, uin
   if (lanes) {  // k_vquad's placement (build_vcache_lanes); false: not placeable, not eligible
     if (!build_vcache_lanes(a, g, lanes, L)) return HIPSPMV_ERR_UNSUPPORTED;
   } else {
-    build_vcache(a, g, L, k == 3 && h->wgather_sort);  // k_wgather: gathers of one x line side by side
+    build_vcache(a, g, L, (k == 3 || k == 4) && h->wgather_sort);  // k_wgather: gathers of one x line side by side
     // the vector-cache geometries (ordered and split): rows of each segment
     // placed for LDS banks (plan.cpp place_segments_banked; every row keeps its
     // run and its column order, so the sums are bit-identical);
@@ -645,13 +647,14 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   return HIPSPMV_OK;
 }
 
-// The vcache-family layout k from the CSR `a` (k 0: ordered vcache, 3: wgather).
+// The vcache-family layout k from the CSR `a` (k 0: ordered vcache, 3: wgather, 4: wgather_split).
 static int build_vc_layout(hipspmv_t* h, int k, const HostCSR& a) {
   if (h->vc[k].ok) return HIPSPMV_OK;
   if (k == 0 && !h->vc0_eligible) return HIPSPMV_ERR_UNSUPPORTED;
   if (k == 3 && !h->wg_eligible) return HIPSPMV_ERR_UNSUPPORTED;
+  if (k == 4 && !h->wgs_eligible) return HIPSPMV_ERR_UNSUPPORTED;
   DeviceGuard g(h->device);
-  return upload_vc(h, k, a, k == 0 ? kVcOrdered : kWgWindow);
+  return upload_vc(h, k, a, k == 0 ? kVcOrdered : k == 3 ? kWgWindow : kWgSplit);
 }
 
 // AUTO, from the round-2 sweeps on MI355X:
@@ -682,6 +685,11 @@ static int auto_pick(const hipspmv_t* h, bool fast_ok, bool built) {
   // round 2 ran it)
   if (!fast_ok && worth(h->vc[0], h->vc0_eligible))
     return !built || h->vc[0].ok ? HIPSPMV_KERNEL_VCACHE : h->sell.built ? HIPSPMV_KERNEL_SELL : generic;
+  // FAST with at most 2^21 rows (a C4 shard): the two-part form, 16384-row
+  // blocks with each XCD's L2 holding half of x (2^21 x 2^24 stripe shard:
+  // DESIGN.md §6.18)
+  if (fast_ok && !h->vc0_eligible && h->wgs_eligible && h->wg_max_run <= kVcRunMax)
+    return !built || h->vc[4].ok ? HIPSPMV_KERNEL_WGATHER_SPLIT : generic;
   if (!h->vc0_eligible && h->wg_eligible && h->wg_max_run <= kVcRunMax)
     return !built || h->vc[3].ok ? HIPSPMV_KERNEL_WGATHER : generic;
   if (!fast_ok) return !built || h->sell.built ? HIPSPMV_KERNEL_SELL : generic;
@@ -745,6 +753,7 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   const bool split_ok = vcache_eligible(a, kVcSplit), quad_ok = vcache_eligible(a, kVcQuad);
   h->wg_eligible = vcache_eligible(a, kWgWindow);
   if (h->wg_eligible) h->wg_max_run = vcache_max_run(a, (uint32_t)kWgWindow.panel);
+  h->wgs_eligible = h->wg_eligible && a.rows <= 128u * (uint32_t)kWgSplit.rows && vcache_eligible(a, kWgSplit);
   if (a.cols >= kWcMinCols) h->wc_segments = windowed_segments(a, kWcLog2Window);
   h->setup_scan_ns = now_ns() - t0;
   t0 = now_ns();
@@ -761,6 +770,7 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
     try {  // a host allocation failure in a layout build is an OOM like a device one
       if (k == HIPSPMV_KERNEL_SELL) st = build_sell_layout(h, a);
       else if (k == HIPSPMV_KERNEL_WGATHER) st = build_vc_layout(h, 3, a);
+      else if (k == HIPSPMV_KERNEL_WGATHER_SPLIT) st = build_vc_layout(h, 4, a);
       else if (k == HIPSPMV_KERNEL_VCACHE) st = build_vc_layout(h, 0, a);
       else if (k == HIPSPMV_KERNEL_WCSR) st = build_wcsr_layout(h, a);
       else st = HIPSPMV_OK;
@@ -844,6 +854,9 @@ static int choose_kernel(const hipspmv_t* h, int mode) {
       return h->vc[2].ok || h->vq_eligible ? HIPSPMV_KERNEL_VCACHE_SPLIT4 : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_WGATHER:  // ordered: valid in both modes
       return h->vc[3].ok || h->wg_eligible ? HIPSPMV_KERNEL_WGATHER : -HIPSPMV_ERR_UNSUPPORTED;
+    case HIPSPMV_KERNEL_WGATHER_SPLIT:
+      if (!fast_ok) return -HIPSPMV_ERR_UNSUPPORTED;
+      return h->vc[4].ok || h->wgs_eligible ? HIPSPMV_KERNEL_WGATHER_SPLIT : -HIPSPMV_ERR_UNSUPPORTED;
     case HIPSPMV_KERNEL_CSR_LANE:
       return HIPSPMV_KERNEL_CSR_LANE;
     case HIPSPMV_KERNEL_SELL:  // ordered: valid in both modes
@@ -918,6 +931,7 @@ static int build_vflow_layout(hipspmv_t* h, const HostCSR& a) {
 static int ensure_layout(hipspmv_t* h, int kernel) {
   const bool need = (kernel == HIPSPMV_KERNEL_SELL && !h->sell.built) ||
                     (kernel == HIPSPMV_KERNEL_WGATHER && !h->vc[3].ok) ||
+                    (kernel == HIPSPMV_KERNEL_WGATHER_SPLIT && !h->vc[4].ok) ||
                     (kernel == HIPSPMV_KERNEL_VCACHE && !h->vc[0].ok) ||
                     (kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4 && !h->vc[2].ok) ||
                     (kernel == HIPSPMV_KERNEL_WCSR && !h->wc.built) ||
@@ -944,7 +958,7 @@ static int ensure_layout(hipspmv_t* h, int kernel) {
                    : upload_vc(h, 2, a, kVcQuad, kVqLanes);
         if (!st) h->vc[2].vc4 = vc4;
         if (st == HIPSPMV_ERR_UNSUPPORTED) h->vq_eligible = false;
-      } else st = build_vc_layout(h, kernel == HIPSPMV_KERNEL_WGATHER ? 3 : 0, a);
+      } else st = build_vc_layout(h, kernel == HIPSPMV_KERNEL_WGATHER ? 3 : kernel == HIPSPMV_KERNEL_WGATHER_SPLIT ? 4 : 0, a);
     }
   } catch (const std::bad_alloc&) {
     drop_partial_layouts(h);
@@ -974,7 +988,7 @@ static uint32_t resident_blocks(uint32_t nblocks, uint64_t nnz) {
 // Set 0 of the combine scratch: the buffers the layouts allocated.
 static void scratch_set0(hipspmv_t* h) {
   auto& c = h->scratch[0];
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < 5; ++k) {
     c.vc_tickets[k] = h->vc[k].d_tickets;
     c.vc_partial[k] = h->vc[k].d_partial;
   }
@@ -1058,6 +1072,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   hipError_t e = hipSuccess;
   if (mode == HIPSPMV_MODE_AUTO) mode = h->mode_opt;
   const bool scratch = kernel == HIPSPMV_KERNEL_VCACHE_SPLIT || kernel == HIPSPMV_KERNEL_VCACHE_SPLIT4 ||
+                       kernel == HIPSPMV_KERNEL_WGATHER_SPLIT ||
                        kernel == HIPSPMV_KERNEL_WCSR || kernel == HIPSPMV_KERNEL_VCACHE_FLOW ||
                        (kernel == HIPSPMV_KERNEL_SELL && h->sell.npieces &&
                         (mode != HIPSPMV_MODE_ORDERED || h->dtype == HIPSPMV_U64));
@@ -1068,7 +1083,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
   if (scratch) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(s, &cap));
-    const int k = kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1 : 2;
+    const int k = kernel == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1 : kernel == HIPSPMV_KERNEL_WGATHER_SPLIT ? 4 : 2;
     if (int st = scratch_for(h, s, cap != hipStreamCaptureStatusNone, kernel, k, &sc)) return st;
   }
   if (kernel == HIPSPMV_KERNEL_SELL) {
@@ -1146,11 +1161,14 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     a.prof = h->d_vfprof;
     h->resident_entry_bytes = 12ull * f.block_first[std::min(a.nt_from, f.nblocks)];
     e = launch_vflow(h->dtype, a, s);
-  } else if (kernel == HIPSPMV_KERNEL_WGATHER) {
-    const auto& v = h->vc[3];
-    VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,    nullptr,
-                 nullptr,     h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
-                 v.npad,      h->nnz - 1, 1,         beta, 0,       (uint32_t)kWgWindow.panel,
+  } else if (kernel == HIPSPMV_KERNEL_WGATHER || kernel == HIPSPMV_KERNEL_WGATHER_SPLIT) {
+    const int k = kernel == HIPSPMV_KERNEL_WGATHER ? 3 : 4;
+    const auto& v = h->vc[k];
+    VcacheArgs a{v.d_seg,     v.d_code,  v.d_vals,   d_x,           d_y_in,  d_y_out,
+                 sc ? sc->vc_partial[k] : nullptr,
+                 sc ? sc->vc_tickets[k] : nullptr,
+                 h->rows,   h->cols,    v.rows_per_block, v.nblocks, v.npanels, v.part_panels,
+                 v.npad,      h->nnz - 1, v.split,   beta, 0,       (uint32_t)kWgWindow.panel,
                  h->vcache_xlane, v.max_seg};
     a.chunk = h->wgather_chunk;
     // entries non-temporal unless option vcache_nt > 0 (full C4: 3391 us against 3594)
@@ -1209,6 +1227,7 @@ static std::string kernel_symbol(const hipspmv_t* h) {
     case HIPSPMV_KERNEL_VCACHE_SPLIT: return "k_vcache<" + T + ", 3,";
     case HIPSPMV_KERNEL_VCACHE_SPLIT4: return "k_vquad<" + T + ",";
     case HIPSPMV_KERNEL_WGATHER: return "k_wgather<" + T + ",";
+    case HIPSPMV_KERNEL_WGATHER_SPLIT: return "k_wgather_split<" + T + ",";
     case HIPSPMV_KERNEL_CSR_LANE: return "k_csr_lane<" + T + ">";
     case HIPSPMV_KERNEL_CSR_VECTOR: return "k_csr_vector<" + T + ", false>";
     case HIPSPMV_KERNEL_WCSR: return "k_csr_vector<" + T + ", true>";
@@ -1315,11 +1334,12 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   if (!h || !key) return HIPSPMV_ERR_INVALID_ARG;
   const std::string k(key);
   if (k == "kernel") {
-    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_VCACHE_FLOW) return HIPSPMV_ERR_INVALID_ARG;
+    if (value < HIPSPMV_KERNEL_AUTO || value > HIPSPMV_KERNEL_WGATHER_SPLIT) return HIPSPMV_ERR_INVALID_ARG;
     if ((value == HIPSPMV_KERNEL_VCACHE_SPLIT4 || value == HIPSPMV_KERNEL_VCACHE_FLOW) && !kExperimental)
       return HIPSPMV_ERR_UNSUPPORTED;
     if (value == HIPSPMV_KERNEL_VCACHE && !h->vc0_eligible) return HIPSPMV_ERR_UNSUPPORTED;
     if (value == HIPSPMV_KERNEL_WGATHER && !h->wg_eligible) return HIPSPMV_ERR_UNSUPPORTED;
+    if (value == HIPSPMV_KERNEL_WGATHER_SPLIT && !h->wgs_eligible) return HIPSPMV_ERR_UNSUPPORTED;
     if (int st = ensure_layout(h, (int)value)) return st;
     h->kernel_opt = (int)value;
   } else if (k == "vcache_dma") {
@@ -1563,6 +1583,9 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "vcache_max_run") *out = h->vc[0].max_run;
   else if (k == "vcache_split_max_run") *out = h->vc[1].max_run;
   else if (k == "wgather_windows") *out = h->vc[3].npanels;
+  else if (k == "wgather_split_eligible") *out = h->vc[4].ok || h->wgs_eligible;
+  else if (k == "wgather_split_rows_per_block") *out = h->vc[4].rows_per_block;
+  else if (k == "wgather_split_units") *out = (uint64_t)h->vc[4].nblocks * kWgSplit.split;
   else if (k == "vcache_split4_x_bytes") *out = h->vc[2].ok ? 8ull * h->vc[2].nblocks * h->cols : 0;
   else if (k == "wcsr_segments") *out = h->wc.built ? h->wc.nseg : h->wc_segments;
   else if (k == "wcsr_max_segment") *out = h->wc.max_seg;
@@ -1602,7 +1625,8 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
              k == "hazard_stalls_model") {
     const int kn = h->last_kernel;
     const int li = kn == HIPSPMV_KERNEL_VCACHE ? 0 : kn == HIPSPMV_KERNEL_VCACHE_SPLIT ? 1
-                 : kn == HIPSPMV_KERNEL_VCACHE_SPLIT4 ? 2 : kn == HIPSPMV_KERNEL_WGATHER ? 3 : -1;
+                 : kn == HIPSPMV_KERNEL_VCACHE_SPLIT4 ? 2 : kn == HIPSPMV_KERNEL_WGATHER ? 3
+                 : kn == HIPSPMV_KERNEL_WGATHER_SPLIT ? 4 : -1;
     const bool lds_x = li >= 0 && li < 3;  // x panels staged in LDS (wgather gathers x from L2)
     if (k == "read_misses" || k == "read_misses_model")  // x words not held on chip when a product needs them
       *out = lds_x ? (uint64_t)h->vc[li].nblocks * h->cols : (uint64_t)h->nnz;
@@ -1663,6 +1687,7 @@ const char* hipspmv_kernel_name(hipspmv_t* h, int mode) {
     case HIPSPMV_KERNEL_VCACHE_SPLIT: return "vcache_split";
     case HIPSPMV_KERNEL_VCACHE_SPLIT4: return "vcache_split4";
     case HIPSPMV_KERNEL_WGATHER: return "wgather";
+    case HIPSPMV_KERNEL_WGATHER_SPLIT: return "wgather_split";
     case HIPSPMV_KERNEL_CSR_LANE: return "csr_lane";
     case HIPSPMV_KERNEL_CSR_VECTOR: return "csr_vector";
     case HIPSPMV_KERNEL_SELL: return "sell";

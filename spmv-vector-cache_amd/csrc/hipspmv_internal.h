@@ -46,6 +46,15 @@ constexpr VcGeom kVcSplit4{16384, 1984, 4};
 // profiles/r04/logs/sweep_c4_*.log.  512 windows of 2^16 at 2^24 columns: the
 // kernel's segment table holds 512 offsets (segmax).
 constexpr VcGeom kWgWindow{16384, 1 << 16, 1, 16, 512};
+// ---- k_wgather, two column parts (FAST; kernel "wgather_split", round 6):
+// a matrix of at most 128 * 16384 rows (a 2^21-row C4 shard) gets 16384-row
+// blocks -- twice the entries per x line in a segment of the one-part
+// layout's 8192 -- and each block's windows are cut in two halves, so the
+// 256 work units still fill the chip once.  Units of part 0 run on XCDs 0-3,
+// part 1 on XCDs 4-7 (workgroup w lands on XCD w mod 8): each XCD's L2 pulls
+// half of x through instead of all of it.  y = p0 + p1 in part order
+// (owner combine, combine.h): deterministic, not bit-identical to ORDERED.
+constexpr VcGeom kWgSplit{16384, 1 << 16, 2, 16, 512};
 // Row blocks per k_wgather launch (option "wgather_chunk"): one per CU.  A
 // matrix with more blocks than that (full C4: 2048 blocks of 8192 rows) runs
 // in several launches, so every launch's workgroups are resident together

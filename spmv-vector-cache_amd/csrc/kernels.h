@@ -137,6 +137,8 @@ hipError_t launch_vquad(int dtype, const VcacheArgs& a, hipStream_t s);
 uint32_t vquad_max_window(int variant);
 hipError_t launch_sell(int dtype, const SellArgs& a, hipStream_t s);
 hipError_t launch_wcsr(int dtype, const WcsrArgs& a, hipStream_t s);
+// k_wgather over a kWgWindow layout (a.split 1, ORDERED), or over a kWgSplit
+// layout (a.split 2, FAST: a.partial / a.tickets as k_vcache's split geometry)
 hipError_t launch_wgather(int dtype, const VcacheArgs& a, hipStream_t s);
 hipError_t launch_csr_lane(int dtype, const CsrArgs& a, hipStream_t s);
 hipError_t launch_csr_vector(int dtype, const CsrArgs& a, hipStream_t s);

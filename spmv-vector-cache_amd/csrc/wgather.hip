@@ -17,6 +17,7 @@
 // gather line touched + 8 per row of y (+8 for beta 1).
 #include <hip/hip_runtime.h>
 
+#include "combine.h"
 #include "device_common.h"
 #include "hipspmv_internal.h"
 #include "kernels.h"
@@ -27,27 +28,49 @@ namespace hipspmv {
 // the block's entries; an out-of-range lane issues no request), so a register
 // window wider than the mean segment costs no over-read -- the launcher sizes
 // EPT to the layout's longest segment and no step takes the slow path.
-template <typename T, int CB, int DE, int EPT, bool NTE = false, bool MSK = false>
-__global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restrict__ seg,
-                                                         const uint32_t* __restrict__ ecode,
-                                                         const T* __restrict__ evals, const T* __restrict__ x,
-                                                         const T* __restrict__ y_in, T* __restrict__ y_out,
-                                                         uint32_t rows, uint32_t rows_per_block, uint32_t npanels,
-                                                         uint32_t npad, uint32_t last, int beta, uint32_t b0) {
+//
+// PARTS 2 (kWgSplit, FAST): work unit (b, h) walks the windows of column part
+// h only, from +0.0 (part 1) or y_in (part 0), and the two partials of block b
+// are combined p0 + p1 by owner_combine.  Workgroup w runs on XCD w mod 8:
+// units are numbered so that part 0 fills XCDs 0-3 and part 1 XCDs 4-7 (a
+// grid tail of fewer than 8 units alternates the parts), so each XCD's L2
+// fetches only its half of x.
+// (The body is shared by the kernels k_wgather, PARTS 1, and k_wgather_split,
+// PARTS 2, so each form has its own symbol in a profile.)
+template <typename T, int CB, int DE, int EPT, bool NTE, bool MSK, int PARTS>
+__device__ __forceinline__ void wgather_body(const uint32_t* __restrict__ seg, const uint32_t* __restrict__ ecode,
+                                             const T* __restrict__ evals, const T* __restrict__ x,
+                                             const T* __restrict__ y_in, T* __restrict__ y_out, uint32_t rows,
+                                             uint32_t rows_per_block, uint32_t npanels, uint32_t npad, uint32_t last,
+                                             int beta, uint32_t b0, T* __restrict__ partial,
+                                             uint32_t* __restrict__ tickets, uint32_t nblocks) {
 #pragma clang fp contract(off)
+  static_assert(PARTS == 1 || PARTS == 2, "one or two column parts");
   constexpr int VT = kVcThreads;
   constexpr uint32_t W = 1u << CB, CMASK = W - 1, RMASK = (1u << (30 - CB)) - 1;
   constexpr int VR = 1 << (30 - CB);
   __shared__ T ylds[VR];
   __shared__ uint32_t segl[kWgWindow.segmax];
   const int t = threadIdx.x;
-  const uint32_t b = b0 + blockIdx.x;  // this launch's blocks start at b0 (launch chunks, kWgChunk)
+  uint32_t b = b0 + blockIdx.x, h = 0;  // this launch's blocks start at b0 (launch chunks, kWgChunk)
+  if constexpr (PARTS == 2) {
+    const uint32_t u = blockIdx.x, full = gridDim.x & ~7u;
+    if (u < full) {
+      h = (u & 7u) >> 2;
+      b = b0 + (u >> 3) * 4 + (u & 3u);
+    } else {
+      h = (u - full) & 1u;
+      b = b0 + full / 2 + (u - full) / 2;
+    }
+  }
   const uint32_t r0 = b * rows_per_block;
   if (r0 >= rows) return;  // never with a vcache_grid_ok geometry
   const uint32_t nr = min(rows_per_block, rows - r0);
-  const uint32_t* sp = seg + (size_t)b * (npad + 1);
+  const uint32_t* sp = seg + ((size_t)b * PARTS + h) * (npad + 1);
+  // this unit's windows: [pf, pf + nloc) (PARTS 1: all of them)
+  const uint32_t pf = vc_part_first(h, npanels, PARTS), nloc = vc_part_first(h + 1, npanels, PARTS) - pf;
   if ((uint32_t)t <= npad) segl[t] = sp[t];
-  for (uint32_t i = t; i < nr; i += VT) ylds[i] = beta ? y_in[r0 + i] : T(0);
+  for (uint32_t i = t; i < nr; i += VT) ylds[i] = beta && h == 0 ? y_in[r0 + i] : T(0);
   __syncthreads();
 
   const uint32_t e0 = __builtin_amdgcn_readfirstlane(segl[0]);
@@ -91,7 +114,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
     ylds[row] = acc;
   };
   auto apply = [&](uint32_t s, const uint32_t* c, const T* v) {
-    const T* xs = x + (size_t)s * W;
+    const T* xs = x + (size_t)(pf + s) * W;
     const uint32_t beg = segl[s], end = segl[s + 1];
     T xv[EPT];
 #pragma unroll
@@ -115,17 +138,43 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
   T EV[DE][EPT];
 #pragma unroll
   for (int i = 0; i < DE; ++i) load_e(i, EC[i], EV[i]);
-  for (uint32_t base = 0; base < npanels; base += DE) {
+  for (uint32_t base = 0; base < nloc; base += DE) {
 #pragma unroll
     for (int i = 0; i < DE; ++i) {
       const uint32_t s = base + i;
-      if (s >= npanels) break;
+      if (s >= nloc) break;
       apply(s, EC[i], EV[i]);
       load_e(s + DE, EC[i], EV[i]);
       __syncthreads();  // window s's y updates before window s+1's
     }
   }
-  for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
+  if constexpr (PARTS == 1) {
+    for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
+  } else {  // (segl is free now: its first words are the combine's LDS scratch)
+    owner_combine<T, PARTS, VT, (uint32_t)VR>(ylds, segl, partial, tickets + 4 * (size_t)b, b, h, nblocks, nr,
+                                              y_out + r0, t);
+  }
+}
+
+template <typename T, int CB, int DE, int EPT, bool NTE = false, bool MSK = false>
+__global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restrict__ seg,
+                                                         const uint32_t* __restrict__ ecode,
+                                                         const T* __restrict__ evals, const T* __restrict__ x,
+                                                         const T* __restrict__ y_in, T* __restrict__ y_out,
+                                                         uint32_t rows, uint32_t rows_per_block, uint32_t npanels,
+                                                         uint32_t npad, uint32_t last, int beta, uint32_t b0) {
+  wgather_body<T, CB, DE, EPT, NTE, MSK, 1>(seg, ecode, evals, x, y_in, y_out, rows, rows_per_block, npanels, npad,
+                                            last, beta, b0, nullptr, nullptr, 0);
+}
+
+template <typename T, int CB, int DE, int EPT, bool NTE = false, bool MSK = false>
+__global__ __launch_bounds__(kVcThreads) void k_wgather_split(
+    const uint32_t* __restrict__ seg, const uint32_t* __restrict__ ecode, const T* __restrict__ evals,
+    const T* __restrict__ x, const T* __restrict__ y_in, T* __restrict__ y_out, uint32_t rows,
+    uint32_t rows_per_block, uint32_t npanels, uint32_t npad, uint32_t last, int beta, uint32_t b0,
+    T* __restrict__ partial, uint32_t* __restrict__ tickets, uint32_t nblocks) {
+  wgather_body<T, CB, DE, EPT, NTE, MSK, 2>(seg, ecode, evals, x, y_in, y_out, rows, rows_per_block, npanels, npad,
+                                            last, beta, b0, partial, tickets, nblocks);
 }
 
 // Pipelined form (option vcache_xlane 2; every segment must fit the register
@@ -263,45 +312,46 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather_pipe(const uint32_t* __r
   for (uint32_t i = t; i < nr; i += VT) y_out[r0 + i] = ylds[i];
 }
 
-template <typename T>
+template <typename T, int DE, int EPT, bool NTE, bool MSK, int PARTS>
+static void launch_one(const VcacheArgs& a, uint32_t n, uint32_t b0, hipStream_t s) {
+  constexpr int CB = kWgWindow.colbits;
+  if constexpr (PARTS == 1)
+    hipLaunchKernelGGL((k_wgather<T, CB, DE, EPT, NTE, MSK>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
+                       (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
+                       a.npanels, a.npad, a.last, a.beta, b0);
+  else
+    hipLaunchKernelGGL((k_wgather_split<T, CB, DE, EPT, NTE, MSK>), dim3(2 * n), dim3(kVcThreads), 0, s, a.seg,
+                       a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
+                       a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0, (T*)a.partial, a.tickets, a.nblocks);
+}
+
+template <typename T, int PARTS>
 static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
   // blocks [b0, b0 + n) per launch: a chunk the chip holds at once walks the x
-  // windows together (kWgChunk); the launches run in stream order
-  const uint32_t chunk = a.chunk ? a.chunk : a.nblocks;
+  // windows together (kWgChunk units); the launches run in stream order
+  const uint32_t chunk = a.chunk ? (a.chunk + PARTS - 1) / PARTS : a.nblocks;
   for (uint32_t b0 = 0; b0 < a.nblocks; b0 += chunk) {
     const uint32_t n = a.nblocks - b0 < chunk ? a.nblocks - b0 : chunk;
-    if (a.xlane >= 2 && a.max_seg <= 2u * kVcThreads)
+    if (PARTS == 1 && a.xlane >= 2 && a.max_seg <= 2u * kVcThreads)
       hipLaunchKernelGGL((k_wgather_pipe<T, kWgWindow.colbits, 4, 2>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
                          (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
                          a.npanels, a.npad, a.last, a.beta, b0);
-    else if (a.xlane >= 2 && a.max_seg <= 4u * kVcThreads)
+    else if (PARTS == 1 && a.xlane >= 2 && a.max_seg <= 4u * kVcThreads)
       hipLaunchKernelGGL((k_wgather_pipe<T, kWgWindow.colbits, 4, 4>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
                          (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
                          a.npanels, a.npad, a.last, a.beta, b0);
     else if (a.nt_from == 0 && a.max_seg <= 2u * kVcThreads)
-      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 4, 2, true, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg,
-                         a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
-                         a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0);
+      launch_one<T, 4, 2, true, true, PARTS>(a, n, b0, s);
     else if (a.nt_from == 0 && a.max_seg <= 3u * kVcThreads)
-      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 4, 3, true, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg,
-                         a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
-                         a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0);
+      launch_one<T, 4, 3, true, true, PARTS>(a, n, b0, s);
     else if (a.nt_from == 0 && a.max_seg <= 6u * kVcThreads)
-      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 2, 6, true, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg,
-                         a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
-                         a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0);
+      launch_one<T, 2, 6, true, true, PARTS>(a, n, b0, s);
     else if (a.nt_from == 0 && a.max_seg <= 9u * kVcThreads)
-      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 2, 9, true, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg,
-                         a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
-                         a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0);
+      launch_one<T, 2, 9, true, true, PARTS>(a, n, b0, s);
     else if (a.nt_from == 0)
-      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 4, 2, true>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
-                         (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
-                         a.npanels, a.npad, a.last, a.beta, b0);
+      launch_one<T, 4, 2, true, false, PARTS>(a, n, b0, s);
     else
-      hipLaunchKernelGGL((k_wgather<T, kWgWindow.colbits, 4, 2>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
-                         (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
-                         a.npanels, a.npad, a.last, a.beta, b0);
+      launch_one<T, 4, 2, false, false, PARTS>(a, n, b0, s);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -310,11 +360,18 @@ static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
 
 hipError_t launch_wgather(int dtype, const VcacheArgs& a, hipStream_t s) {
   // the layout must be kWgWindow's (window width, row-block bound, one part)
+  // or kWgSplit's (two parts, with the combine scratch)
+  static_assert(kWgSplit.colbits == kWgWindow.colbits && kWgSplit.rows == 1 << (30 - kWgSplit.colbits) &&
+                    kWgSplit.panel == kWgWindow.panel,
+                "the two-part layout uses the kernel's window and y block");
+  const VcGeom& g = a.split == 2 ? kWgSplit : kWgWindow;
   if (!vcache_grid_ok(a.rows, a.cols, a.rows_per_block, a.nblocks, a.npanels, a.part_panels, a.npad, a.panel,
-                      a.split, kWgWindow) ||
-      a.part_panels != a.npanels)
+                      a.split, g) ||
+      (a.split == 1 && a.part_panels != a.npanels) || (a.split == 2 && (!a.partial || !a.tickets)))
     return hipErrorInvalidValue;
-  return dtype ? launch_wgather_t<uint64_t>(a, s) : launch_wgather_t<double>(a, s);
+  if (a.split == 2)
+    return dtype ? launch_wgather_t<uint64_t, 2>(a, s) : launch_wgather_t<double, 2>(a, s);
+  return dtype ? launch_wgather_t<uint64_t, 1>(a, s) : launch_wgather_t<double, 1>(a, s);
 }
 
 }  // namespace hipspmv

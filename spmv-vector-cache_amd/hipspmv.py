@@ -37,12 +37,13 @@ KERNEL_VCACHE_SPLIT4, KERNEL_WGATHER = 5, 6  # experimental: never chosen by AUT
 KERNEL_SELL = 7  # SELL-C-sigma lane per row
 KERNEL_WCSR = 8  # csr_vector over column-windowed row segments + a window-order reduce (FAST)
 KERNEL_VFLOW = 9  # four-part vector cache, x ring handed over by LDS flags (FAST, csrc/vflow.hip)
+KERNEL_WGATHER_SPLIT = 10  # k_wgather over two column halves, one per XCD half, y = p0 + p1 (FAST)
 SHARD_ALIGN = 64  # HIPSPMV_SHARD_ALIGN: row shards starting at multiples keep every kernel's bits
 #                   (except WCSR in FAST f64: within the bound, not bit-identical; include/hipspmv.h)
 KERNELS = {"auto": KERNEL_AUTO, "vcache": KERNEL_VCACHE, "csr_lane": KERNEL_CSR_LANE,
            "csr_vector": KERNEL_CSR_VECTOR, "vcache_split": KERNEL_VCACHE_SPLIT,
            "vcache_split4": KERNEL_VCACHE_SPLIT4, "wgather": KERNEL_WGATHER, "sell": KERNEL_SELL,
-           "wcsr": KERNEL_WCSR, "vcache_flow": KERNEL_VFLOW}
+           "wcsr": KERNEL_WCSR, "vcache_flow": KERNEL_VFLOW, "wgather_split": KERNEL_WGATHER_SPLIT}
 STATUS = {0: "ok", 1: "invalid argument", 2: "invalid matrix", 3: "HIP error", 4: "out of memory",
           5: "unsupported", 6: "no device", 7: "unknown key"}
 

@@ -31,6 +31,8 @@ for s in ${STEPS:-streams}; do
              step destroy_deferred 300 python -u spmv-vector-cache_amd/tools/destroy_probe.py &&
              HIPSPMV_SYNC_RELEASE=1 step destroy_sync_trace 300 rocprofv3 --kernel-trace -d $OUT/destroy_sync -o run --output-format csv -- python3 spmv-vector-cache_amd/tools/destroy_probe.py &&
              step destroy_deferred_trace 300 rocprofv3 --kernel-trace -d $OUT/destroy_deferred -o run --output-format csv -- python3 spmv-vector-cache_amd/tools/destroy_probe.py ;;
+    wgstests) step pytest_wgs 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_multi.py tests/test_gpu_fullsize.py -k "wgather or c4_shard" ;;
+    wgsab) step wgs_ab 400 python -u spmv-vector-cache_amd/tools/wgs_ab.py ${WGSAB_ARGS:-} ;;
     pytest) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;
     bench20) step bench20 600 python bench.py --steps 20 --warmup 5 ;;

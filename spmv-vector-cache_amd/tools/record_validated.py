@@ -24,7 +24,10 @@ PRODUCT = [f"void hipspmv::k_{k}<{t}{a}>" for t in ("double", "unsigned long")
                         ("vcache", ", 3, 3, 4, 2, 0, 0, false, 1, 5"),
                         ("csr_lane", ""), ("csr_vector", ", false"), ("wgather", ", 16, 4, 2, true, true"), ("wgather", ", 16, 4, 3, true, true"),
                         ("wgather", ", 16, 2, 6, true, true"), ("wgather", ", 16, 2, 9, true, true"),
-                        ("wgather", ", 16, 4, 2, true, false"))] + \
+                        ("wgather", ", 16, 4, 2, true, false"),
+                        ("wgather_split", ", 16, 4, 2, true, true"), ("wgather_split", ", 16, 4, 3, true, true"),
+                        ("wgather_split", ", 16, 2, 6, true, true"), ("wgather_split", ", 16, 2, 9, true, true"),
+                        ("wgather_split", ", 16, 4, 2, true, false"))] + \
           [f"void hipspmv::(anonymous namespace)::k_sell<{a}>" for a in
            ("double, true", "double, false", "unsigned long, false")] + \
           ["void hipspmv::(anonymous namespace)::k_sell_iso<45>"] + \

@@ -155,6 +155,44 @@ def test_full_size_u64_exact_properties(request, which):
         h.close()
 
 
+@pytest.mark.parametrize("shard", [0, 7])
+def test_c4_shard_auto_picks_wgather_split(c4_csr, shard):
+    """C4 as the 8-GPU job runs it: a 2^21-row shard of the 2^24-column stripe matrix, created alone.
+    AUTO's FAST kernel is wgather_split (bench.py's c4_shards block times it); sampled rows meet the
+    FAST bound, deterministic.  With the values read as u64 the whole shard is exact: the same bits
+    as the ordered wgather and sum(y) equal to the nonzero-wise checksum."""
+    n, rowptr_all, colind_all, vals_all = c4_csr
+    rows = n // 8
+    r0 = shard * rows
+    e0, e1 = int(rowptr_all[r0]), int(rowptr_all[r0 + rows])
+    rowptr = (rowptr_all[r0:r0 + rows + 1] - rowptr_all[r0]).astype(np.uint32)
+    colind, vals = colind_all[e0:e1], vals_all[e0:e1]
+    x = hs.gen_vector(n, 3)
+    sample = _sample(rowptr, rows, k=400)
+    want, absprod = _sequential(rowptr, colind, vals, x, sample)
+    lens = np.diff(rowptr.astype(np.int64))
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, n)
+    try:
+        assert h.kernel_name(hs.MODE_FAST) == "wgather_split", h.kernel_name(hs.MODE_FAST)
+        assert h.stat("wgather_split_rows_per_block") == 16384 and h.stat("wgather_split_units") == 256
+        _check(h, x, sample, want, absprod, lens, "auto", hs.MODE_FAST)
+    finally:
+        h.close()
+    a = vals.view(np.uint64)
+    xu = np.random.default_rng(13).integers(0, 2**64, n, dtype=np.uint64)
+    hu = hs.Handle.from_csr(rowptr, colind, a, rows, n)
+    try:
+        hu.set_kernel("wgather_split")
+        ys = hu.exec(xu, beta=0, mode=hs.MODE_FAST)
+        hu.set_kernel("wgather")
+        yw = hu.exec(xu, beta=0, mode=hs.MODE_ORDERED)
+        assert ys.tobytes() == yw.tobytes()
+        with np.errstate(over="ignore"):
+            assert int(np.sum(ys, dtype=np.uint64)) == _checksum_u64(colind, a, xu)
+    finally:
+        hu.close()
+
+
 @pytest.fixture(scope="module")
 def c5_bounds(gpu):
     bounds, _ = hs.c5_partition(24, 8)  # bench.py's c5_shards partition (wcsr cost model)

@@ -60,6 +60,24 @@ def test_multi_equals_single_device(gpu, kernel, mode):
     m.close()
 
 
+def test_multi_equals_single_device_wgather_split(gpu):
+    # k_wgather_split is position-independent: a row's sum is (y_in + its part-0 products) + its
+    # part-1 products, the halves cut at the same column for every shard -- shards of 2^15 rows
+    # (16384-row blocks of 2048 rows) give the single handle's bits
+    n, cols = 1 << 17, 1 << 21
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, cols, 32)
+    colptr, rowind, cvals = oracle.csr2csc(n, cols, rowptr, colind, vals)
+    x = hs.gen_vector(cols, 3)
+    one = hs.Handle.from_csc(colptr, rowind, cvals, n, cols)
+    assert one.kernel_name(hs.MODE_FAST) == "wgather_split"
+    y1 = one.exec(x, beta=0, mode=hs.MODE_FAST)
+    one.close()
+    m = hs.MultiHandle(colptr, rowind, cvals, n, cols, _devices(4))
+    m.set_kernel("wgather_split")
+    assert m.exec(x, beta=0, mode=hs.MODE_FAST).tobytes() == y1.tobytes()
+    m.close()
+
+
 @pytest.mark.parametrize("kernel", ["csr_vector", "sell"])
 def test_multi_equals_single_device_skewed_fast(gpu, kernel):
     # R-MAT rows: block starts are multiples of HIPSPMV_SHARD_ALIGN, so even

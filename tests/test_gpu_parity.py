@@ -1118,6 +1118,65 @@ def test_wgather_runs_and_line_order(gpu, dtype):
     h.close()
 
 
+def _clustered_wide(rng, rows, cols, dtype):
+    per_row = []
+    for r in range(rows):
+        n = int(rng.integers(0, 12))
+        w = rng.integers(0, cols >> 16, 3)  # entries clustered in up to three windows
+        c = (w[rng.integers(0, 3, n)] << 16) + rng.integers(0, 1 << 16, n)
+        per_row.append(np.unique(np.minimum(c, cols - 1)))
+    lens = np.array([c.size for c in per_row], np.int64)
+    rowptr = np.zeros(rows + 1, np.uint32)
+    rowptr[1:] = np.cumsum(lens)
+    colind = np.concatenate(per_row).astype(np.uint32)
+    if dtype == np.float64:
+        return rowptr, colind, rng.uniform(-1, 1, colind.size), rng.uniform(-1, 1, cols), rng.uniform(-1, 1, rows)
+    return (rowptr, colind, rng.integers(0, 2**64, colind.size, dtype=np.uint64),
+            rng.integers(0, 2**64, cols, dtype=np.uint64), rng.integers(0, 2**64, rows, dtype=np.uint64))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.uint64])
+@pytest.mark.parametrize("shape", ["stripe", "clustered", "ragged"])
+def test_wgather_split_fast(gpu, dtype, shape):
+    # k_wgather_split (two column halves, y = p0 + p1, part 0 on XCDs 0-3): AUTO's FAST kernel for
+    # wide x with <= 2^21 rows; ORDERED stays on wgather.  Within the FAST bound of the oracle's
+    # sums at beta 0 / 1, deterministic, u64 exact; any launch chunking (2 units per block, an odd
+    # grid tail of fewer than 8 units) gives the same bits
+    rng = np.random.default_rng(11)
+    if shape == "stripe":
+        rows, cols = 1 << 17, 1 << 21
+        rowptr, colind, vals = hs.gen_stripe_csr(0, rows, cols, 32)
+        x, y0 = rng.uniform(-1, 1, cols), rng.uniform(-1, 1, rows)
+        if dtype == np.uint64:
+            vals = rng.integers(0, 2**64, colind.size, dtype=np.uint64)
+            x, y0 = rng.integers(0, 2**64, cols, dtype=np.uint64), rng.integers(0, 2**64, rows, dtype=np.uint64)
+    else:
+        rows, cols = (40001, (1 << 21) + 5) if shape == "clustered" else (300, (1 << 21) + 3)
+        rowptr, colind, vals, x, y0 = _clustered_wide(rng, rows, cols, dtype)
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+    assert h.stat("wgather_split_eligible")
+    assert h.kernel_name(hs.MODE_FAST) == "wgather_split"
+    assert h.kernel_name(hs.MODE_ORDERED) == ("wgather" if dtype == np.float64 else "wgather_split")
+    assert h.stat("wgather_split_units") == 2 * -(-rows // h.stat("wgather_split_rows_per_block"))
+    colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+    lens = np.diff(rowptr.astype(np.int64))
+    for beta in (0, 1):
+        y_ref = oracle.spmv_csc(colptr, rowind, cvals, x, y=(y0.copy() if beta else None), rows=rows)
+        outs = []
+        for chunk in (256, 256, 0, 3, 1):
+            h.set_option("wgather_chunk", chunk)
+            outs.append(h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST))
+        assert all(o.tobytes() == outs[0].tobytes() for o in outs), (shape, beta)
+        y = outs[0]
+        if dtype == np.uint64:
+            assert y.tobytes() == y_ref.tobytes(), (shape, beta)
+        else:
+            absprod = np.bincount(np.repeat(np.arange(rows), lens), weights=np.abs(vals * x[colind]), minlength=rows)
+            bound = 2.0 * (lens + 1) * 2.0 ** -53 * (absprod + (np.abs(y0) if beta else 0)) + 1e-300
+            assert np.all(np.abs(y - y_ref) <= bound), (shape, beta)
+    h.close()
+
+
 def test_stream_bandwidth(gpu):
     # the bench's second denominator (hipspmv_stream_bandwidth, csrc/stream.hip): plausible GB/s on an MI355X
     cp, rd = hs.stream_bandwidth(0, 1 << 28, 5)
