@@ -258,6 +258,7 @@ struct hipspmv_handle {
   // with the default policy (Infinity-Cache resident); 0 default: all non-temporal
   int64_t wcsr_res = 0;
   int wcsr_reduce = 0;    // option "wcsr_reduce": 0 the compact reduce over rows with segments, 1 every row
+  int wcsr_xcd = 0;       // option "wcsr_xcd": 1 the segment pass's blocks placed by XCD eighths (kernels.hip)
   int wcsr_fill = -1;     // option "wcsr_fill": 1 the rows without segments written by the segment pass's
                           // launch, 0 by the reduce's; -1 (default) 1 when two thirds of the rows are empty
   // option "sell_nt": SELL slices s >= sell_nt load their entries
@@ -1184,6 +1185,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
     a.res_groups = (uint32_t)std::min<int64_t>(h->wcsr_res, w.ngroups);
     h->resident_entry_bytes = w.group_first.empty() ? 0 : 12ull * w.group_first[a.res_groups];
     a.cols = h->cols;
+    a.xcd = h->wcsr_xcd;
     if (h->wcsr_reduce == 0 && w.d_rrow) {  // the compact reduce (default; option wcsr_reduce 1: all rows)
       a.rrow = w.d_rrow;
       a.rsegc = w.d_rsegc;
@@ -1398,6 +1400,9 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "wcsr_fill") {  // 1: empty rows filled beside the segment pass; 0: after the reduce; -1: by rule
     if (value < -1 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
     h->wcsr_fill = (int)value;
+  } else if (k == "wcsr_xcd") {  // 1: segment-pass blocks by XCD eighths of the window order; same bits
+    if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
+    h->wcsr_xcd = (int)value;
   } else if (k == "wcsr_reduce") {  // 0: compact reduce over the rows with segments (default); 1: every row
     if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
     h->wcsr_reduce = (int)value;

@@ -74,6 +74,7 @@ struct WcsrArgs {  // csr_vector over the column-windowed segment matrix, then k
   const uint32_t* cgroups = nullptr;
   uint32_t ncgroups = 0;
   int fill_early = 0;  // the rows without segments written by the segment pass's launch (k_wpass_fill)
+  int xcd = 0;         // option wcsr_xcd: segment-pass blocks placed by XCD eighths of the window order
 };
 
 struct SellArgs {

@@ -196,10 +196,10 @@ __device__ __forceinline__ void csr_vector_group(const uint32_t* __restrict__ ro
                                                  const uint32_t* __restrict__ colind, const T* __restrict__ vals,
                                                  const T* __restrict__ x, const T* __restrict__ y_in,
                                                  T* __restrict__ y_out, const uint32_t* __restrict__ groups,
-                                                 uint32_t ngroups, int beta) {
+                                                 uint32_t ngroups, int beta, uint32_t blk) {
   __shared__ uint32_t heads[4][kCvGroupNnz / 32];
   const int w = threadIdx.x >> 6;
-  const uint32_t g = blockIdx.x * 4 + w;
+  const uint32_t g = blk * 4 + w;
   if (g >= ngroups) return;  // wave-uniform; no workgroup barriers below
   csr_vector_rows<T, KIND>(rowptr, colind, vals, [&](uint32_t c) { return x[c]; }, RowOut<T>{y_in, y_out, beta},
                            groups[g], groups[g + 1], heads[w]);
@@ -228,6 +228,16 @@ __global__ __launch_bounds__(1024) void k_wseg(const uint32_t* __restrict__ chun
                           RowOut<T>{(const T*)nullptr, ypart, 0}, groups[g], groups[g + 1], heads[w]);
 }
 
+// The wcsr segment pass's XCD placement (option "wcsr_xcd"):
+// workgroup i runs on XCD i mod 8, so with xper = ceil(blocks / 8) it takes
+// block (i mod 8) * xper + i / 8 -- XCD k walks the k-th contiguous eighth of
+// the window-major groups, and its L2 gathers from those windows only instead
+// of every XCD gathering from the window the whole chip is in.  The grid is
+// 8 * xper; virtual blocks past the last return.  xper 0: block i.
+__device__ __forceinline__ uint32_t wcsr_block(uint32_t xper) {
+  return xper ? (blockIdx.x & 7u) * xper + (blockIdx.x >> 3) : blockIdx.x;
+}
+
 // NTE: the wcsr segment pass (KIND 1 above)
 template <typename T, bool NTE = false>
 __global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__ rowptr,
@@ -235,7 +245,16 @@ __global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__
                                                      const T* __restrict__ x, const T* __restrict__ y_in,
                                                      T* __restrict__ y_out, const uint32_t* __restrict__ groups,
                                                      uint32_t ngroups, int beta) {
-  csr_vector_group<T, NTE ? 1 : 0>(rowptr, colind, vals, x, y_in, y_out, groups, ngroups, beta);
+  csr_vector_group<T, NTE ? 1 : 0>(rowptr, colind, vals, x, y_in, y_out, groups, ngroups, beta, blockIdx.x);
+}
+// the wcsr segment pass with the XCD placement
+template <typename T>
+__global__ __launch_bounds__(256) void k_wpass_x(const uint32_t* __restrict__ rowptr,
+                                                  const uint32_t* __restrict__ colind, const T* __restrict__ vals,
+                                                  const T* __restrict__ x, T* __restrict__ ypart,
+                                                  const uint32_t* __restrict__ groups, uint32_t ngroups,
+                                                  uint32_t xper) {
+  csr_vector_group<T, 1>(rowptr, colind, vals, x, (const T*)nullptr, ypart, groups, ngroups, 0, wcsr_block(xper));
 }
 
 // k_wpass (wcsr segment pass with resident entries): the groups g <
@@ -274,16 +293,18 @@ __global__ __launch_bounds__(256) void k_wpass_fill(const uint32_t* __restrict__
                                                      const T* __restrict__ x, T* __restrict__ ypart,
                                                      const uint32_t* __restrict__ groups, uint32_t ngroups,
                                                      const uint32_t* __restrict__ nebits, const T* __restrict__ y_in,
-                                                     T* __restrict__ y_out, uint32_t rows, int beta, uint32_t nfill) {
-  if (blockIdx.x < nfill) {
+                                                     T* __restrict__ y_out, uint32_t rows, int beta, uint32_t nfill,
+                                                     uint32_t xper) {
+  const uint32_t v = wcsr_block(xper);  // (option wcsr_xcd: fill and group blocks placed by XCD eighths)
+  if (v < nfill) {
     const uint32_t stride = nfill * 256;
-    for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < rows; r += stride)
+    for (uint32_t r = v * 256 + threadIdx.x; r < rows; r += stride)
       if (!((nebits[r >> 5] >> (r & 31)) & 1u)) y_out[r] = beta ? y_in[r] : T(0);
     return;
   }
   __shared__ uint32_t heads[4][kCvGroupNnz / 32];
   const int w = threadIdx.x >> 6;
-  const uint32_t g = (blockIdx.x - nfill) * 4 + w;
+  const uint32_t g = (v - nfill) * 4 + w;
   if (g >= ngroups) return;  // wave-uniform
   csr_vector_rows<T, 1>(rowptr, colind, vals, [&](uint32_t c) { return x[c]; },
                         RowOut<T>{(const T*)nullptr, ypart, 0}, groups[g], groups[g + 1], heads[w]);
@@ -298,7 +319,7 @@ __global__ __launch_bounds__(256) void k_wreduce(const uint32_t* __restrict__ ro
                                                   const uint32_t* __restrict__ segidx, const T* __restrict__ ypart,
                                                   const T* __restrict__ y_in, T* __restrict__ y_out,
                                                   const uint32_t* __restrict__ groups, uint32_t ngroups, int beta) {
-  csr_vector_group<T, 2>(rowseg, segidx, (const T*)nullptr, ypart, y_in, y_out, groups, ngroups, beta);
+  csr_vector_group<T, 2>(rowseg, segidx, (const T*)nullptr, ypart, y_in, y_out, groups, ngroups, beta, blockIdx.x);
 }
 
 // k_wreduce_c (wcsr, compact reduce): the same sums as k_wreduce over groups
@@ -365,11 +386,19 @@ hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
                        (const T*)a.seg_vals, (const T*)a.x, a.cols, (T*)a.ypart);
   const bool fill_early = a.rrow && a.fill_early && !a.nchunks && !a.res_groups;
   const uint32_t nfill = std::min((a.rows + 255) / 256, 1024u);
-  if (fill_early)
-    hipLaunchKernelGGL(k_wpass_fill<T>, dim3(nfill + (a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr,
-                       a.seg_colind, (const T*)a.seg_vals, (const T*)a.x, (T*)a.ypart, a.groups, a.ngroups, a.nebits,
-                       (const T*)a.y_in, (T*)a.y_out, a.rows, a.beta, nfill);
-  else if (a.ngroups && a.res_groups)
+  // option wcsr_xcd: the segment pass's blocks placed by XCD eighths (grid 8 * xper)
+  auto xper_of = [&](uint32_t blocks) { return a.xcd ? (blocks + 7) / 8 : 0u; };
+  auto grid_of = [&](uint32_t blocks) { return a.xcd ? 8 * xper_of(blocks) : blocks; };
+  if (fill_early) {
+    const uint32_t nb = nfill + (a.ngroups + 3) / 4;
+    hipLaunchKernelGGL(k_wpass_fill<T>, dim3(grid_of(nb)), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,
+                       (const T*)a.seg_vals, (const T*)a.x, (T*)a.ypart, a.groups, a.ngroups, a.nebits,
+                       (const T*)a.y_in, (T*)a.y_out, a.rows, a.beta, nfill, xper_of(nb));
+  } else if (a.ngroups && a.xcd && !a.res_groups) {
+    const uint32_t nb = (a.ngroups + 3) / 4;
+    hipLaunchKernelGGL(k_wpass_x<T>, dim3(grid_of(nb)), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,
+                       (const T*)a.seg_vals, (const T*)a.x, (T*)a.ypart, a.groups, a.ngroups, xper_of(nb));
+  } else if (a.ngroups && a.res_groups)
     hipLaunchKernelGGL(k_wpass<T>, dim3((a.ngroups + 3) / 4), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,
                        (const T*)a.seg_vals, (const T*)a.x, (T*)a.ypart, a.groups, a.ngroups, a.res_groups);
   else if (a.ngroups)

@@ -33,6 +33,12 @@ for s in ${STEPS:-streams}; do
              step destroy_deferred_trace 300 rocprofv3 --kernel-trace -d $OUT/destroy_deferred -o run --output-format csv -- python3 spmv-vector-cache_amd/tools/destroy_probe.py ;;
     wgstests) step pytest_wgs 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_multi.py tests/test_gpu_fullsize.py -k "wgather or c4_shard" ;;
     wgsab) step wgs_ab 400 python -u spmv-vector-cache_amd/tools/wgs_ab.py ${WGSAB_ARGS:-} ;;
+    c5xcd) step c5_xcd 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set xcd --shards 0,3,7 ;;
+    c5xcd19) HIPSPMV_WCSR_LOG2W=19 step c5_xcd_w19 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set xcd --shards 0,3,7 ;;
+    c5xcd18) HIPSPMV_WCSR_LOG2W=18 step c5_xcd_w18 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set xcd --shards 0,3,7 ;;
+    pmcc4s) KERNELS="wgather_split wgather" WORKLOAD=c4s7 step pmc_c4s7 900 bash spmv-vector-cache_amd/tools/gpurun_pmc.sh &&
+            step pmc_c4s7_split_summary 60 python3 spmv-vector-cache_amd/tools/pmc_summary.py $OUT/pmc_c4s7_wgather_split_summary.csv "k_wgather_split<double," $OUT/pmc_c4s7_wgather_split_*/*counter_collection.csv &&
+            step pmc_c4s7_wg_summary 60 python3 spmv-vector-cache_amd/tools/pmc_summary.py $OUT/pmc_c4s7_wgather_summary.csv "k_wgather<double," $OUT/pmc_c4s7_wgather_[0-9]*/*counter_collection.csv ;;
     pytest) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;
     bench20) step bench20 600 python bench.py --steps 20 --warmup 5 ;;

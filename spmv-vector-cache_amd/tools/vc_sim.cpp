@@ -511,7 +511,9 @@ int main(int argc, char** argv) {
                       {kVcSplit.rows, kVcSplit.panel, 3, 4, 2, 3, 1, 16, 1},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 0, 16, 2},
                       {kVcSplit4.rows, kVcSplit4.panel, 2, 4, 2, 4, 1, 16, 2},
-                      {kWgWindow.rows, kWgWindow.panel, 0, 4, 4, 1, 2, kWgWindow.colbits, 2}};
+                      {kWgWindow.rows, kWgWindow.panel, 0, 4, 4, 1, 2, kWgWindow.colbits, 2},
+                      // k_wgather_split: the window layout in two column halves (kWgSplit)
+                      {kWgSplit.rows, kWgSplit.panel, 0, 4, 3, 2, 2, kWgSplit.colbits}};
   int failures = check_maps<1>() + check_maps<2>() + check_maps<3>() + check_maps<4>();
   {  // the round-1 incident geometry: the ordered (split 1) kernel launched with the split layout's
      // 8192-row blocks -- 256 blocks over 2^20 rows, 128 of them past the last row -- is rejected,
