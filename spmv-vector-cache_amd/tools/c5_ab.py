@@ -23,6 +23,7 @@ SETS = {
     "fill": [("fill beside the segment pass", {"wcsr_fill": 1}), ("fill after the reduce", {"wcsr_fill": 0})],
     "reduce": [("compact reduce", {}), ("all-rows reduce", {"wcsr_reduce": 1})],
     "xcd": [("product", {}), ("xcd eighths", {"wcsr_xcd": 1})],
+    "wg": [("product", {}), ("wgather (kernel 6)", {"kernel": 6})],
     "res": [("all nt (product)", {}), ("resident 1/8", {"wcsr_res": ("groups", 0.125)}),
             ("resident 1/4", {"wcsr_res": ("groups", 0.25)}), ("resident 3/8", {"wcsr_res": ("groups", 0.375)}),
             ("resident 1/2", {"wcsr_res": ("groups", 0.5)})],

@@ -39,6 +39,7 @@ for s in ${STEPS:-streams}; do
     pmcc4s) KERNELS="wgather_split wgather" WORKLOAD=c4s7 step pmc_c4s7 900 bash spmv-vector-cache_amd/tools/gpurun_pmc.sh &&
             step pmc_c4s7_split_summary 60 python3 spmv-vector-cache_amd/tools/pmc_summary.py $OUT/pmc_c4s7_wgather_split_summary.csv "k_wgather_split<double," $OUT/pmc_c4s7_wgather_split_*/*counter_collection.csv &&
             step pmc_c4s7_wg_summary 60 python3 spmv-vector-cache_amd/tools/pmc_summary.py $OUT/pmc_c4s7_wgather_summary.csv "k_wgather<double," $OUT/pmc_c4s7_wgather_[0-9]*/*counter_collection.csv ;;
+    c5wg) step c5_wg 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set wg --shards 0,3,7 ;;
     pytest) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;
     bench20) step bench20 600 python bench.py --steps 20 --warmup 5 ;;

@@ -131,6 +131,35 @@ def test_many_streams_evict_and_stay_exact(gpu):
         h.close()
 
 
+def test_wgather_split_concurrent_streams(gpu):
+    # k_wgather_split's combine scratch (partials + share counters) is per stream like the vector
+    # cache's: launches on three streams with nothing ordering them run at once and each gives the
+    # reference bits, within the FAST bound of the oracle
+    import torch
+    rows, cols = 1 << 15, (1 << 21) + 7
+    rowptr, colind, vals = hs.gen_stripe_csr(3, rows, cols, 32)
+    h = hs.Handle.from_csr(rowptr, colind, vals, rows, cols)
+    assert h.kernel_name(hs.MODE_FAST) == "wgather_split"
+    xh = hs.gen_vector(cols, 9)
+    x = torch.from_numpy(xh).cuda()
+    y0 = torch.empty(rows, dtype=torch.float64, device="cuda")
+    h.exec_device(x, y0, beta=0, mode=hs.MODE_FAST, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    ref = y0.cpu().numpy()
+    colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+    y_ref = oracle.spmv_csc(colptr, rowind, cvals, xh, rows=rows)
+    absprod = np.bincount(np.repeat(np.arange(rows), 32), weights=np.abs(vals * xh[colind]), minlength=rows)
+    assert np.all(np.abs(ref - y_ref) <= 2.0 * 33 * 2.0 ** -53 * absprod + 1e-300)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = [torch.empty_like(y0) for _ in range(12)]
+    for k in range(12):
+        h.exec_device(x, outs[k], beta=0, mode=hs.MODE_FAST, stream=streams[k % 3])
+    torch.cuda.synchronize()
+    for k in range(12):
+        assert outs[k].cpu().numpy().tobytes() == ref.tobytes(), k
+    h.close()
+
+
 def test_destroy_returns_without_waiting_for_the_device(gpu):
     # ~50 launches of a C3-sized vcache_split queued on a side stream; creating and destroying a
     # second handle meanwhile returns long before that queue drains (hipFree would have waited for
