@@ -588,7 +588,8 @@ def run_c4_shards(a, rowptr, colind, vals, n: int, x, dev, stream) -> dict:
         parity = shard_parity(rp, ci, va, x.cpu().numpy(), y.cpu().numpy(), hs.MODE_FAST, sample_rows(rp, 200, seed=r))
         shards.append({"shard": r, "rows": [row0, row1], "nnz": int(ci.size), "kernel": kname,
                        "kernel_us": round(us, 3), "roofline_frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                       "alg_bytes": alg, "parity": parity, "setup_s": round(setup_s, 2)})
+                       "alg_bytes": alg, "resident_entry_bytes": h.stat("resident_entry_bytes"), "parity": parity,
+                       "setup_s": round(setup_s, 2)})
         h.close()
         hs.release_wait()
         del y

@@ -1172,9 +1172,21 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                  v.npad,      h->nnz - 1, v.split,   beta, 0,       (uint32_t)kWgWindow.panel,
                  h->vcache_xlane, v.max_seg};
     a.chunk = h->wgather_chunk;
-    // entries non-temporal unless option vcache_nt > 0 (full C4: 3391 us against 3594)
-    a.nt_from = h->vcache_nt > 0 ? ~0u : 0u;
-    h->resident_entry_bytes = a.nt_from ? 12ull * h->nnz : 0;
+    if (k == 3) {
+      // entries non-temporal unless option vcache_nt > 0 (full C4: 3391 us against 3594)
+      a.nt_from = h->vcache_nt > 0 ? ~0u : 0u;
+      h->resident_entry_bytes = a.nt_from ? 12ull * h->nnz : 0;
+    } else {
+      // wgather_split: row blocks b < nt_from keep their entries resident (option vcache_nt: the first
+      // non-temporal block; default: the leading blocks that fit what x and y leave of
+      // kWgSplitMallBytes)
+      const uint64_t xy = 8ull * h->cols + 8ull * h->rows;
+      const uint64_t budget = kWgSplitMallBytes > xy ? (kWgSplitMallBytes - xy) / 12 : 0;  // entries
+      const uint32_t fit = (uint32_t)(std::upper_bound(v.block_first.begin(), v.block_first.end(), budget) -
+                                      v.block_first.begin()) - 1;  // block_first[fit] <= budget
+      a.nt_from = (uint32_t)std::min<int64_t>(h->vcache_nt >= 0 ? h->vcache_nt : fit, v.nblocks);
+      h->resident_entry_bytes = 12ull * v.block_first[a.nt_from];
+    }
     e = launch_wgather(h->dtype, a, s);
   } else if (kernel == HIPSPMV_KERNEL_WCSR) {
     const auto& w = h->wc;

@@ -55,6 +55,14 @@ constexpr VcGeom kWgWindow{16384, 1 << 16, 1, 16, 512};
 // half of x through instead of all of it.  y = p0 + p1 in part order
 // (owner combine, combine.h): deterministic, not bit-identical to ORDERED.
 constexpr VcGeom kWgSplit{16384, 1 << 16, 2, 16, 512};
+// kWgSplit entry residency: the leading row blocks whose entries fit in
+// kWgSplitMallBytes - 8 * cols - 8 * rows (what x and y leave of the 256 MiB
+// Infinity Cache) load with the default cache policy and stay resident across
+// launches; the rest non-temporal.  C4 shard (x 134 MB, 6.3 MB of entries per
+// block), profiles/r06/wgs/wgs_nt_*.log: 0 / 6 / 9 / 12 / 15 / 18 / 20 / 28
+// blocks resident 358.0 / 353.1 / 352.5 / 350.8 / 349.2 / 352.3 / 358 / 401 us;
+// this budget gives 14 blocks (88 MB).
+constexpr uint64_t kWgSplitMallBytes = 232ull << 20;
 // Row blocks per k_wgather launch (option "wgather_chunk"): one per CU.  A
 // matrix with more blocks than that (full C4: 2048 blocks of 8192 rows) runs
 // in several launches, so every launch's workgroups are resident together

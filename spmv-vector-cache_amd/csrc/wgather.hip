@@ -17,6 +17,8 @@
 // gather line touched + 8 per row of y (+8 for beta 1).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "combine.h"
 #include "device_common.h"
 #include "hipspmv_internal.h"
@@ -43,7 +45,7 @@ __device__ __forceinline__ void wgather_body(const uint32_t* __restrict__ seg, c
                                              const T* __restrict__ y_in, T* __restrict__ y_out, uint32_t rows,
                                              uint32_t rows_per_block, uint32_t npanels, uint32_t npad, uint32_t last,
                                              int beta, uint32_t b0, T* __restrict__ partial,
-                                             uint32_t* __restrict__ tickets, uint32_t nblocks) {
+                                             uint32_t* __restrict__ tickets, uint32_t nblocks, uint32_t nt_from) {
 #pragma clang fp contract(off)
   static_assert(PARTS == 1 || PARTS == 2, "one or two column parts");
   constexpr int VT = kVcThreads;
@@ -80,15 +82,23 @@ __device__ __forceinline__ void wgather_body(const uint32_t* __restrict__ seg, c
     const uint32_t beg = segl[min(s, npad)];
     if constexpr (MSK) {
       const uint32_t end = segl[min(s + 1, npad)] - e0;
-      constexpr int aux = NTE ? 2 : 0;  // nt
+      auto ld = [&](auto aux_c) {
+        constexpr int aux = decltype(aux_c)::value;
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        const uint32_t q = beg - e0 + t + j * VT;
-        const bool in = q < end;
-        c[j] = __builtin_amdgcn_raw_buffer_load_b32(dcode, in ? (int)(4 * q) : (int)0x80000000, 0, aux);
-        v[j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(dvals, in ? (int)(8 * q) : (int)0x80000000,
-                                                                           0, aux));
-      }
+        for (int j = 0; j < EPT; ++j) {
+          const uint32_t q = beg - e0 + t + j * VT;
+          const bool in = q < end;
+          c[j] = __builtin_amdgcn_raw_buffer_load_b32(dcode, in ? (int)(4 * q) : (int)0x80000000, 0, aux);
+          v[j] = __builtin_bit_cast(
+              T, __builtin_amdgcn_raw_buffer_load_b64(dvals, in ? (int)(8 * q) : (int)0x80000000, 0, aux));
+        }
+      };
+      // PARTS 2: row blocks b < nt_from keep their entries with the default policy (Infinity-Cache
+      // resident across launches), the others non-temporal (wave-uniform branch)
+      if (PARTS == 2 && NTE && b < nt_from)
+        ld(std::integral_constant<int, 0>{});
+      else
+        ld(std::integral_constant<int, NTE ? 2 : 0>{});  // nt
       return;
     }
 #pragma unroll
@@ -164,7 +174,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
                                                          uint32_t rows, uint32_t rows_per_block, uint32_t npanels,
                                                          uint32_t npad, uint32_t last, int beta, uint32_t b0) {
   wgather_body<T, CB, DE, EPT, NTE, MSK, 1>(seg, ecode, evals, x, y_in, y_out, rows, rows_per_block, npanels, npad,
-                                            last, beta, b0, nullptr, nullptr, 0);
+                                            last, beta, b0, nullptr, nullptr, 0, 0);
 }
 
 template <typename T, int CB, int DE, int EPT, bool NTE = false, bool MSK = false>
@@ -172,9 +182,9 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather_split(
     const uint32_t* __restrict__ seg, const uint32_t* __restrict__ ecode, const T* __restrict__ evals,
     const T* __restrict__ x, const T* __restrict__ y_in, T* __restrict__ y_out, uint32_t rows,
     uint32_t rows_per_block, uint32_t npanels, uint32_t npad, uint32_t last, int beta, uint32_t b0,
-    T* __restrict__ partial, uint32_t* __restrict__ tickets, uint32_t nblocks) {
+    T* __restrict__ partial, uint32_t* __restrict__ tickets, uint32_t nblocks, uint32_t nt_from) {
   wgather_body<T, CB, DE, EPT, NTE, MSK, 2>(seg, ecode, evals, x, y_in, y_out, rows, rows_per_block, npanels, npad,
-                                            last, beta, b0, partial, tickets, nblocks);
+                                            last, beta, b0, partial, tickets, nblocks, nt_from);
 }
 
 // Pipelined form (option vcache_xlane 2; every segment must fit the register
@@ -322,7 +332,8 @@ static void launch_one(const VcacheArgs& a, uint32_t n, uint32_t b0, hipStream_t
   else
     hipLaunchKernelGGL((k_wgather_split<T, CB, DE, EPT, NTE, MSK>), dim3(2 * n), dim3(kVcThreads), 0, s, a.seg,
                        a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
-                       a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0, (T*)a.partial, a.tickets, a.nblocks);
+                       a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0, (T*)a.partial, a.tickets, a.nblocks,
+                       a.nt_from);
 }
 
 template <typename T, int PARTS>
@@ -330,6 +341,9 @@ static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
   // blocks [b0, b0 + n) per launch: a chunk the chip holds at once walks the x
   // windows together (kWgChunk units); the launches run in stream order
   const uint32_t chunk = a.chunk ? (a.chunk + PARTS - 1) / PARTS : a.nblocks;
+  // non-temporal entry loads: PARTS 1 all or none (nt_from 0: all); PARTS 2 the blocks b >= nt_from,
+  // chosen at run time inside the NTE forms (nt_from >= nblocks: every block resident)
+  const bool nt = PARTS == 1 ? a.nt_from == 0 : true;
   for (uint32_t b0 = 0; b0 < a.nblocks; b0 += chunk) {
     const uint32_t n = a.nblocks - b0 < chunk ? a.nblocks - b0 : chunk;
     if (PARTS == 1 && a.xlane >= 2 && a.max_seg <= 2u * kVcThreads)
@@ -340,18 +354,18 @@ static hipError_t launch_wgather_t(const VcacheArgs& a, hipStream_t s) {
       hipLaunchKernelGGL((k_wgather_pipe<T, kWgWindow.colbits, 4, 4>), dim3(n), dim3(kVcThreads), 0, s, a.seg, a.code,
                          (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows, a.rows_per_block,
                          a.npanels, a.npad, a.last, a.beta, b0);
-    else if (a.nt_from == 0 && a.max_seg <= 2u * kVcThreads)
+    else if (nt && a.max_seg <= 2u * kVcThreads)
       launch_one<T, 4, 2, true, true, PARTS>(a, n, b0, s);
-    else if (a.nt_from == 0 && a.max_seg <= 3u * kVcThreads)
+    else if (nt && a.max_seg <= 3u * kVcThreads)
       launch_one<T, 4, 3, true, true, PARTS>(a, n, b0, s);
-    else if (a.nt_from == 0 && a.max_seg <= 6u * kVcThreads)
+    else if (nt && a.max_seg <= 6u * kVcThreads)
       launch_one<T, 2, 6, true, true, PARTS>(a, n, b0, s);
-    else if (a.nt_from == 0 && a.max_seg <= 9u * kVcThreads)
+    else if (nt && a.max_seg <= 9u * kVcThreads)
       launch_one<T, 2, 9, true, true, PARTS>(a, n, b0, s);
-    else if (a.nt_from == 0)
+    else if (nt)
       launch_one<T, 4, 2, true, false, PARTS>(a, n, b0, s);
-    else
-      launch_one<T, 4, 2, false, false, PARTS>(a, n, b0, s);
+    else if constexpr (PARTS == 1)  // (PARTS 2 always takes an NTE form: residency per block at run time)
+      launch_one<T, 4, 2, false, false, 1>(a, n, b0, s);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -33,6 +33,8 @@ for s in ${STEPS:-streams}; do
              step destroy_deferred_trace 300 rocprofv3 --kernel-trace -d $OUT/destroy_deferred -o run --output-format csv -- python3 spmv-vector-cache_amd/tools/destroy_probe.py ;;
     wgstests) step pytest_wgs 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_multi.py tests/test_gpu_fullsize.py -k "wgather or c4_shard" ;;
     wgsab) step wgs_ab 400 python -u spmv-vector-cache_amd/tools/wgs_ab.py ${WGSAB_ARGS:-} ;;
+    wgsnt) step wgs_nt 600 python -u spmv-vector-cache_amd/tools/wgs_ab.py --kernels wgather_split --nt ${WGS_NT:-0,12,20,28,40} --shards ${WGS_SHARDS:-0} ;;
+    streams2) step pytest_streams2 400 $PYT -m gpu tests/test_gpu_streams.py tests/test_gpu_parity.py -k "wgather_split" ;;
     c5xcd) step c5_xcd 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set xcd --shards 0,3,7 ;;
     c5xcd19) HIPSPMV_WCSR_LOG2W=19 step c5_xcd_w19 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set xcd --shards 0,3,7 ;;
     c5xcd18) HIPSPMV_WCSR_LOG2W=18 step c5_xcd_w18 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set xcd --shards 0,3,7 ;;

@@ -28,6 +28,8 @@ def main():
     p.add_argument("--launches", type=int, default=50)
     p.add_argument("--warm", type=int, default=100)
     p.add_argument("--kernels", default="wgather,wgather_split")
+    p.add_argument("--nt", default="", help="wgather_split entry residency sweep: vcache_nt values (first "
+                   "non-temporal block), e.g. 0,16,32")
     a = p.parse_args()
     n = 1 << 24
     rows = n // 8
@@ -36,21 +38,28 @@ def main():
     yd = torch.empty(rows, dtype=torch.float64, device="cuda")
     s = torch.cuda.current_stream()
     kernels = a.kernels.split(",")
+    if a.nt:  # configurations "wgather_split@K": option vcache_nt = K
+        kernels = [k for k in kernels if k != "wgather_split"] + [f"wgather_split@{v}" for v in a.nt.split(",")]
     for shard in (int(v) for v in a.shards.split(",")):
         rp, ci, va = hs.gen_stripe_csr(shard * rows, rows, n, 32)
         h = hs.Handle.from_csr(rp, ci, va, rows, n)
         print(f"shard {shard}: AUTO FAST {h.kernel_name(hs.MODE_FAST)}, setup {h.stat('setup_ns') / 1e9:.2f} s, "
               f"split rows/block {h.stat('wgather_split_rows_per_block')}", flush=True)
+        def select(k):
+            name, _, nt = k.partition("@")
+            h.set_kernel(name)
+            h.set_option("vcache_nt", int(nt) if nt else -1)
+
         for k in kernels:  # build both layouts before timing
-            h.set_kernel(k)
+            select(k)
         absprod = np.bincount(np.repeat(np.arange(rows), 32), weights=np.abs(va * x[ci]), minlength=rows)
         bound = 2.0 * 33 * 2.0 ** -53 * absprod + 1e-300
         del rp, ci
         times = {k: [] for k in kernels}
-        bits = {}
+        bits, res = {}, {}
         for r in range(a.rounds):
             for k in kernels:
-                h.set_kernel(k)
+                select(k)
                 for _ in range(a.warm if r == 0 else 10):
                     h.exec_device(xd, yd, beta=0, mode=hs.MODE_FAST, stream=s)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -60,6 +69,7 @@ def main():
                 e1.record(s)
                 torch.cuda.synchronize()
                 times[k].append(e0.elapsed_time(e1) * 1e3 / a.launches)
+                res[k] = h.stat("resident_entry_bytes")
                 y = yd.cpu().numpy().tobytes()
                 assert bits.setdefault(k, y) == y, f"{k}: bits changed between launches"
                 print(f"  round {r} {k}: {times[k][-1]:.1f} us", flush=True)
@@ -72,7 +82,7 @@ def main():
                 dev = float(np.max(np.abs(ys[k] - ys[kernels[0]]) / bound))
                 assert dev <= 2.0, (k, dev)
                 msg = f", |y - y_{kernels[0]}| / bound max {dev:.3f}"
-            print(f"shard {shard} {k}: median {np.median(t):.1f} us, best {t.min():.1f} us, "
+            print(f"shard {shard} {k}: resident {res[k] / 1e6:.0f} MB, median {np.median(t):.1f} us, best {t.min():.1f} us, "
                   f"frac {alg / (np.median(t) * 1e-6) / 8e12:.4f}{msg}", flush=True)
         h.close()
 

@@ -1166,6 +1166,12 @@ def test_wgather_split_fast(gpu, dtype, shape):
         for chunk in (256, 256, 0, 3, 1):
             h.set_option("wgather_chunk", chunk)
             outs.append(h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST))
+        h.set_option("wgather_chunk", 256)
+        # entry residency (option vcache_nt: the first non-temporal block; -1 the budget rule): a cache
+        # policy, the same bits
+        for nt in (0, 1, 1 << 20, -1):
+            h.set_option("vcache_nt", nt)
+            outs.append(h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST))
         assert all(o.tobytes() == outs[0].tobytes() for o in outs), (shape, beta)
         y = outs[0]
         if dtype == np.uint64:
