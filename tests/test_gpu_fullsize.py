@@ -1,7 +1,9 @@
 """BASELINE.json's two largest single-GPU configurations at full size:
 C4 (2^24 x 2^24 stripe, 32 nnz/row, 537 M nonzeros) and C5 (R-MAT scale 24,
-263 M nonzeros, longest row 238,554 entries).  The CPU oracle would need
-minutes and ~20 GB per run at these sizes, so the checks are size-independent:
+263 M nonzeros, longest row 238,554 entries).  Whole-matrix checks against the
+C oracle's row-parallel CSR form (every row: ORDERED bit for bit, FAST within
+the bound; the form is pinned to the CSC scatter by tests/test_oracle.py), and
+size-independent ones:
 a sample of rows (first, last, the longest, 2,000 random) is recomputed
 sequentially in Python floats -- products rounded, then added in ascending
 column order, exactly SoftwareSpMV's arithmetic (SoftwareSpMV.cpp:59-64) --
@@ -15,6 +17,7 @@ import numpy as np
 import pytest
 
 import hipspmv as hs
+import oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -101,6 +104,47 @@ def test_full_size_sampled_rows(request, which, kernel, mode):
     _check(h, x, rows, want, absprod, lens, kernel, mode)
 
 
+def _whole_oracle(rowptr, colind, vals, x):
+    """y = A*x over every row by the oracle's row-parallel CSR restatement (oracle.c, 16 threads): each
+    row summed sequentially in its CSR (ascending column) order, SoftwareSpMV's order -- bit-identical to
+    the CSC scatter (tests/test_oracle.py::test_csr_rows_equal_csc_scatter)."""
+    _, y = oracle.time_spmv_csr_f64_mt(rowptr, colind, vals, x, 1, 16)
+    return y
+
+
+def _whole_absprod(rowptr, colind, vals, x, chunk=1 << 25):
+    """sum_e |a_e x[col_e]| per row (the FAST bound's scale), in row chunks."""
+    n = rowptr.size - 1
+    out = np.zeros(n)
+    r0 = 0
+    while r0 < n:
+        r1 = min(n, int(np.searchsorted(rowptr, rowptr[r0] + chunk, side="right")) - 1)
+        r1 = max(r1, r0 + 1)
+        e0, e1 = int(rowptr[r0]), int(rowptr[r1])
+        rows = np.repeat(np.arange(r1 - r0), np.diff(rowptr[r0:r1 + 1].astype(np.int64)))
+        out[r0:r1] = np.bincount(rows, weights=np.abs(vals[e0:e1] * x[colind[e0:e1]]), minlength=r1 - r0)
+        r0 = r1
+    return out
+
+
+@pytest.mark.parametrize("which", ["c4", "c5"])
+def test_full_size_whole_matrix_against_oracle(request, which):
+    """Every row of the full C4 / C5 matrix against the C oracle (the sampled-row checks
+    above re-derive ~2,000 rows in Python): AUTO ORDERED bit-identical over the whole y, AUTO FAST
+    within the per-row bound everywhere."""
+    h, x, _, _, _, lens = request.getfixturevalue(which)
+    n, rowptr, colind, vals = request.getfixturevalue(which + "_csr")
+    want = _whole_oracle(rowptr, colind, vals, x)
+    h.set_kernel("auto")
+    y_o = h.exec(x, beta=0, mode=hs.MODE_ORDERED)
+    bad = np.nonzero(y_o.view(np.uint64) != want.view(np.uint64))[0]
+    assert bad.size == 0, (which, h.kernel_name(hs.MODE_ORDERED), bad[:5])
+    y_f = h.exec(x, beta=0, mode=hs.MODE_FAST)
+    bound = 2.0 * np.maximum(lens, 1) * 2.0 ** -53 * _whole_absprod(rowptr, colind, vals, x) + 1e-300
+    over = np.nonzero(np.abs(y_f - want) > bound)[0]
+    assert over.size == 0, (which, h.kernel_name(hs.MODE_FAST), over[:5])
+
+
 def _checksum_u64(colind, vals, x, chunk=1 << 26):
     """sum_i y_i = sum_e a_e * x[col_e] (mod 2^64), in chunks."""
     s = np.uint64(0)
@@ -176,6 +220,9 @@ def test_c4_shard_auto_picks_wgather_split(c4_csr, shard):
         assert h.kernel_name(hs.MODE_FAST) == "wgather_split", h.kernel_name(hs.MODE_FAST)
         assert h.stat("wgather_split_rows_per_block") == 16384 and h.stat("wgather_split_units") == 256
         _check(h, x, sample, want, absprod, lens, "auto", hs.MODE_FAST)
+        y = h.exec(x, beta=0, mode=hs.MODE_FAST)  # every row of the shard against the C oracle
+        bound = 2.0 * np.maximum(lens, 1) * 2.0 ** -53 * _whole_absprod(rowptr, colind, vals, x) + 1e-300
+        assert np.all(np.abs(y - _whole_oracle(rowptr, colind, vals, x)) <= bound)
     finally:
         h.close()
     a = vals.view(np.uint64)

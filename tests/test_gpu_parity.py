@@ -136,9 +136,12 @@ def _random_csc(rows, cols, density, rng, dtype=np.float64, empty_rows=True, lon
 
 
 # (700, 20001): odd columns over 6 panels of the split geometry (2 per part, the last
-# panel patched); (900, 14001): 4 panels, column parts of 1, 1 and 2 (vc_part_first)
+# panel patched); (900, 14001): 4 panels, column parts of 1, 1 and 2 (vc_part_first);
+# (1, 40001), (64, 12001), (4097, 12001): ragged shapes wide enough for the split
+# geometry (its irregular coverage) -- one row, one row per lane group,
+# a block boundary one row past 4096, each with a full-width row
 @pytest.mark.parametrize("shape", [(1, 1), (1, 300), (300, 1), (257, 1000), (5000, 333), (3000, 20000),
-                                   (700, 20001), (900, 14001)])
+                                   (700, 20001), (900, 14001), (1, 40001), (64, 12001), (4097, 12001)])
 @pytest.mark.parametrize("kernel", ["vcache", "csr_lane", "csr_vector", "vcache_split", "sell", "wcsr",
                                     "vcache_split4", "vcache_flow"])
 def test_random_ragged(gpu, shape, kernel):

@@ -99,3 +99,26 @@ def test_dense_crosscheck_circuit204():
     x = np.random.default_rng(1).uniform(-1, 1, cols)
     y = oracle.spmv_csc(colptr, rowind, vals, x, rows=rows)
     np.testing.assert_allclose(y, A @ x, rtol=1e-12, atol=1e-14)
+
+
+def test_csr_rows_equal_csc_scatter():
+    # the oracle's row-parallel CSR form (oracle_time_spmv_csr_f64_mt: each row summed from +0.0 in its
+    # CSR order) gives SoftwareSpMV's CSC scatter bits on every row -- empty rows, a full-width row,
+    # repeated columns -- so the full-size GPU tests may use it as the whole-matrix oracle
+    rng = np.random.default_rng(21)
+    rows, cols = 30011, 5003
+    lens = rng.integers(0, 40, rows)
+    lens[rng.integers(0, rows, rows // 5)] = 0
+    per_row = [np.sort(rng.integers(0, cols, n)) for n in lens]  # sorted, with repeats
+    per_row[17] = np.arange(cols)
+    lens = np.array([c.size for c in per_row])
+    rowptr = np.zeros(rows + 1, np.uint32)
+    rowptr[1:] = np.cumsum(lens)
+    colind = np.concatenate(per_row).astype(np.uint32)
+    vals = rng.uniform(-1, 1, colind.size)
+    x = rng.uniform(-1, 1, cols)
+    colptr, rowind, cvals = oracle.csr2csc(rows, cols, rowptr, colind, vals)
+    want = oracle.spmv_csc(colptr, rowind, cvals, x, rows=rows)
+    for nt in (1, 7, 16):
+        _, y = oracle.time_spmv_csr_f64_mt(rowptr, colind, vals, x, 1, nt)
+        assert y.tobytes() == want.tobytes(), nt
