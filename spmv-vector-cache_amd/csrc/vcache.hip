@@ -542,12 +542,19 @@ __global__ __launch_bounds__(kVcThreads) void k_vcache(const uint32_t* __restric
     }
     for (uint32_t s = 0; s < nsteps; ++s) {
       if (s + 1 < npu) dma_x(s + 1);
+      if constexpr (AB & 32768) {
+        // ablation (wrong results, timing only): the loaders do not wait for their panel before the
+        // step barrier -- the bound on what decoupling the x latency from the step could gain
+        asm volatile("s_barrier" ::: "memory");
+        continue;
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t t_ready = (AB & 8192) ? tr_now() : 0;
       if (s + 1 < npu) patch_x(s + 1);
       pbarrier();
       tr_rel(s, t_ready, t_ready);
     }
+    if constexpr (AB & 32768) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else if (loader && LD == 2) {
     // same ring, asm loads: storing x(s+1) waits for it with x(s+2)'s NJ
     // loads (issued one step later) still in flight

@@ -26,8 +26,9 @@ using namespace hipspmv;
     }                                                                        \
   } while (0)
 
-template <typename T>
-T* up(const std::vector<T>& v) {
+template <typename V>
+auto up(const V& v) {  // any contiguous host array (std::vector, the layouts' hvec)
+  using T = std::remove_const_t<std::remove_reference_t<decltype(*v.data())>>;
   T* d;
   CK(hipMalloc(&d, sizeof(T) * std::max<size_t>(v.size(), 1)));
   CK(hipMemcpy(d, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
@@ -73,6 +74,8 @@ int main(int argc, char** argv) {
   for (VcGeom g : {kVcOrdered, kVcSplit, kVcSplit4}) {
     VcacheLayout L;
     build_vcache(a, g, L);
+    const bool dmawait = argc > 2 && std::string(argv[2]) == "dmawait";
+    if (dmawait && g.split == 3) place_segments_banked(L, kVcSplitCT);  // the product layout (CX 5 needs it)
     // tickets: 2 per block for the combine + 8 stamp words per unit (AB & 128)
     uint32_t* dtick = up(std::vector<uint32_t>(2 * L.nblocks + 8 * L.nblocks * g.split, 0));
     VcacheArgs A{up(L.seg), up(L.code), up(L.vals), dx, dy, dy, dpart, dtick,
@@ -160,6 +163,16 @@ int main(int argc, char** argv) {
         std::printf("    slot%%8=%u main loop median %7.2f max %7.2f\n", x, lx[lx.size() / 2], lx.back());
       }
     };
+    if (dmawait) {  // round 6: the product against loaders that skip their DMA wait (AB 32768)
+      if (g.split == 3)
+        for (int r = 0; r < 4; ++r) {
+          variant(k_vcache<double, 3, 3, 4, 2, 256, 0, false, 1, 5>, 3, "product (CX5, nt b >= nb/2)", 0,
+                  13 * 64 * 2);
+          variant(k_vcache<double, 3, 3, 4, 2, 256 | 32768, 0, false, 1, 5>, 3, "loaders skip the DMA wait", 32768,
+                  13 * 64 * 2);
+        }
+      continue;
+    }
     if (argc > 2 && std::string(argv[2]) == "stamps") {
       if (g.split == 3) {
         stamps(k_vcache<double, 3, 3, 4, 2, 128, 0, false, 1, 3>, "product (split 3)");
