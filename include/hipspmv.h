@@ -91,8 +91,9 @@ extern "C" {
                                  workgroup each); ordered in ORDERED mode (FAST:
                                  long rows cut into pieces); any matrix */
 #define HIPSPMV_KERNEL_WGATHER_SPLIT 10 /* "wgather_split": k_wgather over two column
-                                  halves of 16384-row blocks, part 0 on XCDs 0-3 and
-                                  part 1 on XCDs 4-7, y = p0 + p1; fast,
+                                  halves of 16384-row blocks (part 0 on XCDs 0-3,
+                                  part 1 on XCDs 4-7; option "wgather_map" 1
+                                  alternates them), y = p0 + p1; fast,
                                   deterministic; chosen by AUTO (FAST) for wide x
                                   with at most 2^21 rows (a C4 shard) */
 
@@ -135,7 +136,13 @@ int hipspmv_create_csr(const uint32_t *rowptr, const uint32_t *colind, const voi
  * vcache_nt of VCACHE / VCACHE_SPLIT load their entries non-temporally, the
  * blocks before them stay in the Infinity Cache across launches; -1 default:
  * about 192 MiB of entries resident -- C3: half the blocks of either; WGATHER:
- * 0 or -1 non-temporal, > 0 the default policy), "sell_nt" (SELL slices s >=
+ * 0 or -1 non-temporal, > 0 the default policy; WGATHER_SPLIT: the first
+ * non-temporal row block, -1 the leading blocks that fit 232 MiB less x and y),
+ * "wgather_chunk" (row blocks per WGATHER launch, 256 default; WGATHER_SPLIT
+ * halves it per launch: two units per block), "wgather_map" (WGATHER_SPLIT:
+ * 0 default, column half 0 on XCDs 0-3 and half 1 on 4-7; 1 alternating; the
+ * same bits), "wcsr_xcd" (1 = WCSR's segment pass placed by XCD eighths of its
+ * window order; the same bits; 0 default), "sell_nt" (SELL slices s >=
  * sell_nt likewise; -1 default: the second half).  The cache policy never
  * changes a result bit.  "vcache_xmask" (1 default: VCACHE's x loaders skip
  * the 128-byte x lines no entry of a unit's panel uses; 0 = load every line;

@@ -259,6 +259,7 @@ struct hipspmv_handle {
   int64_t wcsr_res = 0;
   int wcsr_reduce = 0;    // option "wcsr_reduce": 0 the compact reduce over rows with segments, 1 every row
   int wcsr_xcd = 0;       // option "wcsr_xcd": 1 the segment pass's blocks placed by XCD eighths (kernels.hip)
+  int wgather_map = 0;    // option "wgather_map": wgather_split's halves 0 by XCD, 1 alternating (diagnostic)
   int wcsr_fill = -1;     // option "wcsr_fill": 1 the rows without segments written by the segment pass's
                           // launch, 0 by the reduce's; -1 (default) 1 when two thirds of the rows are empty
   // option "sell_nt": SELL slices s >= sell_nt load their entries
@@ -687,7 +688,7 @@ static int auto_pick(const hipspmv_t* h, bool fast_ok, bool built) {
   if (!fast_ok && worth(h->vc[0], h->vc0_eligible))
     return !built || h->vc[0].ok ? HIPSPMV_KERNEL_VCACHE : h->sell.built ? HIPSPMV_KERNEL_SELL : generic;
   // FAST with at most 2^21 rows (a C4 shard): the two-part form, 16384-row
-  // blocks with each XCD's L2 holding half of x (2^21 x 2^24 stripe shard:
+  // blocks, each XCD's L2 holding half of x (2^21 x 2^24 stripe shard:
   // DESIGN.md §6.18)
   if (fast_ok && !h->vc0_eligible && h->wgs_eligible && h->wg_max_run <= kVcRunMax)
     return !built || h->vc[4].ok ? HIPSPMV_KERNEL_WGATHER_SPLIT : generic;
@@ -1185,6 +1186,7 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
       const uint32_t fit = (uint32_t)(std::upper_bound(v.block_first.begin(), v.block_first.end(), budget) -
                                       v.block_first.begin()) - 1;  // block_first[fit] <= budget
       a.nt_from = (uint32_t)std::min<int64_t>(h->vcache_nt >= 0 ? h->vcache_nt : fit, v.nblocks);
+      a.map = h->wgather_map;
       h->resident_entry_bytes = 12ull * v.block_first[a.nt_from];
     }
     e = launch_wgather(h->dtype, a, s);
@@ -1412,6 +1414,9 @@ int hipspmv_set_option(hipspmv_t* h, const char* key, int64_t value) {
   } else if (k == "wcsr_fill") {  // 1: empty rows filled beside the segment pass; 0: after the reduce; -1: by rule
     if (value < -1 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
     h->wcsr_fill = (int)value;
+  } else if (k == "wgather_map") {  // wgather_split: 0 halves by XCD (default), 1 alternating (A/B); same bits
+    if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
+    h->wgather_map = (int)value;
   } else if (k == "wcsr_xcd") {  // 1: segment-pass blocks by XCD eighths of the window order; same bits
     if (value < 0 || value > 1) return HIPSPMV_ERR_INVALID_ARG;
     h->wcsr_xcd = (int)value;

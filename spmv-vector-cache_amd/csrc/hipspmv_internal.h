@@ -52,7 +52,9 @@ constexpr VcGeom kWgWindow{16384, 1 << 16, 1, 16, 512};
 // layout's 8192 -- and each block's windows are cut in two halves, so the
 // 256 work units still fill the chip once.  Units of part 0 run on XCDs 0-3,
 // part 1 on XCDs 4-7 (workgroup w lands on XCD w mod 8): each XCD's L2 pulls
-// half of x through instead of all of it.  y = p0 + p1 in part order
+// half of x through instead of all of it -- half the memory-side x traffic,
+// though not faster than alternating the parts (the gain is
+// the 16384-row blocks and the entry residency).  y = p0 + p1 in part order
 // (owner combine, combine.h): deterministic, not bit-identical to ORDERED.
 constexpr VcGeom kWgSplit{16384, 1 << 16, 2, 16, 512};
 // kWgSplit entry residency: the leading row blocks whose entries fit in

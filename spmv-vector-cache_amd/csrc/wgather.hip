@@ -45,7 +45,8 @@ __device__ __forceinline__ void wgather_body(const uint32_t* __restrict__ seg, c
                                              const T* __restrict__ y_in, T* __restrict__ y_out, uint32_t rows,
                                              uint32_t rows_per_block, uint32_t npanels, uint32_t npad, uint32_t last,
                                              int beta, uint32_t b0, T* __restrict__ partial,
-                                             uint32_t* __restrict__ tickets, uint32_t nblocks, uint32_t nt_from) {
+                                             uint32_t* __restrict__ tickets, uint32_t nblocks, uint32_t nt_from,
+                                             int xmap) {
 #pragma clang fp contract(off)
   static_assert(PARTS == 1 || PARTS == 2, "one or two column parts");
   constexpr int VT = kVcThreads;
@@ -56,7 +57,9 @@ __device__ __forceinline__ void wgather_body(const uint32_t* __restrict__ seg, c
   const int t = threadIdx.x;
   uint32_t b = b0 + blockIdx.x, h = 0;  // this launch's blocks start at b0 (launch chunks, kWgChunk)
   if constexpr (PARTS == 2) {
-    const uint32_t u = blockIdx.x, full = gridDim.x & ~7u;
+    // xmap 1 (option wgather_map, diagnostic): the halves alternate, h = u mod 2, so every XCD runs
+    // units of both halves -- the A/B of the XCD placement
+    const uint32_t u = blockIdx.x, full = xmap ? 0u : gridDim.x & ~7u;
     if (u < full) {
       h = (u & 7u) >> 2;
       b = b0 + (u >> 3) * 4 + (u & 3u);
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather(const uint32_t* __restri
                                                          uint32_t rows, uint32_t rows_per_block, uint32_t npanels,
                                                          uint32_t npad, uint32_t last, int beta, uint32_t b0) {
   wgather_body<T, CB, DE, EPT, NTE, MSK, 1>(seg, ecode, evals, x, y_in, y_out, rows, rows_per_block, npanels, npad,
-                                            last, beta, b0, nullptr, nullptr, 0, 0);
+                                            last, beta, b0, nullptr, nullptr, 0, 0, 0);
 }
 
 template <typename T, int CB, int DE, int EPT, bool NTE = false, bool MSK = false>
@@ -182,9 +185,9 @@ __global__ __launch_bounds__(kVcThreads) void k_wgather_split(
     const uint32_t* __restrict__ seg, const uint32_t* __restrict__ ecode, const T* __restrict__ evals,
     const T* __restrict__ x, const T* __restrict__ y_in, T* __restrict__ y_out, uint32_t rows,
     uint32_t rows_per_block, uint32_t npanels, uint32_t npad, uint32_t last, int beta, uint32_t b0,
-    T* __restrict__ partial, uint32_t* __restrict__ tickets, uint32_t nblocks, uint32_t nt_from) {
+    T* __restrict__ partial, uint32_t* __restrict__ tickets, uint32_t nblocks, uint32_t nt_from, int xmap) {
   wgather_body<T, CB, DE, EPT, NTE, MSK, 2>(seg, ecode, evals, x, y_in, y_out, rows, rows_per_block, npanels, npad,
-                                            last, beta, b0, partial, tickets, nblocks, nt_from);
+                                            last, beta, b0, partial, tickets, nblocks, nt_from, xmap);
 }
 
 // Pipelined form (option vcache_xlane 2; every segment must fit the register
@@ -333,7 +336,7 @@ static void launch_one(const VcacheArgs& a, uint32_t n, uint32_t b0, hipStream_t
     hipLaunchKernelGGL((k_wgather_split<T, CB, DE, EPT, NTE, MSK>), dim3(2 * n), dim3(kVcThreads), 0, s, a.seg,
                        a.code, (const T*)a.vals, (const T*)a.x, (const T*)a.y_in, (T*)a.y_out, a.rows,
                        a.rows_per_block, a.npanels, a.npad, a.last, a.beta, b0, (T*)a.partial, a.tickets, a.nblocks,
-                       a.nt_from);
+                       a.nt_from, a.map);
 }
 
 template <typename T, int PARTS>

@@ -43,6 +43,7 @@ for s in ${STEPS:-streams}; do
             step pmc_c4s7_wg_summary 60 python3 spmv-vector-cache_amd/tools/pmc_summary.py $OUT/pmc_c4s7_wgather_summary.csv "k_wgather<double," $OUT/pmc_c4s7_wgather_[0-9]*/*counter_collection.csv ;;
     c5wg) step c5_wg 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set wg --shards 0,3,7 ;;
     whole) step pytest_whole 900 python -u -m pytest -x -v -p no:cacheprovider --timeout 600 --timeout-method thread -m gpu tests/test_gpu_fullsize.py tests/test_gpu_parity.py -k "whole or c4_shard or random_ragged" ;;
+    wgsmap) step wgs_map 600 python -u spmv-vector-cache_amd/tools/wgs_ab.py --kernels "wgather,wgather_split,wgather_split#alt" --rounds 4 ;;
     dmawait) step dmawait 300 ./spmv-vector-cache_amd/lib/vc_ablate 20 dmawait ;;
     pytest) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;

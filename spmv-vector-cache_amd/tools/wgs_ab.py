@@ -45,10 +45,13 @@ def main():
         h = hs.Handle.from_csr(rp, ci, va, rows, n)
         print(f"shard {shard}: AUTO FAST {h.kernel_name(hs.MODE_FAST)}, setup {h.stat('setup_ns') / 1e9:.2f} s, "
               f"split rows/block {h.stat('wgather_split_rows_per_block')}", flush=True)
-        def select(k):
-            name, _, nt = k.partition("@")
+        def select(k):  # "kernel", "kernel@NT" (option vcache_nt), "wgather_split#alt" (option wgather_map 1)
+            name, _, alt = k.partition("#")
+            name, _, nt = name.partition("@")
             h.set_kernel(name)
             h.set_option("vcache_nt", int(nt) if nt else -1)
+            if name == "wgather_split":
+                h.set_option("wgather_map", 1 if alt == "alt" else 0)
 
         for k in kernels:  # build both layouts before timing
             select(k)

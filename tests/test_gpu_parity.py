@@ -1175,6 +1175,9 @@ def test_wgather_split_fast(gpu, dtype, shape):
         for nt in (0, 1, 1 << 20, -1):
             h.set_option("vcache_nt", nt)
             outs.append(h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST))
+        h.set_option("wgather_map", 1)  # the halves alternating over the XCDs (A/B placement): same bits
+        outs.append(h.exec(x, y0.copy(), beta=beta, mode=hs.MODE_FAST))
+        h.set_option("wgather_map", 0)
         assert all(o.tobytes() == outs[0].tobytes() for o in outs), (shape, beta)
         y = outs[0]
         if dtype == np.uint64:
