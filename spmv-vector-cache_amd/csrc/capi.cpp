@@ -224,6 +224,8 @@ struct hipspmv_handle {
              *d_segidx = nullptr, *d_rgroups = nullptr, *d_chunks = nullptr;
     // the compact reduce (k_wreduce_c): rows with segments, their offsets, groups, the bitmap
     uint32_t *d_rrow = nullptr, *d_rsegc = nullptr, *d_cgroups = nullptr, *d_nebits = nullptr;
+    uint32_t* d_hot = nullptr;  // hot-column form: [window][hotk] column ids staged in LDS (k_wpass_hot)
+    uint32_t hotk = 0;
     uint64_t *d_vals = nullptr, *d_ypart = nullptr;
     uint32_t nseg = 0, ngroups = 0, rgroups = 0, ncgroups = 0, nrows_ne = 0, max_seg = 0, log2w = 0, nchunks = 0;
     std::vector<uint32_t> group_first;  // ngroups + 1: first entry of each segment-pass group (host)
@@ -259,6 +261,7 @@ struct hipspmv_handle {
   int64_t wcsr_res = 0;
   int wcsr_reduce = 0;    // option "wcsr_reduce": 0 the compact reduce over rows with segments, 1 every row
   int wcsr_xcd = 0;       // option "wcsr_xcd": 1 the segment pass's blocks placed by XCD eighths (kernels.hip)
+  uint32_t wcsr_hot = 0;  // wcsr hot-column form: K (8192 / 16384) or 0 (HIPSPMV_WCSR_HOT at create)
   int wgather_map = 0;    // option "wgather_map": wgather_split's halves 0 by XCD, 1 alternating (diagnostic)
   int wcsr_fill = -1;     // option "wcsr_fill": 1 the rows without segments written by the segment pass's
                           // launch, 0 by the reduce's; -1 (default) 1 when two thirds of the rows are empty
@@ -343,7 +346,7 @@ static void release(hipspmv_t* h) {
   {
     auto& w = h->wc;
     ptrs.insert(ptrs.end(), {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks,
-                             w.d_vals, w.d_ypart, w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits});
+                             w.d_vals, w.d_ypart, w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits, w.d_hot});
   }
   ptrs.push_back(h->d_vfprof);
   ptrs.insert(ptrs.end(), {h->vf.d_code, h->vf.d_wbeg, h->vf.d_wend, h->vf.d_tickets, h->vf.d_vals, h->vf.d_partial,
@@ -461,12 +464,12 @@ static void drop_partial_layouts(hipspmv_t* h) {
   if (!h->wc.built) {
     auto& w = h->wc;
     void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks, w.d_vals, w.d_ypart,
-                  w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits};
+                  w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits, w.d_hot};
     for (void* p : wp)
       if (p) (void)hipFree(p);
     w = hipspmv_handle::Wc{};
   }
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < 5; ++k)
     if (!h->vc[k].ok && (h->vc[k].d_seg || h->vc[k].d_code || h->vc[k].d_vals)) {
       const auto keep = h->vc[k];  // the ordered geometry is known before its entries exist
       free_vc(h, k);
@@ -565,8 +568,24 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   if (const char* e = std::getenv("HIPSPMV_WCSR_MAXSEG")) cap = (uint32_t)std::max(64, std::atoi(e));
   WinLayout L;
   build_windowed(a, log2w, L, cap, !lds && h->wcsr_line_order);
+  // the hot-column form (kernels.hip k_wpass_hot): each window's K most frequent columns staged in
+  // LDS by every segment-pass workgroup (HIPSPMV_WCSR_HOT=K at create: 8192 or 16384; 0 off)
+  uint32_t hotk = h->wcsr_hot;
+  if (const char* e = std::getenv("HIPSPMV_WCSR_HOT")) hotk = (uint32_t)std::max(0, std::atoi(e));
+  if (!kExperimental) hotk = 0;  // measured slower: experimental build only
+  if (hotk != 8192 && hotk != kWcHotMax) hotk = 0;
+  std::vector<uint32_t> hot;
+  if (lds || !hotk || !mark_hot_columns(L, hotk, hot)) {  // (the remap runs only for a hot layout)
+    hotk = 0;
+    hot.clear();
+  }
   std::vector<uint32_t> groups, chunks;
-  if (lds) {  // csr_vector groups inside each window, cut into chunks of <= kWsChunkNnz entries
+  if (lds || hotk) {  // csr_vector groups inside each window, cut into chunks of <= kWsChunkNnz entries
+    // (hot form: chunks of about nnz / 240 entries -- one wave of 1024-thread workgroups over the chip,
+    // each staging its window's hot columns once)
+    // (8192 hot columns: 64 KiB of LDS, two workgroups per CU -- twice the chunks)
+    const uint32_t chunk_nnz =
+        lds ? kWsChunkNnz : std::max<uint32_t>(8192u, (uint32_t)(a.nnz / (hotk == kWcHotMax ? 240u : 480u) + 1));
     const auto& rp = L.seg.rowptr;
     for (uint32_t win = 0; win + 1 < L.winseg.size(); ++win) {
       const uint32_t s0 = L.winseg[win], s1 = L.winseg[win + 1];
@@ -576,7 +595,7 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
       uint32_t cg = (uint32_t)groups.size(), cnnz = 0;
       for (size_t i = 0; i + 1 < wg.size(); ++i) {
         const uint32_t n = rp[s0 + wg[i + 1]] - rp[s0 + wg[i]];
-        if (cnnz && cnnz + n > kWsChunkNnz) {
+        if (cnnz && cnnz + n > chunk_nnz) {
           chunks.insert(chunks.end(), {win, cg, (uint32_t)groups.size()});
           cg = (uint32_t)groups.size();
           cnnz = 0;
@@ -593,7 +612,7 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   const uint64_t bytes0 = h->device_bytes;
   auto fail = [&](int st) {
     void* wp[] = {w.d_rowptr, w.d_colind, w.d_groups, w.d_rowseg, w.d_segidx, w.d_rgroups, w.d_chunks,
-                  w.d_vals, w.d_ypart, w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits};
+                  w.d_vals, w.d_ypart, w.d_rrow, w.d_rsegc, w.d_cgroups, w.d_nebits, w.d_hot};
     for (void* p : wp)
       if (p) (void)hipFree(p);
     w = hipspmv_handle::Wc{};
@@ -608,6 +627,8 @@ static int build_wcsr_layout(hipspmv_t* h, const HostCSR& a) {
   if (!chunks.empty() && (st = dev_upload(&w.d_chunks, chunks.data(), chunks.size(), h->device_bytes)))
     return fail(st);
   w.nchunks = (uint32_t)(chunks.size() / 3);
+  if (hotk && (st = dev_upload(&w.d_hot, hot.data(), hot.size(), h->device_bytes))) return fail(st);
+  w.hotk = hotk;
   if ((st = dev_upload(&w.d_rowseg, L.rowseg.data(), L.rowseg.size(), h->device_bytes))) return fail(st);
   if ((st = dev_upload(&w.d_segidx, L.segidx.data(), L.segidx.size(), h->device_bytes))) return fail(st);
   {  // the reduce is a csr_vector over (rowseg, segidx) with ypart as x: its own balanced row groups
@@ -1196,6 +1217,8 @@ static int launch(hipspmv_t* h, int kernel, const void* d_x, const void* d_y_in,
                w.d_rgroups, w.rgroups,   sc ? sc->wc_ypart : w.d_ypart, d_x, d_y_in, d_y_out, h->rows, beta};
     a.chunks = w.d_chunks;
     a.nchunks = w.nchunks;
+    a.hot = w.d_hot;
+    a.hotk = w.hotk;
     a.res_groups = (uint32_t)std::min<int64_t>(h->wcsr_res, w.ngroups);
     h->resident_entry_bytes = w.group_first.empty() ? 0 : 12ull * w.group_first[a.res_groups];
     a.cols = h->cols;
@@ -1613,6 +1636,7 @@ int hipspmv_stat(hipspmv_t* h, const char* key, uint64_t* out) {
   else if (k == "wcsr_max_segment") *out = h->wc.max_seg;
   else if (k == "wcsr_window_log2") *out = h->wc.built ? h->wc.log2w : kWcLog2Window;
   else if (k == "wcsr_chunks") *out = h->wc.nchunks;
+  else if (k == "wcsr_hot") *out = h->wc.hotk;
   else if (k == "wcsr_groups") *out = h->wc.ngroups;
   else if (k == "wcsr_reduce_groups") *out = h->wc.built ? (h->wcsr_reduce == 0 ? h->wc.ncgroups : h->wc.rgroups) : 0;
   else if (k == "wcsr_rows_with_segments") *out = h->wc.nrows_ne;

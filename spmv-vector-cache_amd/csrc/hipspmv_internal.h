@@ -133,6 +133,13 @@ constexpr uint32_t kWcLog2Window = 20;
 // 1024-thread workgroup
 constexpr uint32_t kWsLog2Window = 14;
 constexpr uint32_t kWsChunkNnz = 49152;
+// wcsr hot-column form (round 6): per 2^kWcLog2Window window
+// the K most frequent columns of the layout's entries (R-MAT: 16384 of 2^20
+// columns carry ~60 % of a window's entries) are staged in LDS by each
+// workgroup of the segment pass; their entries' colind become kWcHotFlag |
+// slot, the rest gather from global memory as before.
+constexpr uint32_t kWcHotFlag = 1u << 31;
+constexpr uint32_t kWcHotMax = 16384;
 constexpr uint32_t kWcMinCols = 1u << 21;
 
 // ---- csr_vector geometry ---------------------------------------------------
@@ -393,6 +400,12 @@ void build_sell(const HostCSR& a, SellLayout& out);
 // column (then row), so a wave's gathers share lines; else by row
 void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t cap = UINT32_MAX,
                     bool by_line = false);
+// The hot-column form of a global-x windowed layout: for each window w, its
+// K most frequent columns ascending at hot[w * K ...] (padded with column 0),
+// and every entry of such a column rewritten to kWcHotFlag | its slot.  The
+// sums are unchanged (the same x values, read from LDS).  False (layout
+// untouched) when a column id would collide with the flag.
+bool mark_hot_columns(WinLayout& L, uint32_t K, std::vector<uint32_t>& hot);
 // Segments build_windowed would make (one pass, no allocation).
 uint64_t windowed_segments(const HostCSR& a, uint32_t log2w);
 // Cost-balanced contiguous row partition (plan.cpp; hipspmv_partition_rows):

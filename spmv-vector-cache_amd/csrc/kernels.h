@@ -75,6 +75,10 @@ struct WcsrArgs {  // csr_vector over the column-windowed segment matrix, then k
   uint32_t ncgroups = 0;
   int fill_early = 0;  // the rows without segments written by the segment pass's launch (k_wpass_fill)
   int xcd = 0;         // option wcsr_xcd: segment-pass blocks placed by XCD eighths of the window order
+  // hot-column form (k_wpass_hot, needs chunks): [window][hotk] columns each workgroup stages in LDS;
+  // entries with colind & kWcHotFlag read slot colind & ~kWcHotFlag of it
+  const uint32_t* hot = nullptr;
+  uint32_t hotk = 0;
 };
 
 struct SellArgs {

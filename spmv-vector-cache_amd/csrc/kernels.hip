@@ -238,6 +238,37 @@ __device__ __forceinline__ uint32_t wcsr_block(uint32_t xper) {
   return xper ? (blockIdx.x & 7u) * xper + (blockIdx.x >> 3) : blockIdx.x;
 }
 
+// k_wpass_hot (wcsr, hot-column form): one chunk (window,
+// first group, end group) per 1024-thread workgroup, as k_wseg, but over the
+// global-x windows: the window's HK hot columns (mark_hot_columns, csrc/plan.cpp)
+// are gathered into LDS once, then 16 waves run the chunk's csr_vector groups
+// with the hot entries' x from LDS and the others from global memory.  The
+// same products in the same order as k_csr_vector over these groups.
+// Measured slower than the product's segment pass on every C5 shard (§6.19):
+// experimental build only (make EXPERIMENTAL=1, HIPSPMV_WCSR_HOT=K at create).
+#ifdef HIPSPMV_EXPERIMENTAL_KERNELS
+template <typename T, uint32_t HK>
+__global__ __launch_bounds__(1024) void k_wpass_hot(const uint32_t* __restrict__ chunks,
+                                                    const uint32_t* __restrict__ groups,
+                                                    const uint32_t* __restrict__ rowptr,
+                                                    const uint32_t* __restrict__ colind, const T* __restrict__ vals,
+                                                    const T* __restrict__ x, const uint32_t* __restrict__ hot,
+                                                    T* __restrict__ ypart) {
+  __shared__ T xh[HK];
+  __shared__ uint32_t heads[16][kCvGroupNnz / 32];
+  const uint32_t* ck = chunks + 3 * (size_t)blockIdx.x;
+  const uint32_t win = ck[0], g0 = ck[1], g1 = ck[2];
+  const uint32_t* hw = hot + (size_t)win * HK;
+  for (uint32_t i = threadIdx.x; i < HK; i += 1024) xh[i] = x[hw[i]];
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  auto xv = [&](uint32_t c) { return (c & kWcHotFlag) ? xh[c & (HK - 1)] : x[c]; };
+  for (uint32_t g = g0 + (uint32_t)w; g < g1; g += 16)
+    csr_vector_rows<T, 3>(rowptr, colind, vals, xv, RowOut<T>{(const T*)nullptr, ypart, 0}, groups[g], groups[g + 1],
+                          heads[w]);
+}
+#endif
+
 // NTE: the wcsr segment pass (KIND 1 above)
 template <typename T, bool NTE = false>
 __global__ __launch_bounds__(256) void k_csr_vector(const uint32_t* __restrict__ rowptr,
@@ -381,7 +412,18 @@ template <typename T>
 hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
   // the segment partials: csr_vector over A', beta 0, entries non-temporal;
   // the LDS form when the layout has window chunks
-  if (a.nchunks)
+  if (a.nchunks && a.hot) {
+#ifdef HIPSPMV_EXPERIMENTAL_KERNELS
+    if (a.hotk == kWcHotMax)
+      hipLaunchKernelGGL((k_wpass_hot<T, kWcHotMax>), dim3(a.nchunks), dim3(1024), 0, s, a.chunks, a.groups,
+                         a.seg_rowptr, a.seg_colind, (const T*)a.seg_vals, (const T*)a.x, a.hot, (T*)a.ypart);
+    else
+      hipLaunchKernelGGL((k_wpass_hot<T, 8192>), dim3(a.nchunks), dim3(1024), 0, s, a.chunks, a.groups,
+                         a.seg_rowptr, a.seg_colind, (const T*)a.seg_vals, (const T*)a.x, a.hot, (T*)a.ypart);
+#else
+    return hipErrorNotSupported;  // (capi builds hot layouts only in the experimental build)
+#endif
+  } else if (a.nchunks)
     hipLaunchKernelGGL(k_wseg<T>, dim3(a.nchunks), dim3(1024), 0, s, a.chunks, a.groups, a.seg_rowptr, a.seg_colind,
                        (const T*)a.seg_vals, (const T*)a.x, a.cols, (T*)a.ypart);
   const bool fill_early = a.rrow && a.fill_early && !a.nchunks && !a.res_groups;
@@ -394,6 +436,9 @@ hipError_t launch_wcsr(const WcsrArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_wpass_fill<T>, dim3(grid_of(nb)), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,
                        (const T*)a.seg_vals, (const T*)a.x, (T*)a.ypart, a.groups, a.ngroups, a.nebits,
                        (const T*)a.y_in, (T*)a.y_out, a.rows, a.beta, nfill, xper_of(nb));
+  } else if (a.nchunks) {
+    // (the chunked forms above wrote every segment partial; the hot form's colind carry the LDS flag and
+    // must not reach a global-x pass)
   } else if (a.ngroups && a.xcd && !a.res_groups) {
     const uint32_t nb = (a.ngroups + 3) / 4;
     hipLaunchKernelGGL(k_wpass_x<T>, dim3(grid_of(nb)), dim3(256), 0, s, a.seg_rowptr, a.seg_colind,

@@ -1158,6 +1158,50 @@ void build_windowed(const HostCSR& a, uint32_t log2w, WinLayout& out, uint32_t c
   });
 }
 
+// The hot-column form (hipspmv_internal.h): one window per thread; a dense
+// counter and slot map of the window's 2^log2w columns, the K most frequent
+// columns by (count descending, column ascending), their slots in column
+// order (the segment pass stages them in LDS with one gather per slot, so
+// neighbouring slots share x lines).
+bool mark_hot_columns(WinLayout& L, uint32_t K, std::vector<uint32_t>& hot) {
+  HostCSR& g = L.seg;
+  if ((uint64_t)g.cols > kWcHotFlag || K == 0) return false;
+  const uint32_t nwin = (uint32_t)L.winseg.size() - 1, W = 1u << L.log2w;
+  hot.assign((size_t)nwin * K, 0u);
+  const unsigned nt = std::max(1u, std::min(plan_threads(), nwin));
+  par_chunks(nwin, nt, [&](unsigned, uint64_t w0, uint64_t w1) {
+    std::vector<uint32_t> cnt(W), slot(W);
+    std::vector<uint64_t> cand;
+    for (uint64_t w = w0; w < w1; ++w) {
+      const uint64_t e0 = g.rowptr[L.winseg[w]], e1 = g.rowptr[L.winseg[w + 1]];
+      if (e0 == e1) continue;
+      const uint32_t c0 = (uint32_t)(w << L.log2w);
+      std::fill(cnt.begin(), cnt.end(), 0u);
+      for (uint64_t e = e0; e < e1; ++e) cnt[g.colind[e] - c0]++;
+      cand.clear();
+      for (uint32_t c = 0; c < W; ++c)  // key: count descending, then column ascending
+        if (cnt[c]) cand.push_back((uint64_t)(UINT32_MAX - cnt[c]) << 32 | c);
+      const size_t k = std::min<size_t>(K, cand.size());
+      std::nth_element(cand.begin(), cand.begin() + (k ? k - 1 : 0), cand.end());
+      std::vector<uint32_t> cols(k);
+      for (size_t i = 0; i < k; ++i) cols[i] = (uint32_t)cand[i];
+      std::sort(cols.begin(), cols.end());
+      std::fill(slot.begin(), slot.end(), UINT32_MAX);
+      uint32_t* hw = hot.data() + (size_t)w * K;
+      for (size_t i = 0; i < k; ++i) {
+        slot[cols[i]] = (uint32_t)i;
+        hw[i] = c0 + cols[i];
+      }
+      for (size_t i = k; i < K; ++i) hw[i] = c0;  // padding: never referenced
+      for (uint64_t e = e0; e < e1; ++e) {
+        const uint32_t sl = slot[g.colind[e] - c0];
+        if (sl != UINT32_MAX) g.colind[e] = kWcHotFlag | sl;
+      }
+    }
+  });
+  return true;
+}
+
 // Greedy row groups: consecutive rows while the group stays within
 // kCvGroupNnz nonzeros and kCvGroupRows rows; a longer row is a group alone.
 // No group crosses a multiple of HIPSPMV_SHARD_ALIGN rows, so the groups of a

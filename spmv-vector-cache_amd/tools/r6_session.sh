@@ -44,6 +44,14 @@ for s in ${STEPS:-streams}; do
     c5wg) step c5_wg 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set wg --shards 0,3,7 ;;
     whole) step pytest_whole 900 python -u -m pytest -x -v -p no:cacheprovider --timeout 600 --timeout-method thread -m gpu tests/test_gpu_fullsize.py tests/test_gpu_parity.py -k "whole or c4_shard or random_ragged" ;;
     wgsmap) step wgs_map 600 python -u spmv-vector-cache_amd/tools/wgs_ab.py --kernels "wgather,wgather_split,wgather_split#alt" --rounds 4 ;;
+    hottests) HIPSPMV_EXPERIMENTAL=1 HIPSPMV_WCSR_HOT=16384 step pytest_hot 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_multi.py -k "wcsr" &&
+              HIPSPMV_EXPERIMENTAL=1 HIPSPMV_WCSR_HOT=8192 step pytest_hot8k 600 $PYT -m gpu tests/test_gpu_parity.py -k "wcsr" ;;
+    hotab) step c5_hot_off 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set one --shards 0,3,7 &&
+           HIPSPMV_EXPERIMENTAL=1 HIPSPMV_WCSR_HOT=16384 step c5_hot_16k 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set one --shards 0,3,7 &&
+           HIPSPMV_EXPERIMENTAL=1 HIPSPMV_WCSR_HOT=8192 step c5_hot_8k 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set one --shards 0,3,7 ;;
+    hotab2) step c5_hot_off 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set one --shards 0,3,7 &&
+            HIPSPMV_EXPERIMENTAL=1 HIPSPMV_WCSR_HOT=8192 step c5_hot_8k 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set one --shards 0,3,7 ;;
+    graph) step pytest_graph 300 $PYT -m gpu tests/test_gpu_parity.py -k "graph_capture" ;;
     dmawait) step dmawait 300 ./spmv-vector-cache_amd/lib/vc_ablate 20 dmawait ;;
     pytest) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python bench.py ;;

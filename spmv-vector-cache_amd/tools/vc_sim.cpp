@@ -639,6 +639,36 @@ int main(int argc, char** argv) {
         std::vector<uint32_t> gg;
         build_row_groups(G, gg);
         wins = wins && gg.front() == 0 && gg.back() == G.rows;
+        // the hot-column form (mark_hot_columns): every entry decodes to its column, slots < K, each
+        // window's hot columns ascending, distinct and inside the window, and a hot column's count is
+        // at least every cold column's of the window
+        for (const uint32_t K : {1u, 16u}) {
+          if (!wins) break;
+          WinLayout H = W;
+          std::vector<uint32_t> hot;
+          wins = mark_hot_columns(H, K, hot) && hot.size() == (size_t)(W.winseg.size() - 1) * K;
+          for (uint32_t w = 0; w + 1 < W.winseg.size() && wins; ++w) {
+            const uint32_t e0 = G.rowptr[W.winseg[w]], e1 = G.rowptr[W.winseg[w + 1]];
+            std::vector<uint32_t> cnt(1u << lw, 0);
+            std::vector<char> is_hot(1u << lw, 0);
+            uint32_t nh = 0;
+            for (uint32_t e = e0; e < e1 && wins; ++e) {
+              const uint32_t c = H.seg.colind[e];
+              const uint32_t col = (c & kWcHotFlag) ? hot[(size_t)w * K + (c & ~kWcHotFlag)] : c;
+              wins = col == G.colind[e] && ((c & kWcHotFlag) == 0 || (c & ~kWcHotFlag) < K);
+              cnt[col & ((1u << lw) - 1)]++;
+              if (c & kWcHotFlag) is_hot[col & ((1u << lw) - 1)] = 1;
+            }
+            uint32_t minhot = UINT32_MAX, maxcold = 0;
+            for (uint32_t c = 0; c < (1u << lw); ++c) {
+              if (is_hot[c]) minhot = std::min(minhot, cnt[c]), ++nh;
+              else maxcold = std::max(maxcold, cnt[c]);
+            }
+            wins = wins && (nh == 0 || minhot >= maxcold) && nh <= K;
+            for (uint32_t i = 1; i < nh && wins; ++i)
+              wins = hot[(size_t)w * K + i - 1] < hot[(size_t)w * K + i] && (hot[(size_t)w * K + i] >> lw) == w;
+          }
+        }
       }
       nfail += !(same && tiles && shards && wins);
       std::fprintf(fo, "%-28s csc_to_csr %s, row groups %s, shard groups %s, windowed segments %s\n", cs.name.c_str(),

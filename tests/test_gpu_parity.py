@@ -1020,16 +1020,17 @@ def test_split_eligible_at_four_panels(gpu):
         _check("4 panels", 1500, 14001, colptr, rowind, vals, x, "vcache_split", beta, hs.MODE_FAST)
 
 
-def test_graph_capture_after_eager_launch_on_another_stream(gpu):
-    # A scratch kernel (vcache_split: tickets + partials) launched eagerly on stream A, then captured
+@pytest.mark.parametrize("kernel", ["vcache_split", "wgather_split"])
+def test_graph_capture_after_eager_launch_on_another_stream(gpu, kernel):
+    # A scratch kernel (tickets + partials) launched eagerly on stream A, then captured
     # on a fresh stream B: the library neither waits on nor records its scratch event inside the
     # capture, the replays give the eager bits, and eager launches on A resume after it.
     import torch
-    n = 1 << 16
-    rowptr, colind, vals = hs.gen_stripe_csr(0, n, n, 32)
-    h = hs.Handle.from_csr(rowptr, colind, vals, n, n)
-    h.set_kernel("vcache_split")
-    xd = torch.from_numpy(hs.gen_vector(n, 3)).cuda()
+    n, cols = (1 << 16, 1 << 16) if kernel == "vcache_split" else (1 << 15, (1 << 21) + 7)
+    rowptr, colind, vals = hs.gen_stripe_csr(0, n, cols, 32)
+    h = hs.Handle.from_csr(rowptr, colind, vals, n, cols)
+    h.set_kernel(kernel)
+    xd = torch.from_numpy(hs.gen_vector(cols, 3)).cuda()
     ya, yb = (torch.empty(n, dtype=torch.float64, device="cuda") for _ in range(2))
     sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
     h.exec_device(xd, ya, beta=0, mode=hs.MODE_FAST, stream=sa)
