@@ -776,7 +776,10 @@ static int finish_create(hipspmv_t* h, HostCSR& a) {
   const bool split_ok = vcache_eligible(a, kVcSplit), quad_ok = vcache_eligible(a, kVcQuad);
   h->wg_eligible = vcache_eligible(a, kWgWindow);
   if (h->wg_eligible) h->wg_max_run = vcache_max_run(a, (uint32_t)kWgWindow.panel);
-  h->wgs_eligible = h->wg_eligible && a.rows <= 128u * (uint32_t)kWgSplit.rows && vcache_eligible(a, kWgSplit);
+  // (probe HIPSPMV_WGS_MAXROWS: another row cap for the two-part form, for its A/B on larger shards)
+  uint64_t wgs_cap = 128ull * (uint32_t)kWgSplit.rows;
+  if (const char* e = std::getenv("HIPSPMV_WGS_MAXROWS")) wgs_cap = std::strtoull(e, nullptr, 10);
+  h->wgs_eligible = h->wg_eligible && a.rows <= wgs_cap && vcache_eligible(a, kWgSplit);
   if (a.cols >= kWcMinCols) h->wc_segments = windowed_segments(a, kWcLog2Window);
   h->setup_scan_ns = now_ns() - t0;
   t0 = now_ns();

@@ -53,6 +53,8 @@ for s in ${STEPS:-streams}; do
             HIPSPMV_EXPERIMENTAL=1 HIPSPMV_WCSR_HOT=8192 step c5_hot_8k 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set one --shards 0,3,7 ;;
     ldsab) step c5_lds_off 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set one --shards 0,3,7 &&
            HIPSPMV_WCSR_LDS=1 step c5_lds_on 600 python -u spmv-vector-cache_amd/tools/c5_ab.py --set one --shards 0,3,7 ;;
+    wgs4) HIPSPMV_WGS_MAXROWS=16777216 step wgs_ab4 600 python -u spmv-vector-cache_amd/tools/wgs_ab.py --parts 4 --shards 0 &&
+          HIPSPMV_WGS_MAXROWS=16777216 step wgs_ab2 600 python -u spmv-vector-cache_amd/tools/wgs_ab.py --parts 2 --shards 0 --rounds 2 --launches 20 ;;
     graph) step pytest_graph 300 $PYT -m gpu tests/test_gpu_parity.py -k "graph_capture" ;;
     dmawait) step dmawait 300 ./spmv-vector-cache_amd/lib/vc_ablate 20 dmawait ;;
     pytest) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;

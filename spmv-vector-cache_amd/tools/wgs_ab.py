@@ -28,11 +28,12 @@ def main():
     p.add_argument("--launches", type=int, default=50)
     p.add_argument("--warm", type=int, default=100)
     p.add_argument("--kernels", default="wgather,wgather_split")
+    p.add_argument("--parts", type=int, default=8, help="shards of the C4 matrix (rows = 2^24 / parts)")
     p.add_argument("--nt", default="", help="wgather_split entry residency sweep: vcache_nt values (first "
                    "non-temporal block), e.g. 0,16,32")
     a = p.parse_args()
     n = 1 << 24
-    rows = n // 8
+    rows = n // a.parts
     x = hs.gen_vector(n, 3)
     xd = torch.from_numpy(x).cuda()
     yd = torch.empty(rows, dtype=torch.float64, device="cuda")
